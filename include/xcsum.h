@@ -1,0 +1,151 @@
+/*
+ * xcsum.h -- C ABI of the MI355X-native UDP checksum engine (libxcsum.so).
+ *
+ * Drop-in boundary for libxudp's per-packet UDP checksum path
+ * (cclinuxer/libxudp xudp/checksum.h, driven from xudp/packet.c and
+ * xudp/tx.c).  Plain pointers and sizes only; every call returns 0 or a
+ * negative XCSUM_ERR_* code (the reference's convention of negative
+ * XUDP_ERR_* codes, include/xudp.h:67-140), never aborts.
+ *
+ * Each entry point names the reference interface it replaces.  The
+ * packet_info-level mirror (xudp_packet_udp & co.) is in xudp_packet.h.
+ *
+ * Threading: one xcsum_ctx per host thread (or per stream); the library keeps
+ * no global mutable state besides the lazily created default context used by
+ * the void-returning packet.c mirrors.  HIP is initialised lazily by
+ * xcsum_ctx_create(), so a process may fork (libxudp's master/worker model,
+ * test/case/lib.c:169) before its first call.
+ */
+#ifndef XCSUM_H
+#define XCSUM_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define XCSUM_ABI_VERSION 1
+
+/* Layout-identical to struct xdp_desc (linux/if_xdp.h), the descriptor xudp
+ * publishes on the AF_XDP TX ring (xudp/tx.c:450-452, include/queue.h:183-184).
+ * addr = offset of the Ethernet frame inside the UMEM buffer, len = frame
+ * length (xudp_packet_udp sets it to payload+42 / payload+62, packet.c:168/190). */
+struct xcsum_desc {
+	uint64_t addr;
+	uint32_t len;
+	uint32_t options;
+};
+
+/* What out[i] is.  In every mode out[i] is the 16-bit value to store into
+ * udp->check (i.e. already in wire byte order). */
+enum xcsum_mode {
+	/* IPv4, xudp/checksum.h:107-140 udp_checksum() bit for bit, including
+	 * its single-fold quirk (checksum.h:100-104); no 0 -> 0xffff mapping. */
+	XCSUM_MODE_V4_LEGACY = 0,
+	/* IPv4, RFC 768/1071 (full fold, 0 -> 0xffff). */
+	XCSUM_MODE_V4_RFC = 1,
+	/* IPv6, xudp/packet.c:105-117 udp_csum6() bit for bit. */
+	XCSUM_MODE_V6 = 2,
+	/* Per frame from eth->h_proto: 0x0800 -> V4_LEGACY (or V4_RFC with
+	 * XCSUM_F_V4_RFC), 0x86DD -> V6, anything else -> out 0 + error. */
+	XCSUM_MODE_AUTO = 3,
+};
+
+/* Flags (bitwise OR). */
+#define XCSUM_F_INPLACE  0x1u /* also store out[i] into udp->check in the frame */
+#define XCSUM_F_IPHDR    0x2u /* IPv4 frames: also compute and store iph->check
+				 (== xudp_checksum_half, packet.c:43-66) */
+#define XCSUM_F_V4_RFC   0x4u /* AUTO mode: IPv4 frames use V4_RFC */
+#define XCSUM_F_ZEROCOPY 0x8u /* host batches: kernel reads the registered UMEM
+				 through its device mapping instead of copying */
+
+/* Error codes (returned negated). */
+enum {
+	XCSUM_ERR_INVAL = 9000,  /* bad argument */
+	XCSUM_ERR_HIP,           /* a HIP runtime call failed */
+	XCSUM_ERR_NODEV,         /* no such device / no GPU */
+	XCSUM_ERR_NOMEM,         /* device or pinned allocation failed */
+	XCSUM_ERR_NOT_REGISTERED,/* zero-copy asked for an unregistered UMEM */
+	XCSUM_ERR_FRAME,         /* >=1 frame was malformed (too short, jumbo > 65535
+				    UDP bytes, unknown h_proto): its out[i] is 0 */
+};
+
+/* Frame layout facts the kernel relies on (those of every frame xudp builds,
+ * packet.c:19-21, :99): IPv4 has ihl == 5, IPv6 has nexthdr == UDP (no
+ * extension headers); udp_len = len - 34 (IPv4) / len - 54 (IPv6); the check
+ * field is 0 on entry (udp_build, packet.c:125) -- a nonzero field is summed
+ * like any other byte, which is exactly a receive-side verify. */
+
+typedef struct xcsum_ctx xcsum_ctx;
+
+/* Create a context bound to HIP device `device` (-1: $XCSUM_DEVICE or 0). */
+int xcsum_ctx_create(int device, xcsum_ctx **out);
+void xcsum_ctx_destroy(xcsum_ctx *ctx);
+int xcsum_ctx_device(const xcsum_ctx *ctx);
+/* Number of malformed frames seen by this context since the last call
+ * (device-side counter; synchronises the context's device). */
+int xcsum_ctx_take_errors(xcsum_ctx *ctx, uint64_t *count);
+
+/* Force the kernel geometry used by this context's launches (tuning and
+ * tests): G lanes per frame (8/16/32/64), U frames in flight per segment,
+ * K chunks preloaded per lane.  G = 0 restores the automatic choice (from
+ * len_hint).  Results never depend on the geometry.  -XCSUM_ERR_INVAL if the
+ * combination is not compiled in. */
+int xcsum_ctx_set_geometry(xcsum_ctx *ctx, int G, int U, int K);
+
+/* ---- device-resident batch ------------------------------------------------
+ * Replaces the per-frame checksum work of the xudp_frame_send loop
+ * (xudp/tx.c:696-726 -> __xudp_frame_send -> xudp_packet_udp, packet.c:156)
+ * for a whole batch: one launch, asynchronous on `stream` (a hipStream_t;
+ * NULL = the default stream).  d_umem, d_desc and d_out are device pointers
+ * (d_out may be NULL with XCSUM_F_INPLACE).  len_hint = typical frame length
+ * in bytes (0 = unknown); it only picks the kernel geometry, never results. */
+int xcsum_batch_device(xcsum_ctx *ctx, uint8_t *d_umem, const struct xcsum_desc *d_desc,
+		       uint32_t n, uint16_t *d_out, uint32_t mode, uint32_t flags,
+		       uint32_t len_hint, void *stream);
+
+/* ---- host-resident batch (frames in the AF_XDP UMEM) ----------------------
+ * Same semantics with host pointers.  Synchronous.  Frames are moved with
+ * chunked, double-buffered hipMemcpyAsync (pinned when the UMEM range is
+ * registered) -> kernel -> the 2-byte results back; with XCSUM_F_INPLACE the
+ * results are also written into the host frames' udp->check (and iph->check
+ * with XCSUM_F_IPHDR).  With XCSUM_F_ZEROCOPY and a registered UMEM the
+ * kernel reads the frames in place over PCIe instead. */
+int xcsum_batch_host(xcsum_ctx *ctx, uint8_t *h_umem, const struct xcsum_desc *h_desc,
+		     uint32_t n, uint16_t *h_out, uint32_t mode, uint32_t flags);
+
+/* Page-lock and map a host region (xudp's UMEM, xudp/xsk.c:222-341) for DMA
+ * and zero-copy access.  Ownership stays with the caller. */
+int xcsum_register_umem(xcsum_ctx *ctx, void *base, size_t size);
+int xcsum_unregister_umem(xcsum_ctx *ctx, void *base);
+
+/* Wait for all work the context issued on `stream`. */
+int xcsum_sync(xcsum_ctx *ctx, void *stream);
+
+/* ---- synthetic frames (bench + tests; same bytes on host and device) ------
+ * Frames exactly as xudp_packet_udp() lays them out (packet.c:156-194) with
+ * both check fields 0, random MACs/addresses/ports/payload from a SplitMix64
+ * stream keyed by (seed, first_index + i).  family: 4 or 6.
+ * gen_layout fills descriptors: payload size uniform in [pmin, pmax], frames
+ * packed back to back at `align`-byte boundaries (stride == 0), or one frame
+ * every `stride` bytes at offset `offset` (UMEM-mirror layout). */
+int xcsum_gen_layout(uint32_t n, uint32_t family, uint32_t pmin, uint32_t pmax,
+		     uint64_t seed, uint64_t first_index, uint32_t align,
+		     uint32_t stride, uint32_t offset,
+		     struct xcsum_desc *h_desc, uint64_t *umem_bytes);
+int xcsum_gen_fill_host(uint8_t *h_umem, const struct xcsum_desc *h_desc, uint32_t n,
+			uint32_t family, uint64_t seed, uint64_t first_index);
+int xcsum_gen_fill_device(uint8_t *d_umem, const struct xcsum_desc *d_desc, uint32_t n,
+			  uint32_t family, uint64_t seed, uint64_t first_index, void *stream);
+
+/* Split [0, n) into `nshards` contiguous ranges of near-equal frame bytes
+ * (multi-GPU sharding, one range per GPU); returns shard `idx`'s range. */
+int xcsum_shard_by_bytes(const struct xcsum_desc *h_desc, uint32_t n, uint32_t nshards,
+			 uint32_t idx, uint32_t *first, uint32_t *count);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* XCSUM_H */

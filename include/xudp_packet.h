@@ -1,0 +1,82 @@
+/*
+ * xudp_packet.h -- packet.c-level mirror (drop-in for cclinuxer/libxudp
+ * xudp/packet.h + xudp/packet.c), backed by libxcsum.so.
+ *
+ * struct packet_info is layout-identical to xudp/packet.h:28-53, so libxudp's
+ * tx.c can link against these symbols in place of packet.o.  Header bytes are
+ * written on the host exactly as packet.c does (they are the frame's own
+ * fields, not checksum work); every checksum is computed by the gfx950 kernel.
+ */
+#ifndef XUDP_PACKET_H
+#define XUDP_PACKET_H
+
+#include <stdint.h>
+#include <netinet/in.h>
+#include "xcsum.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* xudp/packet.h:28-53 */
+struct packet_info {
+	uint8_t family;
+	unsigned char *dmac;
+	unsigned char *smac;
+	union {
+		struct sockaddr_in *to;
+		struct sockaddr_in6 *to6;
+	};
+	union {
+		struct sockaddr_in *from;
+		struct sockaddr_in6 *from6;
+	};
+	union {
+		struct sockaddr_in _from;
+		struct sockaddr_in6 _from6;
+	};
+
+	char *head;
+	char *data;
+
+	char *payload;
+	int payload_size;
+
+	char *packet;
+	int len;
+};
+
+/* xudp/packet.h:58-60: 14 + 2 + 40 + 8 */
+#define XUDP_TX_HEADROOM 64
+
+/* Replaces xudp/packet.c:156-194.  Builds eth + IPv4/IPv6 + UDP headers in
+ * front of info->data and fills info->packet / info->len like the reference;
+ * IPv4: iph->check via the kernel, udp->check = 0 (packet.c:125);
+ * IPv6: udp->check = udp_csum6 (packet.c:188) via the kernel.
+ * One-frame batch on the calling thread's default context: correct, but
+ * latency-bound (a launch + PCIe round trip per call); batch with
+ * xudp_packet_udp_batch().  errno = EIO if the device path failed. */
+void xudp_packet_udp(struct packet_info *info);
+
+/* Replaces xudp/packet.c:196-203: data = head + XUDP_TX_HEADROOM, copy the
+ * payload there, then xudp_packet_udp(). */
+void xudp_packet_udp_payload(struct packet_info *info);
+
+/* Batched xudp_packet_udp over n frames (the xudp_frame_send loop,
+ * tx.c:696-726): host header build for all n, then ONE checksum batch for
+ * them all.  ctx NULL = the thread's default context.  flags: XCSUM_F_V4_RFC
+ * fills the IPv4 UDP checksum (RFC) instead of 0, XCSUM_F_ZEROCOPY as in
+ * xcsum_batch_host.  Frames may live anywhere in host memory; if all of them
+ * lie in one registered UMEM the DMA is pinned.  Returns 0 or -XCSUM_ERR_*. */
+int xudp_packet_udp_batch(xcsum_ctx *ctx, struct packet_info *infos, uint32_t n,
+			  uint32_t flags);
+
+/* Header build only (both check fields left 0): the host half of
+ * xudp_packet_udp, exposed for callers that checksum device-resident frames
+ * with xcsum_batch_device(). */
+void xudp_packet_build_headers(struct packet_info *info);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* XUDP_PACKET_H */

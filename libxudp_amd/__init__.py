@@ -1,0 +1,230 @@
+"""libxudp_amd -- MI355X-native UDP checksum engine for cclinuxer/libxudp.
+
+The product is ``libxcsum.so`` (gfx950 HIP kernels + the C ABI declared in
+``include/xcsum.h`` and ``include/xudp_packet.h``).  This module is a thin
+ctypes binding used by the tests, ``bench.py`` and ``__graft_entry__``; C
+callers (libxudp's tx.c) link the shared library directly, see INTEGRATION.md.
+
+Importing never falls back to anything: if the library is missing the import
+raises, and every compute call goes to the GPU kernel or returns an error.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libxcsum.so")
+
+# include/xcsum.h
+MODE_V4_LEGACY = 0
+MODE_V4_RFC = 1
+MODE_V6 = 2
+MODE_AUTO = 3
+
+F_INPLACE = 0x1
+F_IPHDR = 0x2
+F_V4_RFC = 0x4
+F_ZEROCOPY = 0x8
+
+ERR_INVAL = 9000
+ERR_HIP = 9001
+ERR_NODEV = 9002
+ERR_NOMEM = 9003
+ERR_NOT_REGISTERED = 9004
+ERR_FRAME = 9005
+
+ERR_NAMES = {ERR_INVAL: "XCSUM_ERR_INVAL", ERR_HIP: "XCSUM_ERR_HIP",
+             ERR_NODEV: "XCSUM_ERR_NODEV", ERR_NOMEM: "XCSUM_ERR_NOMEM",
+             ERR_NOT_REGISTERED: "XCSUM_ERR_NOT_REGISTERED",
+             ERR_FRAME: "XCSUM_ERR_FRAME"}
+
+# struct xcsum_desc == struct xdp_desc
+DESC_DTYPE = np.dtype([("addr", "<u8"), ("len", "<u4"), ("options", "<u4")])
+
+HDR4 = 42  # eth 14 + ip 20 + udp 8
+HDR6 = 62  # eth 14 + ip6 40 + udp 8
+
+
+class XcsumError(RuntimeError):
+    def __init__(self, rc, what):
+        self.rc = rc
+        super().__init__(f"{what} failed: -{ERR_NAMES.get(-rc, rc)}")
+
+
+_lib = None
+
+_SIGS = {
+    "xcsum_ctx_create": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]),
+    "xcsum_ctx_destroy": (None, [ctypes.c_void_p]),
+    "xcsum_ctx_device": (ctypes.c_int, [ctypes.c_void_p]),
+    "xcsum_ctx_take_errors": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64)]),
+    "xcsum_ctx_set_geometry": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
+                                              ctypes.c_int]),
+    "xcsum_batch_device": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                          ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint32,
+                                          ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p]),
+    "xcsum_batch_host": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                        ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint32,
+                                        ctypes.c_uint32]),
+    "xcsum_register_umem": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t]),
+    "xcsum_unregister_umem": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
+    "xcsum_sync": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
+    "xcsum_gen_layout": (ctypes.c_int, [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
+                                        ctypes.c_uint32, ctypes.c_uint64, ctypes.c_uint64,
+                                        ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
+                                        ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64)]),
+    "xcsum_gen_fill_host": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32,
+                                           ctypes.c_uint32, ctypes.c_uint64, ctypes.c_uint64]),
+    "xcsum_gen_fill_device": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32,
+                                             ctypes.c_uint32, ctypes.c_uint64, ctypes.c_uint64,
+                                             ctypes.c_void_p]),
+    "xcsum_shard_by_bytes": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32,
+                                            ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint32),
+                                            ctypes.POINTER(ctypes.c_uint32)]),
+    "xudp_packet_build_headers": (None, [ctypes.c_void_p]),
+    "xudp_packet_udp": (None, [ctypes.c_void_p]),
+    "xudp_packet_udp_payload": (None, [ctypes.c_void_p]),
+    "xudp_packet_udp_batch": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32,
+                                             ctypes.c_uint32]),
+}
+
+
+def lib():
+    """Load libxcsum.so (raises ImportError if it was not built)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(
+                f"{LIB_PATH} is missing: build it with `make -C libxudp_amd` "
+                "or `python -c 'import __graft_entry__ as g; g.build()'`")
+        L = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in _SIGS.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+def _check(rc, what):
+    if rc != 0:
+        raise XcsumError(rc, what)
+    return rc
+
+
+def _ptr(a):
+    """Raw address of a numpy array, torch tensor, int or None."""
+    if a is None:
+        return None
+    if isinstance(a, int):
+        return a
+    if isinstance(a, np.ndarray):
+        return a.ctypes.data
+    if hasattr(a, "data_ptr"):
+        return a.data_ptr()
+    raise TypeError(type(a))
+
+
+# ---- synthetic frames (host side, no GPU needed) -------------------------
+
+def gen_layout(n, family, pmin, pmax=None, seed=0, first_index=0, align=8, stride=0, offset=0):
+    """Descriptors for n synthetic frames -> (desc ndarray, umem_bytes)."""
+    if pmax is None:
+        pmax = pmin
+    desc = np.zeros(n, dtype=DESC_DTYPE)
+    nbytes = ctypes.c_uint64(0)
+    _check(lib().xcsum_gen_layout(n, family, pmin, pmax, seed, first_index, align, stride,
+                                  offset, _ptr(desc), ctypes.byref(nbytes)), "xcsum_gen_layout")
+    return desc, int(nbytes.value)
+
+
+def gen_fill_host(umem, desc, family, seed=0, first_index=0):
+    _check(lib().xcsum_gen_fill_host(_ptr(umem), _ptr(desc), len(desc), family, seed,
+                                     first_index), "xcsum_gen_fill_host")
+
+
+def gen_frames_host(n, family, pmin, pmax=None, seed=0, first_index=0, align=8, stride=0,
+                    offset=0, pad=64):
+    """Convenience: (umem uint8 ndarray, desc) generated on the host."""
+    desc, nbytes = gen_layout(n, family, pmin, pmax, seed, first_index, align, stride, offset)
+    umem = np.zeros(nbytes + pad, dtype=np.uint8)
+    gen_fill_host(umem, desc, family, seed, first_index)
+    return umem, desc
+
+
+def shard_by_bytes(desc, nshards, idx):
+    first = ctypes.c_uint32(0)
+    count = ctypes.c_uint32(0)
+    _check(lib().xcsum_shard_by_bytes(_ptr(desc), len(desc), nshards, idx, ctypes.byref(first),
+                                      ctypes.byref(count)), "xcsum_shard_by_bytes")
+    return int(first.value), int(count.value)
+
+
+def alg_bytes(desc, family):
+    """Algorithmic bytes of a batch: span read + 2-byte write.
+    span = udp_len + 8 (IPv4 addresses) or + 32 (IPv6)."""
+    ln = desc["len"].astype(np.int64)
+    if family == 6:
+        span = ln - 54 + 32
+    else:
+        span = ln - 34 + 8
+    return int(span.sum()) + 2 * len(desc)
+
+
+# ---- device context --------------------------------------------------------
+
+class Engine:
+    """One xcsum_ctx (one device, one host thread)."""
+
+    def __init__(self, device=-1):
+        self._ctx = ctypes.c_void_p(0)
+        _check(lib().xcsum_ctx_create(device, ctypes.byref(self._ctx)), "xcsum_ctx_create")
+        self.device = lib().xcsum_ctx_device(self._ctx)
+
+    @property
+    def ctx(self):
+        return self._ctx
+
+    def close(self):
+        if self._ctx:
+            lib().xcsum_ctx_destroy(self._ctx)
+            self._ctx = ctypes.c_void_p(0)
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def set_geometry(self, G=0, U=0, K=0):
+        _check(lib().xcsum_ctx_set_geometry(self._ctx, G, U, K), "xcsum_ctx_set_geometry")
+
+    def take_errors(self):
+        c = ctypes.c_uint64(0)
+        _check(lib().xcsum_ctx_take_errors(self._ctx, ctypes.byref(c)), "xcsum_ctx_take_errors")
+        return int(c.value)
+
+    def batch_device(self, d_umem, d_desc, n, d_out, mode, flags=0, len_hint=0, stream=None):
+        """Asynchronous device-resident batch (pointers: torch tensors or ints)."""
+        _check(lib().xcsum_batch_device(self._ctx, _ptr(d_umem), _ptr(d_desc), n, _ptr(d_out),
+                                        mode, flags, len_hint, _ptr(stream)),
+               "xcsum_batch_device")
+
+    def batch_host(self, umem, desc, out, mode, flags=0):
+        _check(lib().xcsum_batch_host(self._ctx, _ptr(umem), _ptr(desc), len(desc), _ptr(out),
+                                      mode, flags), "xcsum_batch_host")
+
+    def register_umem(self, buf):
+        _check(lib().xcsum_register_umem(self._ctx, _ptr(buf), buf.nbytes),
+               "xcsum_register_umem")
+
+    def unregister_umem(self, buf):
+        _check(lib().xcsum_unregister_umem(self._ctx, _ptr(buf)), "xcsum_unregister_umem")
+
+    def sync(self, stream=None):
+        _check(lib().xcsum_sync(self._ctx, _ptr(stream)), "xcsum_sync")
+
+    def gen_fill_device(self, d_umem, d_desc, n, family, seed=0, first_index=0, stream=None):
+        _check(lib().xcsum_gen_fill_device(_ptr(d_umem), _ptr(d_desc), n, family, seed,
+                                           first_index, _ptr(stream)), "xcsum_gen_fill_device")

@@ -1,0 +1,507 @@
+/*
+ * xcsum_api.hip -- host side of libxcsum.so: the C ABI of include/xcsum.h.
+ *
+ * Error behaviour follows the reference (include/xudp.h:67-140): negative
+ * codes, never abort, errno untouched except by the packet.c mirrors.
+ */
+#include <errno.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <new>
+
+#include "xcsum_internal.h"
+#include "xcsum_gen.h"
+
+using namespace xcsum;
+
+#define HIPCHK(x)                                   \
+	do {                                        \
+		if ((x) != hipSuccess)              \
+			return -XCSUM_ERR_HIP;      \
+	} while (0)
+
+/* $XCSUM_GEOMETRY="G,U,K" forces a geometry for every new context (sweeps) */
+static Geometry env_geometry()
+{
+	const char *s = getenv("XCSUM_GEOMETRY");
+	int G, U, K;
+	if (s && sscanf(s, "%d,%d,%d", &G, &U, &K) == 3 && geometry_supported(Geometry{G, U, K}))
+		return Geometry{G, U, K};
+	return Geometry{0, 0, 0};
+}
+
+extern "C" int xcsum_ctx_create(int device, xcsum_ctx **out)
+{
+	int count = 0;
+	if (!out)
+		return -XCSUM_ERR_INVAL;
+	*out = nullptr;
+	if (device < 0) {
+		const char *e = getenv("XCSUM_DEVICE");
+		device = e ? atoi(e) : 0;
+	}
+	if (hipGetDeviceCount(&count) != hipSuccess || count <= 0)
+		return -XCSUM_ERR_NODEV;
+	if (device >= count)
+		return -XCSUM_ERR_NODEV;
+	HIPCHK(hipSetDevice(device));
+	xcsum_ctx *c = new (std::nothrow) xcsum_ctx();
+	if (!c)
+		return -XCSUM_ERR_NOMEM;
+	c->device = device;
+	hipDeviceProp_t prop;
+	if (hipGetDeviceProperties(&prop, device) != hipSuccess) {
+		delete c;
+		return -XCSUM_ERR_HIP;
+	}
+	c->cus = prop.multiProcessorCount;
+	c->max_blocks = c->cus * 8;
+	c->d_err = nullptr;
+	if (hipMalloc(&c->d_err, sizeof(unsigned long long)) != hipSuccess) {
+		delete c;
+		return -XCSUM_ERR_NOMEM;
+	}
+	(void)hipMemset(c->d_err, 0, sizeof(unsigned long long));
+	for (int s = 0; s < Ctx::NSLOT; s++) {
+		c->streams[s] = nullptr;
+		c->done[s] = nullptr;
+		c->d_frames[s] = nullptr;
+		c->d_desc[s] = nullptr;
+		c->d_out[s] = nullptr;
+		c->h_out[s] = nullptr;
+	}
+	c->frame_cap = 0;
+	c->desc_cap = 0;
+	c->geom = env_geometry();
+	*out = c;
+	return 0;
+}
+
+static void free_staging(xcsum_ctx *c)
+{
+	for (int s = 0; s < Ctx::NSLOT; s++) {
+		if (c->streams[s]) (void)hipStreamDestroy(c->streams[s]);
+		if (c->done[s]) (void)hipEventDestroy(c->done[s]);
+		if (c->d_frames[s]) (void)hipFree(c->d_frames[s]);
+		if (c->d_desc[s]) (void)hipFree(c->d_desc[s]);
+		if (c->d_out[s]) (void)hipFree(c->d_out[s]);
+		if (c->h_out[s]) (void)hipHostFree(c->h_out[s]);
+		c->streams[s] = nullptr;
+		c->done[s] = nullptr;
+		c->d_frames[s] = nullptr;
+		c->d_desc[s] = nullptr;
+		c->d_out[s] = nullptr;
+		c->h_out[s] = nullptr;
+	}
+	c->frame_cap = 0;
+	c->desc_cap = 0;
+}
+
+extern "C" void xcsum_ctx_destroy(xcsum_ctx *c)
+{
+	if (!c)
+		return;
+	(void)hipSetDevice(c->device);
+	(void)hipDeviceSynchronize();
+	free_staging(c);
+	for (auto &r : c->regions)
+		(void)hipHostUnregister(r.host);
+	if (c->d_err)
+		(void)hipFree(c->d_err);
+	delete c;
+}
+
+extern "C" int xcsum_ctx_device(const xcsum_ctx *c)
+{
+	return c ? c->device : -XCSUM_ERR_INVAL;
+}
+
+extern "C" int xcsum_ctx_take_errors(xcsum_ctx *c, uint64_t *count)
+{
+	unsigned long long v = 0;
+	if (!c || !count)
+		return -XCSUM_ERR_INVAL;
+	HIPCHK(hipSetDevice(c->device));
+	HIPCHK(hipDeviceSynchronize());
+	HIPCHK(hipMemcpy(&v, c->d_err, sizeof(v), hipMemcpyDeviceToHost));
+	HIPCHK(hipMemset(c->d_err, 0, sizeof(v)));
+	*count = v;
+	return 0;
+}
+
+static Geometry geometry_for(const xcsum_ctx *c, uint32_t len_hint)
+{
+	return c->geom.G ? c->geom : pick_geometry(len_hint);
+}
+
+extern "C" int xcsum_ctx_set_geometry(xcsum_ctx *c, int G, int U, int K)
+{
+	if (!c)
+		return -XCSUM_ERR_INVAL;
+	if (G == 0) {
+		c->geom = Geometry{0, 0, 0};
+		return 0;
+	}
+	if (!geometry_supported(Geometry{G, U, K}))
+		return -XCSUM_ERR_INVAL;
+	c->geom = Geometry{G, U, K};
+	return 0;
+}
+
+extern "C" int xcsum_batch_device(xcsum_ctx *c, uint8_t *d_umem, const struct xcsum_desc *d_desc,
+				  uint32_t n, uint16_t *d_out, uint32_t mode, uint32_t flags,
+				  uint32_t len_hint, void *stream)
+{
+	if (!c || mode > XCSUM_MODE_AUTO)
+		return -XCSUM_ERR_INVAL;
+	if (n == 0)
+		return 0;
+	if (!d_umem || !d_desc || (!d_out && !(flags & XCSUM_F_INPLACE)))
+		return -XCSUM_ERR_INVAL;
+	HIPCHK(hipSetDevice(c->device));
+	CsumArgs a;
+	a.umem = d_umem;
+	a.desc = d_desc;
+	a.n = n;
+	a.out = d_out;
+	a.out_ip = nullptr;
+	a.mode = mode;
+	a.flags = flags & (XCSUM_F_INPLACE | XCSUM_F_IPHDR | XCSUM_F_V4_RFC);
+	a.bias = 0;
+	a.err = c->d_err;
+	HIPCHK(launch_csum(a, geometry_for(c, len_hint), c->max_blocks, (hipStream_t)stream));
+	return 0;
+}
+
+extern "C" int xcsum_sync(xcsum_ctx *c, void *stream)
+{
+	if (!c)
+		return -XCSUM_ERR_INVAL;
+	HIPCHK(hipSetDevice(c->device));
+	HIPCHK(hipStreamSynchronize((hipStream_t)stream));
+	return 0;
+}
+
+/* ---- UMEM registration --------------------------------------------------- */
+
+extern "C" int xcsum_register_umem(xcsum_ctx *c, void *base, size_t size)
+{
+	void *dev = nullptr;
+	if (!c || !base || !size)
+		return -XCSUM_ERR_INVAL;
+	HIPCHK(hipSetDevice(c->device));
+	if (hipHostRegister(base, size, hipHostRegisterMapped) != hipSuccess)
+		return -XCSUM_ERR_HIP;
+	if (hipHostGetDevicePointer(&dev, base, 0) != hipSuccess) {
+		(void)hipHostUnregister(base);
+		return -XCSUM_ERR_HIP;
+	}
+	c->regions.push_back(Region{(uint8_t *)base, size, (uint8_t *)dev});
+	return 0;
+}
+
+extern "C" int xcsum_unregister_umem(xcsum_ctx *c, void *base)
+{
+	if (!c || !base)
+		return -XCSUM_ERR_INVAL;
+	for (size_t i = 0; i < c->regions.size(); i++) {
+		if (c->regions[i].host == (uint8_t *)base) {
+			HIPCHK(hipSetDevice(c->device));
+			(void)hipHostUnregister(base);
+			c->regions.erase(c->regions.begin() + i);
+			return 0;
+		}
+	}
+	return -XCSUM_ERR_NOT_REGISTERED;
+}
+
+static const Region *find_region(const xcsum_ctx *c, const uint8_t *lo, const uint8_t *hi)
+{
+	for (auto &r : c->regions)
+		if (lo >= r.host && hi <= r.host + r.size)
+			return &r;
+	return nullptr;
+}
+
+/* ---- host-resident batches ----------------------------------------------- */
+
+static int ensure_staging(xcsum_ctx *c)
+{
+	if (c->frame_cap)
+		return 0;
+	const size_t frame_cap = 32u << 20;   /* bytes of UMEM per chunk */
+	const uint32_t desc_cap = 1u << 16;   /* frames per chunk */
+	for (int s = 0; s < Ctx::NSLOT; s++) {
+		if (hipStreamCreateWithFlags(&c->streams[s], hipStreamNonBlocking) != hipSuccess ||
+		    hipEventCreateWithFlags(&c->done[s], hipEventDisableTiming) != hipSuccess ||
+		    hipMalloc(&c->d_frames[s], frame_cap + 64) != hipSuccess ||
+		    hipMalloc(&c->d_desc[s], desc_cap * sizeof(struct xcsum_desc)) != hipSuccess ||
+		    hipMalloc(&c->d_out[s], 2 * desc_cap * sizeof(uint16_t)) != hipSuccess ||
+		    hipHostMalloc(&c->h_out[s], 2 * desc_cap * sizeof(uint16_t), 0) != hipSuccess) {
+			free_staging(c);
+			return -XCSUM_ERR_NOMEM;
+		}
+	}
+	c->frame_cap = frame_cap;
+	c->desc_cap = desc_cap;
+	return 0;
+}
+
+/* udp->check / iph->check offsets of a frame for the resolved family */
+static int host_family(const uint8_t *eth, uint32_t mode)
+{
+	if (mode == XCSUM_MODE_V6)
+		return 6;
+	if (mode != XCSUM_MODE_AUTO)
+		return 4;
+	uint32_t proto = ((uint32_t)eth[12] << 8) | eth[13];
+	return proto == 0x86DDu ? 6 : (proto == 0x0800u ? 4 : 0);
+}
+
+struct Pending {
+	uint32_t first, count;
+	bool busy;
+};
+
+/* results of one finished chunk -> caller arrays / host frames */
+static void retire(const Pending &pd, const uint16_t *h_res, uint8_t *h_umem,
+		   const struct xcsum_desc *h_desc, uint16_t *h_out, uint16_t *h_out_ip,
+		   uint32_t mode, uint32_t flags)
+{
+	const uint16_t *res = h_res, *res_ip = h_res + pd.count;
+	if (h_out)
+		memcpy(h_out + pd.first, res, pd.count * sizeof(uint16_t));
+	if (h_out_ip)
+		memcpy(h_out_ip + pd.first, res_ip, pd.count * sizeof(uint16_t));
+	if (flags & XCSUM_F_INPLACE) {
+		for (uint32_t i = 0; i < pd.count; i++) {
+			const struct xcsum_desc &d = h_desc[pd.first + i];
+			uint8_t *eth = h_umem + d.addr;
+			int fam = host_family(eth, mode);
+			if (fam == 6) {
+				memcpy(eth + 60, &res[i], 2);
+			} else if (fam == 4) {
+				memcpy(eth + 40, &res[i], 2);
+				if (flags & XCSUM_F_IPHDR)
+					memcpy(eth + 24, &res_ip[i], 2);
+			}
+		}
+	}
+}
+
+namespace xcsum {
+
+int batch_host_impl(xcsum_ctx *c, uint8_t *h_umem, const struct xcsum_desc *h_desc, uint32_t n,
+		    uint16_t *h_out, uint16_t *h_out_ip, uint32_t mode, uint32_t flags)
+{
+	if (!c || mode > XCSUM_MODE_AUTO)
+		return -XCSUM_ERR_INVAL;
+	if (n == 0)
+		return 0;
+	if (!h_desc || (!h_out && !h_out_ip && !(flags & XCSUM_F_INPLACE)))
+		return -XCSUM_ERR_INVAL;
+	HIPCHK(hipSetDevice(c->device));
+	int rc = ensure_staging(c);
+	if (rc)
+		return rc;
+	const bool want_ip = (flags & XCSUM_F_IPHDR) != 0;
+
+	/* zero-copy: the kernel reads frames where they are (registered UMEM) */
+	const Region *zc = nullptr;
+	if (flags & XCSUM_F_ZEROCOPY) {
+		uint64_t lo = UINT64_MAX, hi = 0;
+		for (uint32_t i = 0; i < n; i++) {
+			if (h_desc[i].addr < lo) lo = h_desc[i].addr;
+			if (h_desc[i].addr + h_desc[i].len > hi) hi = h_desc[i].addr + h_desc[i].len;
+		}
+		zc = find_region(c, h_umem + lo, h_umem + hi);
+		if (!zc)
+			return -XCSUM_ERR_NOT_REGISTERED;
+	}
+
+	/* zero-copy + INPLACE: the kernel already wrote the host frames */
+	const uint32_t rflags = zc ? (flags & ~XCSUM_F_INPLACE) : flags;
+	Pending pend[Ctx::NSLOT];
+	for (int s = 0; s < Ctx::NSLOT; s++)
+		pend[s].busy = false;
+
+	uint32_t i = 0;
+	int slot = 0;
+	while (i < n) {
+		/* grow a chunk: <= desc_cap frames, UMEM range <= frame_cap */
+		uint64_t lo = h_desc[i].addr, hi = h_desc[i].addr + h_desc[i].len;
+		if (!zc && hi - lo > c->frame_cap)
+			return -XCSUM_ERR_INVAL;
+		uint32_t cnt = 1;
+		while (i + cnt < n && cnt < c->desc_cap) {
+			const struct xcsum_desc &d = h_desc[i + cnt];
+			uint64_t nlo = d.addr < lo ? d.addr : lo;
+			uint64_t nhi = d.addr + d.len > hi ? d.addr + d.len : hi;
+			if (!zc && nhi - nlo > c->frame_cap)
+				break;
+			lo = nlo;
+			hi = nhi;
+			cnt++;
+		}
+		if (pend[slot].busy) {
+			HIPCHK(hipEventSynchronize(c->done[slot]));
+			retire(pend[slot], c->h_out[slot], h_umem, h_desc, h_out, h_out_ip, mode, rflags);
+			pend[slot].busy = false;
+		}
+		hipStream_t st = c->streams[slot];
+		CsumArgs a;
+		a.desc = c->d_desc[slot];
+		a.n = cnt;
+		a.out = c->d_out[slot];
+		a.out_ip = want_ip ? c->d_out[slot] + cnt : nullptr;
+		a.mode = mode;
+		a.err = c->d_err;
+		if (zc) {
+			a.umem = zc->dev + (h_umem - zc->host);
+			a.bias = 0;
+			a.flags = flags & (XCSUM_F_INPLACE | XCSUM_F_IPHDR | XCSUM_F_V4_RFC);
+		} else {
+			/* 16-byte aligned copy of [lo, hi) keeps every frame's address
+			 * parity and 16-byte phase identical to the host UMEM */
+			uint64_t alo = lo & ~(uint64_t)15;
+			HIPCHK(hipMemcpyAsync(c->d_frames[slot], h_umem + alo, hi - alo,
+					      hipMemcpyHostToDevice, st));
+			a.umem = c->d_frames[slot];
+			a.bias = alo;
+			a.flags = flags & (XCSUM_F_IPHDR | XCSUM_F_V4_RFC); /* device copy is scratch */
+		}
+		HIPCHK(hipMemcpyAsync(c->d_desc[slot], h_desc + i, cnt * sizeof(struct xcsum_desc),
+				      hipMemcpyHostToDevice, st));
+		uint32_t avg = (uint32_t)((hi - lo) / cnt);
+		HIPCHK(launch_csum(a, geometry_for(c, avg), c->max_blocks, st));
+		HIPCHK(hipMemcpyAsync(c->h_out[slot], c->d_out[slot],
+				      (want_ip ? 2 : 1) * cnt * sizeof(uint16_t),
+				      hipMemcpyDeviceToHost, st));
+		HIPCHK(hipEventRecord(c->done[slot], st));
+		pend[slot].first = i;
+		pend[slot].count = cnt;
+		pend[slot].busy = true;
+		i += cnt;
+		slot = (slot + 1) % Ctx::NSLOT;
+	}
+	for (int k = 0; k < Ctx::NSLOT; k++) {
+		int s = (slot + k) % Ctx::NSLOT;
+		if (pend[s].busy) {
+			HIPCHK(hipEventSynchronize(c->done[s]));
+			retire(pend[s], c->h_out[s], h_umem, h_desc, h_out, h_out_ip, mode, rflags);
+			pend[s].busy = false;
+		}
+	}
+	return 0;
+}
+
+} /* namespace xcsum */
+
+extern "C" int xcsum_batch_host(xcsum_ctx *c, uint8_t *h_umem, const struct xcsum_desc *h_desc,
+				uint32_t n, uint16_t *h_out, uint32_t mode, uint32_t flags)
+{
+	return batch_host_impl(c, h_umem, h_desc, n, h_out, nullptr, mode, flags);
+}
+
+/* ---- synthetic frames ---------------------------------------------------- */
+
+extern "C" int xcsum_gen_layout(uint32_t n, uint32_t family, uint32_t pmin, uint32_t pmax,
+				uint64_t seed, uint64_t first_index, uint32_t align,
+				uint32_t stride, uint32_t offset, struct xcsum_desc *h_desc,
+				uint64_t *umem_bytes)
+{
+	if ((family != 4 && family != 6) || pmin > pmax || (n && !h_desc) || !umem_bytes)
+		return -XCSUM_ERR_INVAL;
+	const uint32_t hdr = family == 6 ? XG_HDR6 : XG_HDR4;
+	if ((uint64_t)pmax + hdr > 0xffffffffull)
+		return -XCSUM_ERR_INVAL;
+	if (align == 0)
+		align = 8;
+	uint64_t off = 0;
+	for (uint32_t i = 0; i < n; i++) {
+		uint32_t len = hdr + xg_payload_size(seed, first_index + i, pmin, pmax);
+		if (stride) {
+			if ((uint64_t)offset + len > stride)
+				return -XCSUM_ERR_INVAL;
+			h_desc[i].addr = (uint64_t)i * stride + offset;
+		} else {
+			h_desc[i].addr = off;
+			off = (off + len + align - 1) / align * align;
+		}
+		h_desc[i].len = len;
+		h_desc[i].options = 0;
+	}
+	*umem_bytes = stride ? (uint64_t)n * stride : off;
+	return 0;
+}
+
+extern "C" int xcsum_gen_fill_host(uint8_t *h_umem, const struct xcsum_desc *h_desc, uint32_t n,
+				   uint32_t family, uint64_t seed, uint64_t first_index)
+{
+	if ((family != 4 && family != 6) || (n && (!h_umem || !h_desc)))
+		return -XCSUM_ERR_INVAL;
+	const uint32_t hdr = family == 6 ? XG_HDR6 : XG_HDR4;
+	for (uint32_t i = 0; i < n; i++) {
+		uint8_t *eth = h_umem + h_desc[i].addr;
+		uint32_t len = h_desc[i].len;
+		uint64_t key = xg_key(seed, first_index + i);
+		if (len < hdr)
+			return -XCSUM_ERR_INVAL;
+		for (uint32_t o = 0; o < hdr; o++)
+			eth[o] = xg_header_byte(family, key, len, o);
+		uint8_t *pl = eth + hdr;
+		uint32_t plen = len - hdr;
+		for (uint32_t q = 0; q < plen; q += 8) {
+			uint64_t w = xg_payload_word(key, q >> 3);
+			uint32_t k = plen - q < 8 ? plen - q : 8;
+			memcpy(pl + q, &w, k); /* little-endian host: byte i = bits 8i.. */
+		}
+	}
+	return 0;
+}
+
+extern "C" int xcsum_gen_fill_device(uint8_t *d_umem, const struct xcsum_desc *d_desc, uint32_t n,
+				     uint32_t family, uint64_t seed, uint64_t first_index,
+				     void *stream)
+{
+	if ((family != 4 && family != 6) || (n && (!d_umem || !d_desc)))
+		return -XCSUM_ERR_INVAL;
+	int dev = 0, cus = 256;
+	HIPCHK(hipGetDevice(&dev));
+	(void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+	HIPCHK(launch_gen(d_umem, d_desc, n, family, seed, first_index, cus * 8,
+			  (hipStream_t)stream));
+	return 0;
+}
+
+extern "C" int xcsum_shard_by_bytes(const struct xcsum_desc *h_desc, uint32_t n, uint32_t nshards,
+				    uint32_t idx, uint32_t *first, uint32_t *count)
+{
+	if (!first || !count || nshards == 0 || idx >= nshards || (n && !h_desc))
+		return -XCSUM_ERR_INVAL;
+	uint64_t total = 0;
+	for (uint32_t i = 0; i < n; i++)
+		total += h_desc[i].len;
+	/* shard k = frames whose starting cumulative byte lies in
+	 * [k*total/nshards, (k+1)*total/nshards) */
+	uint64_t lo_b = total * idx / nshards, hi_b = total * (idx + 1) / nshards;
+	uint64_t cum = 0;
+	uint32_t f = n, e = n;
+	for (uint32_t i = 0; i < n; i++) {
+		if (f == n && cum >= lo_b)
+			f = i;
+		if (cum >= hi_b) {
+			e = i;
+			break;
+		}
+		cum += h_desc[i].len;
+	}
+	if (f > e)
+		f = e;
+	if (idx + 1 == nshards)
+		e = n;
+	*first = f;
+	*count = e - f;
+	return 0;
+}

@@ -1,0 +1,72 @@
+/* xcsum_internal.h -- shared between the kernel TU and the host API TU. */
+#ifndef XCSUM_INTERNAL_H
+#define XCSUM_INTERNAL_H
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <vector>
+#include "xcsum.h"
+
+namespace xcsum {
+
+/* Kernel arguments (passed by value). */
+struct CsumArgs {
+	uint8_t *umem;                 /* frame i starts at umem + desc[i].addr - bias */
+	const struct xcsum_desc *desc;
+	uint32_t n;
+	uint16_t *out;                 /* may be null (INPLACE only) */
+	uint16_t *out_ip;              /* IPHDR: iph->check per frame (may be null) */
+	uint32_t mode;
+	uint32_t flags;
+	uint64_t bias;
+	unsigned long long *err;       /* device counter of malformed frames */
+};
+
+/* Kernel geometry: G lanes cooperate on one frame, each segment keeps U frames
+ * in flight, and each lane preloads K 16-byte chunks per frame. */
+struct Geometry {
+	int G, U, K;
+};
+
+Geometry pick_geometry(uint32_t len_hint);
+int batch_host_impl(struct xcsum_ctx *c, uint8_t *h_umem, const struct xcsum_desc *h_desc,
+		    uint32_t n, uint16_t *h_out, uint16_t *h_out_ip, uint32_t mode, uint32_t flags);
+bool geometry_supported(Geometry g);
+hipError_t launch_csum(const CsumArgs &a, Geometry g, int max_blocks, hipStream_t s);
+hipError_t launch_gen(uint8_t *d_umem, const struct xcsum_desc *d_desc, uint32_t n,
+		      uint32_t family, uint64_t seed, uint64_t first_index, int max_blocks,
+		      hipStream_t s);
+
+struct Region {
+	uint8_t *host;
+	size_t size;
+	uint8_t *dev;  /* device alias of the page-locked mapping */
+};
+
+/* Per-thread context.  Owns only scratch: the error counter and the staging
+ * ring of the host-resident path. */
+struct Ctx {
+	int device;
+	int cus;
+	int max_blocks;
+	Geometry geom;                 /* forced geometry, G == 0: automatic */
+	unsigned long long *d_err;
+	std::vector<Region> regions;
+
+	/* host path staging: NSLOT slots of frames + descriptors + results */
+	static const int NSLOT = 2;
+	hipStream_t streams[NSLOT];
+	hipEvent_t done[NSLOT];
+	uint8_t *d_frames[NSLOT];
+	struct xcsum_desc *d_desc[NSLOT];
+	uint16_t *d_out[NSLOT];
+	uint16_t *h_out[NSLOT];        /* pinned */
+	size_t frame_cap;              /* bytes per slot */
+	uint32_t desc_cap;             /* frames per slot */
+};
+
+} /* namespace xcsum */
+
+struct xcsum_ctx : xcsum::Ctx {};
+
+#endif

@@ -1,0 +1,376 @@
+/*
+ * xcsum_kernels.hip -- gfx950 (CDNA4) kernels of the UDP checksum engine.
+ *
+ * What is computed (reference: cclinuxer/libxudp xudp/checksum.h and
+ * xudp/packet.c).  Every frame xudp builds has no IP options / no IPv6
+ * extension headers (packet.c:19-21, :99), so a frame's whole checksum input
+ * is ONE contiguous span: the pseudo-header addresses sit right before the
+ * UDP header.
+ *     IPv4: span = [eth+26, eth+len)   (saddr, daddr, UDP header, payload)
+ *     IPv6: span = [eth+22, eth+len)   (saddr, daddr, UDP header, payload)
+ * Let S be the EXACT integer sum of the span's big-endian 16-bit words (odd
+ * tail byte padded as a high byte) plus 17 + (udp_len >> 16) + (udp_len &
+ * 0xffff).  S < 2^32 for udp_len <= 65535 and, being an exact integer sum, it
+ * is independent of reduction order.  Then
+ *     V4_LEGACY (checksum.h:100-104 udp_checksum): r = ~(u16)((S&0xffff)+(S>>16))
+ *     V4_RFC / V6 (packet.c:105-117 udp_csum6):   r = ~fold(fold(S)), 0 -> 0xffff
+ * and out = htons(r), the value stored into udp->check.  The legacy quirk
+ * (the dropped end-around carry) is reproduced because S is exact.
+ *
+ * How (memory-bound integer reduction, no MFMA):
+ *   - G lanes own one frame; each lane loads aligned 16-byte chunks
+ *     (global_load_dwordx4, coalesced: the G lanes of a frame read G*16
+ *     consecutive bytes per instruction) and masks the bytes outside the span
+ *     only in the frame's first and last chunk;
+ *   - per lane, two exact u32 sums with v_dot4_u32_u8: E = bytes at even
+ *     addresses, O = bytes at odd addresses (2 VALU per dword);
+ *     lane value = 256*E + O (or 256*O + E when the span starts odd);
+ *   - G-lane butterfly reduction (ds_swizzle/DPP via __shfl_xor), lane 0 of
+ *     the segment finalizes and stores 2 bytes.
+ *   - persistent grid (<= 8 blocks/CU), frames strided over segments; each
+ *     segment keeps U frames' loads in flight (K chunks per lane per frame
+ *     preloaded), the rest of a jumbo frame streams in a tail loop.
+ */
+#include "xcsum_internal.h"
+#include "xcsum_gen.h"
+
+namespace xcsum {
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+static __device__ __forceinline__ uint32_t dot_even(uint32_t w, uint32_t acc)
+{
+	return __builtin_amdgcn_udot4(w, 0x00010001u, acc, false);
+}
+static __device__ __forceinline__ uint32_t dot_odd(uint32_t w, uint32_t acc)
+{
+	return __builtin_amdgcn_udot4(w, 0x01000100u, acc, false);
+}
+
+struct Frame {
+	uint8_t *eth;
+	uintptr_t lo, hi, base; /* span [lo, hi), base = lo & ~15 */
+	uint32_t udp_len;
+	int mode;               /* 0 legacy, 1 rfc, 2 v6, -1 malformed, -2 none */
+};
+
+typedef __attribute__((address_space(1))) const u32x4 gu32x4;
+
+/* 16-byte global load (global_load_dwordx4, not flat: flat ops count on
+ * lgkmcnt too and force full drains) */
+static __device__ __forceinline__ u32x4 load_chunk(uintptr_t addr)
+{
+	return __builtin_nontemporal_load((gu32x4 *)addr);
+}
+
+static __device__ __forceinline__ u32x4 load_desc(const CsumArgs &a, uint32_t p)
+{
+	/* clamped so the load is unconditional; validity is decided by p < n */
+	uint32_t q = p < a.n ? p : a.n - 1;
+	return *((gu32x4 *)(a.desc + q));
+}
+
+static __device__ __forceinline__ Frame resolve(const CsumArgs &a, u32x4 d, bool present)
+{
+	Frame f;
+	uint64_t addr = (((uint64_t)d.y << 32) | d.x) - a.bias;
+	uint32_t len = d.z;
+	int mode = (int)a.mode;
+	f.eth = a.umem + addr;
+	if (!present) {
+		f.mode = -2;
+		f.lo = f.hi = f.base = 0;
+		f.udp_len = 0;
+		return f;
+	}
+	if (mode == XCSUM_MODE_AUTO) {
+		uint32_t proto = ((uint32_t)f.eth[12] << 8) | f.eth[13];
+		mode = proto == 0x0800u ? ((a.flags & XCSUM_F_V4_RFC) ? 1 : 0)
+		     : proto == 0x86DDu ? 2 : -1;
+	}
+	uint32_t hdr = mode == 2 ? 54u : 34u;
+	uint32_t pre = mode == 2 ? 32u : 8u;
+	if (mode < 0 || len < hdr + 8u || len - hdr > 65535u) {
+		mode = -1;
+		len = hdr;
+	}
+	f.mode = mode;
+	f.udp_len = len - hdr;
+	f.lo = (uintptr_t)f.eth + hdr - pre;
+	f.hi = mode < 0 ? f.lo : (uintptr_t)f.eth + len;
+	f.base = f.lo & ~(uintptr_t)15;
+	return f;
+}
+
+static __device__ __forceinline__ uint32_t byte_mask(int lo, int hi)
+{
+	/* bytes [lo, hi) of a dword, lo/hi already clamped to [0, 4] */
+	int n = hi - lo;
+	return n <= 0 ? 0u : ((0xffffffffu >> (32 - 8 * n)) << (8 * lo));
+}
+
+static __device__ __forceinline__ int clamp4(int x) { return x < 0 ? 0 : (x > 4 ? 4 : x); }
+
+/* accumulate one 16-byte chunk at address `a` into E (even bytes), O (odd) */
+static __device__ __forceinline__ void accum(u32x4 v, uintptr_t a, const Frame &f,
+					     uint32_t &E, uint32_t &O)
+{
+	if (a >= f.lo && a + 16 <= f.hi) {
+		E = dot_even(v.x, E); O = dot_odd(v.x, O);
+		E = dot_even(v.y, E); O = dot_odd(v.y, O);
+		E = dot_even(v.z, E); O = dot_odd(v.z, O);
+		E = dot_even(v.w, E); O = dot_odd(v.w, O);
+	} else if (a < f.hi && a + 16 > f.lo) {
+		int lo = a >= f.lo ? 0 : (int)(f.lo - a);
+		int hi = f.hi >= a + 16 ? 16 : (int)(f.hi - a);
+		uint32_t w;
+		w = v.x & byte_mask(clamp4(lo), clamp4(hi));
+		E = dot_even(w, E); O = dot_odd(w, O);
+		w = v.y & byte_mask(clamp4(lo - 4), clamp4(hi - 4));
+		E = dot_even(w, E); O = dot_odd(w, O);
+		w = v.z & byte_mask(clamp4(lo - 8), clamp4(hi - 8));
+		E = dot_even(w, E); O = dot_odd(w, O);
+		w = v.w & byte_mask(clamp4(lo - 12), clamp4(hi - 12));
+		E = dot_even(w, E); O = dot_odd(w, O);
+	}
+}
+
+template <int G>
+static __device__ __forceinline__ uint32_t seg_sum(uint32_t v)
+{
+#pragma unroll
+	for (int m = G / 2; m >= 1; m >>= 1)
+		v += __shfl_xor(v, m, G);
+	return v;
+}
+
+static __device__ __forceinline__ uint16_t bswap16(uint32_t x)
+{
+	return (uint16_t)(((x >> 8) & 0xffu) | ((x & 0xffu) << 8));
+}
+
+static __device__ __forceinline__ void store_u16(uint8_t *p, uint16_t v)
+{
+	if (((uintptr_t)p & 1) == 0) {
+		*reinterpret_cast<uint16_t *>(p) = v;
+	} else {
+		p[0] = (uint8_t)v;
+		p[1] = (uint8_t)(v >> 8);
+	}
+}
+
+/* IPv4 header checksum (RFC 1071 over the 20-byte header, check field as 0);
+ * equals xudp_checksum_half() (packet.c:43-66) on every header iph_build()
+ * writes (ihl is always 5 there, packet.c:21, and the frame-layout contract
+ * of xcsum.h).  Returns the memory-order value for iph->check. */
+static __device__ uint16_t ip_header_csum(const uint8_t *iph)
+{
+	uint32_t sum = 0;
+#pragma unroll
+	for (uint32_t i = 0; i < 20; i += 2)
+		if (i != 10)
+			sum += ((uint32_t)iph[i] << 8) | iph[i + 1];
+	sum = (sum & 0xffffu) + (sum >> 16);
+	sum = (sum & 0xffffu) + (sum >> 16);
+	return bswap16(~sum & 0xffffu);
+}
+
+static __device__ __forceinline__ void finalize(const CsumArgs &a, const Frame &f, uint32_t p,
+						uint32_t s)
+{
+	uint16_t wire = 0;
+	if (f.mode >= 0) {
+		uint32_t S = s + 17u + (f.udp_len >> 16) + (f.udp_len & 0xffffu);
+		uint32_t r;
+		if (f.mode == 0) {
+			/* checksum.h:100-104: one fold, carry dropped by the u16 cast */
+			r = ~((S & 0xffffu) + (S >> 16)) & 0xffffu;
+		} else {
+			uint32_t t = (S & 0xffffu) + (S >> 16);
+			t = (t & 0xffffu) + (t >> 16);
+			r = ~t & 0xffffu;
+			if (r == 0)
+				r = 0xffffu; /* CSUM_MANGLED_0, packet.c:23, :115-116 */
+		}
+		wire = bswap16(r);
+		if (a.flags & XCSUM_F_INPLACE)
+			store_u16(f.eth + (f.mode == 2 ? 60 : 40), wire);
+		if ((a.flags & XCSUM_F_IPHDR) && f.mode != 2) {
+			uint16_t ipc = ip_header_csum(f.eth + 14);
+			if (a.flags & XCSUM_F_INPLACE)
+				store_u16(f.eth + 24, ipc);
+			if (a.out_ip)
+				a.out_ip[p] = ipc;
+		}
+	} else {
+		atomicAdd(a.err, 1ull);
+	}
+	if (a.out)
+		a.out[p] = wire;
+	if (a.out_ip && !((a.flags & XCSUM_F_IPHDR) && f.mode >= 0 && f.mode != 2))
+		a.out_ip[p] = 0;
+}
+
+template <int G, int U, int K>
+__global__ void __launch_bounds__(256) csum_kernel(CsumArgs a)
+{
+	const uint32_t lane = threadIdx.x & (G - 1);
+	uint32_t seg = (blockIdx.x * 256u + threadIdx.x) / G;
+	const uint32_t nseg = gridDim.x * (256u / G);
+	if (G == 64)
+		seg = __builtin_amdgcn_readfirstlane(seg);
+
+	const uint32_t step = nseg * U;
+	u32x4 dcur[U];
+#pragma unroll
+	for (int u = 0; u < U; u++)
+		dcur[u] = load_desc(a, seg + u * nseg);
+
+	for (uint32_t p0 = seg; p0 < a.n; p0 += step) {
+		Frame f[U];
+		u32x4 v[U][K];
+#pragma unroll
+		for (int u = 0; u < U; u++)
+			f[u] = resolve(a, dcur[u], p0 + u * nseg < a.n);
+#pragma unroll
+		for (int u = 0; u < U; u++) {
+#pragma unroll
+			for (int k = 0; k < K; k++) {
+				uintptr_t addr = f[u].base + 16u * (lane + k * G);
+				v[u][k] = addr < f[u].hi ? load_chunk(addr) : u32x4{0, 0, 0, 0};
+			}
+		}
+		/* next iteration's descriptors fly while this one reduces */
+#pragma unroll
+		for (int u = 0; u < U; u++)
+			dcur[u] = load_desc(a, p0 + step + u * nseg);
+#pragma unroll
+		for (int u = 0; u < U; u++) {
+			uint32_t E = 0, O = 0;
+#pragma unroll
+			for (int k = 0; k < K; k++)
+				accum(v[u][k], f[u].base + 16u * (lane + k * G), f[u], E, O);
+			for (uintptr_t addr = f[u].base + 16u * (lane + K * G); addr < f[u].hi;
+			     addr += 16u * G)
+				accum(load_chunk(addr), addr, f[u], E, O);
+			uint32_t s = (f[u].lo & 1) ? (O << 8) + E : (E << 8) + O;
+			s = seg_sum<G>(s);
+			if (lane == 0 && f[u].mode != -2)
+				finalize(a, f[u], p0 + u * nseg, s);
+		}
+	}
+}
+
+Geometry pick_geometry(uint32_t len_hint)
+{
+	if (len_hint == 0 || len_hint >= 768)
+		return Geometry{64, 2, 2};
+	if (len_hint >= 384)
+		return Geometry{32, 2, 2};
+	if (len_hint >= 160)
+		return Geometry{16, 2, 2};
+	return Geometry{8, 4, 1};
+}
+
+template <int G, int U, int K>
+static hipError_t launch_t(const CsumArgs &a, int max_blocks, hipStream_t s)
+{
+	uint64_t segs = ((uint64_t)a.n + U - 1) / U;
+	uint64_t blocks = (segs * G + 255) / 256;
+	if (blocks > (uint64_t)max_blocks)
+		blocks = max_blocks;
+	if (blocks == 0)
+		blocks = 1;
+	hipLaunchKernelGGL((csum_kernel<G, U, K>), dim3((unsigned)blocks), dim3(256), 0, s, a);
+	return hipGetLastError();
+}
+
+#define XCSUM_GEOMETRIES(X) \
+	X(64, 2, 2) X(64, 1, 2) X(64, 4, 2) X(64, 1, 4) X(64, 2, 4) \
+	X(32, 2, 2) X(32, 4, 1) X(16, 2, 2) X(16, 4, 1) X(8, 4, 1) X(8, 2, 1) X(8, 8, 1)
+
+bool geometry_supported(Geometry g)
+{
+#define X(g_, u_, k_) if (g.G == g_ && g.U == u_ && g.K == k_) return true;
+	XCSUM_GEOMETRIES(X)
+#undef X
+	return false;
+}
+
+hipError_t launch_csum(const CsumArgs &a, Geometry g, int max_blocks, hipStream_t s)
+{
+	if (a.n == 0)
+		return hipSuccess;
+#define X(g_, u_, k_) \
+	if (g.G == g_ && g.U == u_ && g.K == k_) return launch_t<g_, u_, k_>(a, max_blocks, s);
+	XCSUM_GEOMETRIES(X)
+#undef X
+	return hipErrorInvalidValue;
+}
+
+/* ---- synthetic frame fill: one wave per frame, dword stores ------------- */
+
+static __device__ uint32_t gen_dword(uint32_t family, uint64_t key, uint32_t len, uint32_t hdr,
+				     long o0)
+{
+	/* 4 frame bytes starting at frame offset o0 (all inside the frame) */
+	if (o0 >= (long)hdr) {
+		uint64_t q = (uint64_t)(o0 - hdr);
+		uint64_t w0 = xg_payload_word(key, q >> 3);
+		uint64_t w1 = ((q + 3) >> 3) != (q >> 3) ? xg_payload_word(key, (q >> 3) + 1) : w0;
+		uint32_t v = 0;
+		for (int k = 0; k < 4; k++) {
+			uint64_t qq = q + k;
+			uint64_t w = (qq >> 3) == (q >> 3) ? w0 : w1;
+			v |= (uint32_t)xg_byte_of(w, (uint32_t)(qq & 7)) << (8 * k);
+		}
+		return v;
+	}
+	uint32_t v = 0;
+	for (int k = 0; k < 4; k++)
+		v |= (uint32_t)xg_frame_byte(family, key, len, (uint32_t)(o0 + k)) << (8 * k);
+	return v;
+}
+
+__global__ void __launch_bounds__(256) gen_kernel(uint8_t *umem, const struct xcsum_desc *desc,
+						  uint32_t n, uint32_t family, uint64_t seed,
+						  uint64_t first)
+{
+	const uint32_t lane = threadIdx.x & 63;
+	const uint32_t nw = gridDim.x * 4;
+	const uint32_t hdr = family == 6 ? XG_HDR6 : XG_HDR4;
+	for (uint32_t p = (blockIdx.x * 256 + threadIdx.x) / 64; p < n; p += nw) {
+		const struct xcsum_desc d = desc[p];
+		uint8_t *eth = umem + d.addr;
+		const uint64_t key = xg_key(seed, first + p);
+		const uintptr_t e = (uintptr_t)eth + d.len;
+		for (uintptr_t w = ((uintptr_t)eth & ~(uintptr_t)3) + 4 * lane; w < e; w += 256) {
+			long o0 = (long)(w - (uintptr_t)eth);
+			if (w >= (uintptr_t)eth && w + 4 <= e) {
+				*reinterpret_cast<uint32_t *>(w) = gen_dword(family, key, d.len, hdr, o0);
+			} else {
+				for (int k = 0; k < 4; k++) {
+					long o = o0 + k;
+					if (o >= 0 && o < (long)d.len)
+						eth[o] = xg_frame_byte(family, key, d.len, (uint32_t)o);
+				}
+			}
+		}
+	}
+}
+
+hipError_t launch_gen(uint8_t *d_umem, const struct xcsum_desc *d_desc, uint32_t n,
+		      uint32_t family, uint64_t seed, uint64_t first_index, int max_blocks,
+		      hipStream_t s)
+{
+	if (n == 0)
+		return hipSuccess;
+	uint64_t blocks = ((uint64_t)n + 3) / 4;
+	if (blocks > (uint64_t)max_blocks)
+		blocks = max_blocks;
+	hipLaunchKernelGGL(gen_kernel, dim3((unsigned)blocks), dim3(256), 0, s, d_umem, d_desc, n,
+			   family, seed, first_index);
+	return hipGetLastError();
+}
+
+} /* namespace xcsum */

@@ -1,0 +1,318 @@
+/*
+ * xcsum_oracle.c -- CPU restatement of libxudp's UDP checksum path.
+ *
+ * TEST INFRASTRUCTURE ONLY.  This file is the parity oracle: only tests/,
+ * __graft_entry__.smoke() and bench.py's cpu_baseline leg may load it, and
+ * only as the checker / the timed CPU baseline.  The product library
+ * (libxudp_amd/libxcsum.so) never links, loads or calls it.
+ *
+ * Each function restates the reference algorithm with the SAME loop shape
+ * (so timing it is a faithful proxy for checksum.h) and cites the reference
+ * file:line it follows (paths relative to cclinuxer/libxudp).
+ *
+ * Parity is pinned two ways (see DESIGN.md "Oracle"):
+ *   - against tests/golden fixtures and digests produced by the reference's
+ *     own checksum.h / packet.c compiled in the build container
+ *     (oracle/_ref, recipe oracle/Makefile, generator tests/golden/make_golden.py);
+ *   - against the reference's known-answer vectors.
+ */
+#include <stdint.h>
+#include <string.h>
+#include <pthread.h>
+#include <time.h>
+
+typedef uint8_t u8;
+typedef uint16_t u16;
+typedef uint32_t u32;
+typedef uint64_t u64;
+
+#define ORC_IPPROTO_UDP 17u
+
+static inline u16 orc_bswap16(u16 x) { return (u16)((x >> 8) | (x << 8)); }
+static inline u32 orc_bswap32(u32 x)
+{
+	return (x >> 24) | ((x >> 8) & 0xff00u) | ((x << 8) & 0xff0000u) | (x << 24);
+}
+
+/* xudp/checksum.h:84-105  checksum(): bytewise big-endian word sum seeded
+ * with `sum`, odd tail byte shifted <<8, then ONE fold truncated to u16
+ * (the end-around carry of that fold is dropped -- the "legacy quirk"). */
+u16 orc_checksum(const u8 *p, u32 num, u32 sum)
+{
+	u32 i;
+
+	if (num % 2 == 1) {
+		--num;
+		sum += (u32)p[num] << 8;
+	}
+	for (i = 0; i < num; i += 2) {
+		sum += (u32)p[i] << 8;
+		sum += p[i + 1];
+	}
+	{
+		u32 l = sum & 0x0000FFFFu;
+		u32 h = sum >> 16;
+		u16 c = (u16)(l + h);
+		return (u16)~c;
+	}
+}
+
+/* xudp/checksum.h:107-140  udp_checksum(): IPv4 pseudo-header (saddr, daddr
+ * as BE words, + IPPROTO_UDP, + size as a BE word) seeded into checksum().
+ * saddr/daddr are passed in network byte order (memory order), exactly as the
+ * reference's __be32 arguments.  Returns the HOST-order u16. */
+u16 orc_udp_checksum(const u8 *u, u32 saddr_be, u32 daddr_be, u16 size)
+{
+	u32 sum = 0;
+	const u8 *p;
+	u8 l[2];
+
+	p = (const u8 *)&saddr_be;
+	sum += (u32)p[0] << 8;
+	sum += p[1];
+	sum += (u32)p[2] << 8;
+	sum += p[3];
+
+	p = (const u8 *)&daddr_be;
+	sum += (u32)p[0] << 8;
+	sum += p[1];
+	sum += (u32)p[2] << 8;
+	sum += p[3];
+
+	sum += ORC_IPPROTO_UDP;
+
+	l[0] = (u8)(size >> 8); /* htons(size) in memory order */
+	l[1] = (u8)size;
+	sum += (u32)l[0] << 8;
+	sum += l[1];
+
+	return orc_checksum(u, size, sum);
+}
+
+/* xudp/checksum.h:142-147  sum32 macro: 32-bit add with end-around carry. */
+static inline u32 orc_sum32(u32 sum, u32 val)
+{
+	u32 carry;
+	sum += val;
+	carry = sum < val;
+	sum += carry;
+	return sum;
+}
+
+static inline u32 orc_load32(const u8 *p) { u32 v; memcpy(&v, p, 4); return v; }
+static inline u16 orc_load16(const u8 *p) { u16 v; memcpy(&v, p, 2); return v; }
+
+/* xudp/checksum.h:149-166  udp6_hdr_csum(): native-endian (little-endian
+ * host) u32 words of both addresses, htonl(size), htonl(IPPROTO_UDP). */
+u32 orc_udp6_hdr_csum(u32 sum, const u8 *saddr16, const u8 *daddr16, u32 size)
+{
+	int i;
+	for (i = 0; i < 4; i++)
+		sum = orc_sum32(sum, orc_load32(saddr16 + 4 * i));
+	for (i = 0; i < 4; i++)
+		sum = orc_sum32(sum, orc_load32(daddr16 + 4 * i));
+	sum = orc_sum32(sum, orc_bswap32(size));
+	sum = orc_sum32(sum, orc_bswap32(ORC_IPPROTO_UDP));
+	return sum;
+}
+
+/* xudp/checksum.h:168-194  do_csum(): native u32 accumulate with carry
+ * (the hot loop, :172-176), fold to 17 bits, + u16 tail, + byte tail
+ * (glibc defines __LITTLE_ENDIAN, so the byte is added unshifted, :186-187). */
+u32 orc_do_csum(const u8 *buf, u32 size)
+{
+	u32 sum = 0;
+
+	while (size >= 4) {
+		sum = orc_sum32(sum, orc_load32(buf));
+		buf += 4;
+		size -= 4;
+	}
+	sum = (sum & 0xffffu) + (sum >> 16);
+	if (size & 2) {
+		sum += orc_load16(buf);
+		buf += 2;
+	}
+	if (size & 1)
+		sum += *buf;
+	return sum;
+}
+
+/* xudp/checksum.h:224-229  csum_fold(): two folds then complement. */
+u16 orc_csum_fold(u32 sum)
+{
+	sum = (sum & 0xffffu) + (sum >> 16);
+	sum = (sum & 0xffffu) + (sum >> 16);
+	return (u16)~sum;
+}
+
+/* xudp/packet.c:105-117  udp_csum6(): do_csum + udp6_hdr_csum + csum_fold,
+ * 0 -> CSUM_MANGLED_0 (0xffff, packet.c:23).  Returns the value the
+ * reference stores raw into udp->check (memory order == wire order). */
+u16 orc_udp_csum6(const u8 *udp, u32 size, const u8 *saddr16, const u8 *daddr16)
+{
+	u32 sum = orc_do_csum(udp, size);
+	u16 c;
+	sum = orc_udp6_hdr_csum(sum, saddr16, daddr16, size);
+	c = orc_csum_fold(sum);
+	if (c == 0)
+		c = 0xffff;
+	return c;
+}
+
+/* xudp/packet.c:43-66  xudp_checksum_half(): IPv4 header checksum from the
+ * constant half-sum (ver/ihl/tos, ttl/proto, DF) + tot_len + addresses, in
+ * native u16 order; fold, fold, complement.  `iph` points at a 20-byte
+ * header built by iph_build (packet.c:68-84).  Returns the raw value stored
+ * into iph->check (memory order). */
+u16 orc_ip_checksum_half(const u8 *iph)
+{
+	/* ntohs(IP_VIT) + ntohs((64<<8)+17) + ntohs(IP_DF) on a little-endian host */
+	u32 sum = (u32)orc_bswap16(0x4500) + orc_bswap16((64 << 8) + 17) + orc_bswap16(0x4000);
+	sum += orc_load16(iph + 2);          /* tot_len (network order, raw) */
+	sum += orc_load16(iph + 12);
+	sum += orc_load16(iph + 14);
+	sum += orc_load16(iph + 16);
+	sum += orc_load16(iph + 18);
+	sum = (sum & 0xFFFFu) + (sum >> 16);
+	sum += sum >> 16;
+	return (u16)~sum;
+}
+
+/* RFC 1071 checksum over the 20-byte IPv4 header (ihl 5, packet.c:21) with
+ * the check field (bytes 10..11) treated as zero.  Equals
+ * xudp_checksum_half() on every header iph_build() produces; used to check
+ * the fused IP-header output. */
+u16 orc_ip_header_rfc(const u8 *iph)
+{
+	u32 i, sum = 0;
+	for (i = 0; i < 20; i += 2) {
+		if (i == 10)
+			continue;
+		sum += ((u32)iph[i] << 8) | iph[i + 1];
+	}
+	while (sum >> 16)
+		sum = (sum & 0xffff) + (sum >> 16);
+	return orc_bswap16((u16)~sum); /* memory order */
+}
+
+/* ------------------------------------------------------------------------ */
+/* Batch driver with the product's semantics (include/xcsum.h):            */
+/*   desc[i] = {addr, len, options} (struct xdp_desc, tx.c:450-452),        */
+/*   addr = Ethernet frame offset in umem, len = frame length               */
+/*   (xudp_packet_udp sets len = payload + 42 / 62, packet.c:168, :190).    */
+/*   out[i] = the u16 to store into udp->check (wire order).                */
+/* ------------------------------------------------------------------------ */
+
+struct orc_desc { u64 addr; u32 len; u32 options; };
+
+enum { ORC_MODE_V4_LEGACY = 0, ORC_MODE_V4_RFC = 1, ORC_MODE_V6 = 2, ORC_MODE_AUTO = 3 };
+#define ORC_FLAG_V4_RFC 0x4u  /* == XCSUM_F_V4_RFC: AUTO mode, IPv4 frames use RFC */
+
+/* RFC 768 IPv4 UDP checksum computed through the reference's own IPv6
+ * machinery (do_csum + sum32 + csum_fold, checksum.h:142-229), with the
+ * IPv4 pseudo-header.  The reference never emits this (IPv4 check is 0,
+ * packet.c:125); it is the optional "V4_RFC" mode. */
+static u16 orc_udp_csum4_rfc(const u8 *udp, u32 size, const u8 *saddr4, const u8 *daddr4)
+{
+	u32 sum = orc_do_csum(udp, size);
+	u16 c;
+	sum = orc_sum32(sum, orc_load32(saddr4));
+	sum = orc_sum32(sum, orc_load32(daddr4));
+	sum = orc_sum32(sum, orc_bswap32(size));
+	sum = orc_sum32(sum, orc_bswap32(ORC_IPPROTO_UDP));
+	c = orc_csum_fold(sum);
+	if (c == 0)
+		c = 0xffff;
+	return c;
+}
+
+static u16 orc_one(const u8 *frame, u32 len, int mode, u32 flags)
+{
+	int fam6;
+	if (mode == ORC_MODE_AUTO) {
+		u16 proto = ((u16)frame[12] << 8) | frame[13];
+		if (proto == 0x0800)
+			mode = (flags & ORC_FLAG_V4_RFC) ? ORC_MODE_V4_RFC : ORC_MODE_V4_LEGACY;
+		else if (proto == 0x86DD)
+			mode = ORC_MODE_V6;
+		else
+			return 0;
+	}
+	fam6 = mode == ORC_MODE_V6;
+	if (len < (fam6 ? 62u : 42u))
+		return 0;
+	if (fam6) {
+		const u8 *ip6 = frame + 14;
+		u32 size = len - 54;
+		if (size > 0xffff) /* payload_len is 16 bits (packet.c:91) */
+			return 0;
+		return orc_udp_csum6(ip6 + 40, size, ip6 + 8, ip6 + 24);
+	} else {
+		const u8 *iph = frame + 14;
+		u32 size = len - 34;
+		u32 s, d;
+		if (size > 0xffff)
+			return 0;
+		if (mode == ORC_MODE_V4_RFC)
+			return orc_udp_csum4_rfc(iph + 20, size, iph + 12, iph + 16);
+		memcpy(&s, iph + 12, 4);
+		memcpy(&d, iph + 16, 4);
+		return orc_bswap16(orc_udp_checksum(iph + 20, s, d, (u16)size));
+	}
+}
+
+void orc_batch(const u8 *umem, const struct orc_desc *desc, u32 n, u16 *out,
+	       int mode, u32 flags)
+{
+	u32 i;
+	for (i = 0; i < n; i++)
+		out[i] = orc_one(umem + desc[i].addr, desc[i].len, mode, flags);
+}
+
+/* Threaded CPU baseline: static packet partition, one pthread per slice.
+ * Returns elapsed wall seconds for `reps` passes (CLOCK_MONOTONIC). */
+struct orc_job { const u8 *umem; const struct orc_desc *desc; u32 n; u16 *out; int mode; u32 flags; int reps; };
+
+static void *orc_worker(void *arg)
+{
+	struct orc_job *j = (struct orc_job *)arg;
+	int r;
+	for (r = 0; r < j->reps; r++)
+		orc_batch(j->umem, j->desc, j->n, j->out, j->mode, j->flags);
+	return 0;
+}
+
+double orc_batch_timed(const u8 *umem, const struct orc_desc *desc, u32 n, u16 *out,
+		       int mode, u32 flags, int nthreads, int reps)
+{
+	struct orc_job jobs[256];
+	pthread_t th[256];
+	struct timespec t0, t1;
+	u32 per, start = 0;
+	int t;
+
+	if (nthreads < 1)
+		nthreads = 1;
+	if (nthreads > 256)
+		nthreads = 256;
+	per = (n + nthreads - 1) / nthreads;
+	for (t = 0; t < nthreads; t++) {
+		u32 cnt = start >= n ? 0 : (n - start < per ? n - start : per);
+		jobs[t].umem = umem; jobs[t].desc = desc + start; jobs[t].n = cnt;
+		jobs[t].out = out + start; jobs[t].mode = mode; jobs[t].flags = flags;
+		jobs[t].reps = reps;
+		start += cnt;
+	}
+	clock_gettime(CLOCK_MONOTONIC, &t0);
+	if (nthreads == 1) {
+		orc_worker(&jobs[0]);
+	} else {
+		for (t = 0; t < nthreads; t++)
+			pthread_create(&th[t], 0, orc_worker, &jobs[t]);
+		for (t = 0; t < nthreads; t++)
+			pthread_join(th[t], 0);
+	}
+	clock_gettime(CLOCK_MONOTONIC, &t1);
+	return (t1.tv_sec - t0.tv_sec) + 1e-9 * (t1.tv_nsec - t0.tv_nsec);
+}

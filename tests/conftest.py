@@ -1,0 +1,52 @@
+import json
+import os
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+GOLDEN = os.path.join(ROOT, "tests", "golden")
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (runs on the GPU box)")
+    config.addinivalue_line("markers", "slow: full-size parity (seconds to minutes)")
+
+
+@pytest.fixture(scope="session")
+def golden():
+    g = np.load(os.path.join(GOLDEN, "fixtures.npz"))
+    return {k: g[k] for k in g.files}
+
+
+@pytest.fixture(scope="session")
+def digests():
+    return json.load(open(os.path.join(GOLDEN, "digests.json")))
+
+
+def golden_desc(g, sel=None):
+    import libxudp_amd as X
+    idx = np.arange(len(g["len"])) if sel is None else sel
+    d = np.zeros(len(idx), dtype=X.DESC_DTYPE)
+    d["addr"] = g["addr"][idx]
+    d["len"] = g["len"][idx]
+    return d
+
+
+@pytest.fixture(scope="session")
+def engine():
+    import libxudp_amd as X
+    e = X.Engine(0)
+    yield e
+    e.close()
+
+
+@pytest.fixture(scope="session")
+def torch_cuda():
+    import torch
+    assert torch.cuda.is_available(), "GPU test on a host without a GPU"
+    return torch

@@ -1,0 +1,188 @@
+"""GPU parity: the gfx950 kernel (through the C ABI) vs the reference.
+
+Expected values come from the reference's own checksum.h / packet.c
+(tests/golden, made by tests/golden/make_golden.py) and, for generated
+inputs, from the oracle restatement (oracle/xcsum_oracle.c), itself pinned
+to the reference by the CPU tests.  Integer work: bit-exact, no tolerance.
+"""
+import numpy as np
+import pytest
+
+import libxudp_amd as X
+import oracle
+from conftest import golden_desc
+
+pytestmark = pytest.mark.gpu
+
+GEOMETRIES = [(64, 2, 2), (64, 1, 2), (64, 4, 2), (64, 1, 4), (64, 2, 4), (32, 2, 2),
+              (32, 4, 1), (16, 2, 2), (16, 4, 1), (8, 4, 1), (8, 2, 1), (8, 8, 1)]
+
+
+def run_device(torch, eng, umem, desc, mode, flags=0, len_hint=0, out=True):
+    dev = torch.device("cuda:0")
+    d_umem = torch.from_numpy(umem).to(dev)
+    d_desc = torch.from_numpy(desc.view(np.uint8)).to(dev)
+    d_out = torch.full((max(len(desc), 1),), 0x5a5a, dtype=torch.int32,
+                       device=dev).to(torch.int16) if out else None
+    s = torch.cuda.current_stream(dev).cuda_stream
+    eng.batch_device(d_umem, d_desc, len(desc), d_out, mode, flags, len_hint, stream=s)
+    torch.cuda.synchronize(dev)
+    res = d_out[:len(desc)].cpu().numpy().view(np.uint16) if out else None
+    return res, d_umem.cpu().numpy()
+
+
+@pytest.mark.parametrize("geom", GEOMETRIES)
+def test_golden_v4_legacy_all_geometries(torch_cuda, engine, golden, geom):
+    sel = np.nonzero(golden["family"] == 4)[0]
+    engine.set_geometry(*geom)
+    try:
+        got, _ = run_device(torch_cuda, engine, golden["umem"], golden_desc(golden, sel),
+                            X.MODE_V4_LEGACY)
+    finally:
+        engine.set_geometry(0)
+    exp = golden["exp_legacy"][sel]
+    assert np.array_equal(got, exp), f"{int((got != exp).sum())} mismatches"
+
+
+@pytest.mark.parametrize("geom", GEOMETRIES)
+def test_golden_v6_all_geometries(torch_cuda, engine, golden, geom):
+    sel = np.nonzero(golden["family"] == 6)[0]
+    engine.set_geometry(*geom)
+    try:
+        got, _ = run_device(torch_cuda, engine, golden["umem"], golden_desc(golden, sel),
+                            X.MODE_V6)
+    finally:
+        engine.set_geometry(0)
+    assert np.array_equal(got, golden["exp_v6"][sel])
+
+
+def test_golden_v4_rfc(torch_cuda, engine, golden):
+    sel = np.nonzero(golden["family"] == 4)[0]
+    got, _ = run_device(torch_cuda, engine, golden["umem"], golden_desc(golden, sel),
+                        X.MODE_V4_RFC)
+    assert np.array_equal(got, golden["exp_rfc"][sel])
+
+
+def test_golden_quirk_cases_present_and_exact(torch_cuda, engine, golden):
+    """Frames where udp_checksum()'s dropped carry makes legacy != RFC."""
+    q = np.nonzero((golden["family"] == 4) & (golden["exp_legacy"] != golden["exp_rfc"]))[0]
+    assert len(q) >= 100
+    got, _ = run_device(torch_cuda, engine, golden["umem"], golden_desc(golden, q),
+                        X.MODE_V4_LEGACY)
+    assert np.array_equal(got, golden["exp_legacy"][q])
+
+
+@pytest.mark.parametrize("len_hint", [0, 100, 200, 500, 1500, 9000])
+def test_golden_auto_mixed_families(torch_cuda, engine, golden, len_hint):
+    fam = golden["family"]
+    exp = np.where(fam == 6, golden["exp_v6"], golden["exp_legacy"])
+    got, _ = run_device(torch_cuda, engine, golden["umem"], golden_desc(golden), X.MODE_AUTO,
+                        len_hint=len_hint)
+    assert np.array_equal(got, exp)
+    exp_rfc = np.where(fam == 6, golden["exp_v6"], golden["exp_rfc"])
+    got, _ = run_device(torch_cuda, engine, golden["umem"], golden_desc(golden), X.MODE_AUTO,
+                        X.F_V4_RFC, len_hint=len_hint)
+    assert np.array_equal(got, exp_rfc)
+
+
+def test_golden_inplace_and_iphdr(torch_cuda, engine, golden):
+    """INPLACE writes udp->check, IPHDR writes iph->check == xudp_checksum_half."""
+    fam = golden["family"]
+    umem = golden["umem"].copy()
+    desc = golden_desc(golden)
+    got, after = run_device(torch_cuda, engine, umem, desc, X.MODE_AUTO,
+                            X.F_INPLACE | X.F_IPHDR)
+    for i, d in enumerate(desc):
+        a = int(d["addr"])
+        f = after[a:a + int(d["len"])]
+        if fam[i] == 6:
+            assert int(f[60:62].view("<u2")[0]) == golden["exp_v6"][i]
+        else:
+            assert int(f[40:42].view("<u2")[0]) == golden["exp_legacy"][i]
+            assert int(f[24:26].view("<u2")[0]) == golden["exp_iphdr"][i]
+    # nothing outside the check fields changed
+    mask = np.ones(len(umem), dtype=bool)
+    for i, d in enumerate(desc):
+        a = int(d["addr"])
+        if fam[i] == 6:
+            mask[a + 60:a + 62] = False
+        else:
+            mask[a + 40:a + 42] = False
+            mask[a + 24:a + 26] = False
+    assert np.array_equal(after[mask], golden["umem"][mask])
+    # NO_OUT: out == NULL with INPLACE is legal
+    _, after2 = run_device(torch_cuda, engine, golden["umem"].copy(), desc, X.MODE_AUTO,
+                           X.F_INPLACE | X.F_IPHDR, out=False)
+    assert np.array_equal(after2, after)
+
+
+@pytest.mark.parametrize("family", [4, 6])
+@pytest.mark.parametrize("layout", ["packed8", "packed1", "umem_mirror"])
+def test_generated_vs_oracle(torch_cuda, engine, family, layout):
+    kw = dict(align=8)
+    if layout == "packed1":
+        kw = dict(align=1)
+    elif layout == "umem_mirror":
+        # xudp TX frame layout: 4096-byte chunks, eth at F+342 (v4) / F+322 (v6)
+        kw = dict(stride=4096, offset=342 if family == 4 else 322)
+    umem, desc = X.gen_frames_host(3000, family, 0, 3000, seed=11 + family, **kw)
+    mode = X.MODE_V6 if family == 6 else X.MODE_V4_LEGACY
+    for hint in (0, 100, 1500):
+        got, _ = run_device(torch_cuda, engine, umem, desc, mode, len_hint=hint)
+        assert np.array_equal(got, oracle.batch(umem, desc, mode))
+
+
+def test_device_generator_matches_host(torch_cuda, engine):
+    for family in (4, 6):
+        for kw in (dict(align=8), dict(align=1), dict(stride=4096, offset=342)):
+            umem, desc = X.gen_frames_host(500, family, 0, 2000, seed=5, first_index=77, **kw)
+            dev = torch_cuda.device("cuda:0")
+            d_umem = torch_cuda.zeros(len(umem), dtype=torch_cuda.uint8, device=dev)
+            d_desc = torch_cuda.from_numpy(desc.view(np.uint8)).to(dev)
+            engine.gen_fill_device(d_umem, d_desc, len(desc), family, 5, 77)
+            torch_cuda.cuda.synchronize()
+            assert np.array_equal(d_umem.cpu().numpy(), umem)
+
+
+def test_edge_cases(torch_cuda, engine):
+    # empty batch
+    dev = torch_cuda.device("cuda:0")
+    d = torch_cuda.zeros(16, dtype=torch_cuda.uint8, device=dev)
+    engine.batch_device(d, d, 0, d, X.MODE_V4_LEGACY)
+    # malformed frames: too short, jumbo > 65535 UDP bytes, unknown h_proto
+    umem, desc = X.gen_frames_host(8, 4, 10, 10, seed=3)
+    desc = desc.copy()
+    desc["len"][1] = 41          # < eth+ip+udp
+    desc["len"][2] = 34 + 65536  # udp_len > 65535
+    umem = np.concatenate([umem, np.zeros(70000, dtype=np.uint8)])
+    umem[int(desc["addr"][3]) + 12] = 0x12  # h_proto garbage (AUTO only)
+    engine.take_errors()
+    got, _ = run_device(torch_cuda, engine, umem, desc, X.MODE_AUTO)
+    exp = oracle.batch(umem, desc, X.MODE_AUTO)
+    assert got[1] == 0 and got[2] == 0 and got[3] == 0
+    assert np.array_equal(got, exp)
+    assert engine.take_errors() == 3
+    # maximum UDP length: 65535
+    umem, desc = X.gen_frames_host(3, 4, 65535 - 8, 65535 - 8, seed=4)
+    for hint in (0, 100):
+        got, _ = run_device(torch_cuda, engine, umem, desc, X.MODE_V4_LEGACY, len_hint=hint)
+        assert np.array_equal(got, oracle.batch(umem, desc, X.MODE_V4_LEGACY))
+    umem, desc = X.gen_frames_host(3, 6, 65535 - 8, 65535 - 8, seed=4)
+    got, _ = run_device(torch_cuda, engine, umem, desc, X.MODE_V6)
+    assert np.array_equal(got, oracle.batch(umem, desc, X.MODE_V6))
+    # saturating: all-0xff frames of every small length
+    umem, desc = X.gen_frames_host(400, 4, 0, 399, seed=9, align=1)
+    for d in desc:
+        a = int(d["addr"])
+        umem[a + 26:a + int(d["len"])] = 0xff
+    got, _ = run_device(torch_cuda, engine, umem, desc, X.MODE_V4_LEGACY, len_hint=100)
+    assert np.array_equal(got, oracle.batch(umem, desc, X.MODE_V4_LEGACY))
+
+
+def test_bad_arguments(engine):
+    with pytest.raises(X.XcsumError):
+        engine.batch_device(None, None, 5, None, X.MODE_V4_LEGACY)
+    with pytest.raises(X.XcsumError):
+        engine.batch_device(1, 1, 5, 1, 7)
+    with pytest.raises(X.XcsumError):
+        engine.set_geometry(7, 1, 1)

@@ -1,0 +1,68 @@
+#!/usr/bin/env python3
+"""Kernel-geometry sweep for one BASELINE config, in ONE process with
+interleaved rounds (cdna_hip_programming.md 5.4 rule 24).  Prints one JSON
+line per geometry: median / min kernel time and GB/s of algorithmic bytes.
+
+Usage: python tools/sweep.py --config 2 [--rounds 5] [--launches 20]
+"""
+import argparse
+import json
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import libxudp_amd as X  # noqa: E402
+import bench  # noqa: E402
+
+GEOMS = [(64, 2, 2), (64, 1, 2), (64, 4, 2), (64, 1, 4), (64, 2, 4), (32, 2, 2), (32, 4, 1),
+         (16, 2, 2), (16, 4, 1), (8, 4, 1), (8, 2, 1), (8, 8, 1)]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", type=int, default=2)
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--launches", type=int, default=20)
+    ap.add_argument("--geoms", default="")
+    args = ap.parse_args()
+    import torch
+    dev = torch.device("cuda:0")
+    cfg = dict(bench.CONFIGS[args.config], id=args.config)
+    eng = X.Engine(0)
+    s = torch.cuda.current_stream(dev)
+    desc, d_desc, bufs, out, first, count = bench.build_batch(cfg, 0, 1, torch, dev, eng,
+                                                              s.cuda_stream)
+    alg = X.alg_bytes(desc, cfg["family"])
+    geoms = GEOMS if not args.geoms else [tuple(int(v) for v in g.split(","))
+                                          for g in args.geoms.split(";")]
+    times = {g: [] for g in geoms}
+    for r in range(args.rounds):
+        for g in geoms:
+            eng.set_geometry(*g)
+            for k in range(3):
+                eng.batch_device(bufs[k % len(bufs)], d_desc, count, out, cfg["mode"],
+                                 stream=s.cuda_stream)
+            evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                   for _ in range(args.launches)]
+            for k in range(args.launches):
+                evs[k][0].record(s)
+                eng.batch_device(bufs[k % len(bufs)], d_desc, count, out, cfg["mode"],
+                                 stream=s.cuda_stream)
+                evs[k][1].record(s)
+            torch.cuda.synchronize()
+            times[g] += [a.elapsed_time(b) for a, b in evs]
+    for g in geoms:
+        t = np.array(times[g])
+        print(json.dumps({"config": args.config, "geometry": g, "median_ms": round(float(
+            np.median(t)), 4), "min_ms": round(float(t.min()), 4), "GBps_median": round(
+            alg / (np.median(t) * 1e-3) / 1e9, 1), "GBps_best": round(alg / (t.min() * 1e-3) / 1e9,
+                                                                      1)}), flush=True)
+    eng.close()
+
+
+if __name__ == "__main__":
+    main()
