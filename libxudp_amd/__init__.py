@@ -39,6 +39,12 @@ ERR_NAMES = {ERR_INVAL: "XCSUM_ERR_INVAL", ERR_HIP: "XCSUM_ERR_HIP",
              ERR_NOT_REGISTERED: "XCSUM_ERR_NOT_REGISTERED",
              ERR_FRAME: "XCSUM_ERR_FRAME"}
 
+# kernel geometries compiled into libxcsum.so (XCSUM_GEOMETRIES in
+# csrc/xcsum_kernels.hip): (G lanes per frame, U frames per iteration, K chunks)
+GEOMETRIES = [(64, 1, 2), (64, 1, 9), (32, 1, 3), (32, 1, 6), (16, 1, 2), (16, 1, 3),
+              (16, 1, 6), (16, 2, 6), (16, 1, 12), (8, 1, 2), (8, 2, 1), (8, 1, 12), (4, 2, 2),
+              (4, 4, 2), (4, 1, 2)]
+
 # struct xcsum_desc == struct xdp_desc
 DESC_DTYPE = np.dtype([("addr", "<u8"), ("len", "<u4"), ("options", "<u4")])
 

@@ -170,7 +170,7 @@ extern "C" int xcsum_batch_device(xcsum_ctx *c, uint8_t *d_umem, const struct xc
 	a.flags = flags & (XCSUM_F_INPLACE | XCSUM_F_IPHDR | XCSUM_F_V4_RFC);
 	a.bias = 0;
 	a.err = c->d_err;
-	HIPCHK(launch_csum(a, geometry_for(c, len_hint), c->max_blocks, (hipStream_t)stream));
+	HIPCHK(launch_csum(a, geometry_for(c, len_hint), c->cus, (hipStream_t)stream));
 	return 0;
 }
 
@@ -374,7 +374,7 @@ int batch_host_impl(xcsum_ctx *c, uint8_t *h_umem, const struct xcsum_desc *h_de
 		HIPCHK(hipMemcpyAsync(c->d_desc[slot], h_desc + i, cnt * sizeof(struct xcsum_desc),
 				      hipMemcpyHostToDevice, st));
 		uint32_t avg = (uint32_t)((hi - lo) / cnt);
-		HIPCHK(launch_csum(a, geometry_for(c, avg), c->max_blocks, st));
+		HIPCHK(launch_csum(a, geometry_for(c, avg), c->cus, st));
 		HIPCHK(hipMemcpyAsync(c->h_out[slot], c->d_out[slot],
 				      (want_ip ? 2 : 1) * cnt * sizeof(uint16_t),
 				      hipMemcpyDeviceToHost, st));

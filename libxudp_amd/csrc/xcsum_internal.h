@@ -32,7 +32,7 @@ Geometry pick_geometry(uint32_t len_hint);
 int batch_host_impl(struct xcsum_ctx *c, uint8_t *h_umem, const struct xcsum_desc *h_desc,
 		    uint32_t n, uint16_t *h_out, uint16_t *h_out_ip, uint32_t mode, uint32_t flags);
 bool geometry_supported(Geometry g);
-hipError_t launch_csum(const CsumArgs &a, Geometry g, int max_blocks, hipStream_t s);
+hipError_t launch_csum(const CsumArgs &a, Geometry g, int cus, hipStream_t s);
 hipError_t launch_gen(uint8_t *d_umem, const struct xcsum_desc *d_desc, uint32_t n,
 		      uint32_t family, uint64_t seed, uint64_t first_index, int max_blocks,
 		      hipStream_t s);

@@ -33,6 +33,7 @@
  */
 #include "xcsum_internal.h"
 #include "xcsum_gen.h"
+#include <stdlib.h>
 
 namespace xcsum {
 
@@ -47,26 +48,44 @@ static __device__ __forceinline__ uint32_t dot_odd(uint32_t w, uint32_t acc)
 	return __builtin_amdgcn_udot4(w, 0x01000100u, acc, false);
 }
 
+/* Per-frame geometry.  The span [lo, hi) is covered by nchunks aligned
+ * 16-byte chunks starting at base = lo & ~15; `head` bytes before lo and
+ * `tail` bytes after hi inside those chunks are summed and then subtracted
+ * again by the one lane that holds the first / last chunk. */
 struct Frame {
+	const uint8_t *base;
 	uint8_t *eth;
-	uintptr_t lo, hi, base; /* span [lo, hi), base = lo & ~15 */
+	uint32_t nchunks;       /* 0: nothing to load (malformed / absent) */
+	uint32_t head, tail;    /* 0..15 bytes to drop at either end */
 	uint32_t udp_len;
-	int mode;               /* 0 legacy, 1 rfc, 2 v6, -1 malformed, -2 none */
+	uint32_t odd;           /* span starts at an odd address */
+	int mode;               /* 0 legacy, 1 rfc, 2 v6, -1 malformed, -2 absent */
 };
 
 typedef __attribute__((address_space(1))) const u32x4 gu32x4;
 
-/* 16-byte global load (global_load_dwordx4, not flat: flat ops count on
- * lgkmcnt too and force full drains) */
-static __device__ __forceinline__ u32x4 load_chunk(uintptr_t addr)
+/* 16 zero bytes: lanes past the end of their frame load these, so the
+ * accumulation needs no data masking (one select per chunk) */
+__device__ u32x4 g_zero_chunk[4];
+
+static __device__ __forceinline__ u32x4 load_chunk(const uint8_t *p)
 {
-	return __builtin_nontemporal_load((gu32x4 *)addr);
+	return __builtin_nontemporal_load((gu32x4 *)p);
 }
 
+/* Descriptor of frame p (clamped so the load is unconditional; validity is
+ * decided by p < n).  With one frame per wave (UNIFORM) it is a scalar load
+ * (s_load_dwordx4, counted on lgkmcnt): the compiler moves uniform values to
+ * SGPRs right after a vector load, which would make every prefetched
+ * descriptor wait stall on the in-order vmcnt of the chunk loads. */
+typedef __attribute__((address_space(4))) const u32x4 cu32x4;
+
+template <bool UNIFORM>
 static __device__ __forceinline__ u32x4 load_desc(const CsumArgs &a, uint32_t p)
 {
-	/* clamped so the load is unconditional; validity is decided by p < n */
 	uint32_t q = p < a.n ? p : a.n - 1;
+	if (UNIFORM)
+		return *((cu32x4 *)(a.desc + q));
 	return *((gu32x4 *)(a.desc + q));
 }
 
@@ -77,28 +96,27 @@ static __device__ __forceinline__ Frame resolve(const CsumArgs &a, u32x4 d, bool
 	uint32_t len = d.z;
 	int mode = (int)a.mode;
 	f.eth = a.umem + addr;
-	if (!present) {
-		f.mode = -2;
-		f.lo = f.hi = f.base = 0;
-		f.udp_len = 0;
-		return f;
-	}
-	if (mode == XCSUM_MODE_AUTO) {
+	if (present && mode == XCSUM_MODE_AUTO) {
 		uint32_t proto = ((uint32_t)f.eth[12] << 8) | f.eth[13];
 		mode = proto == 0x0800u ? ((a.flags & XCSUM_F_V4_RFC) ? 1 : 0)
 		     : proto == 0x86DDu ? 2 : -1;
 	}
 	uint32_t hdr = mode == 2 ? 54u : 34u;
 	uint32_t pre = mode == 2 ? 32u : 8u;
-	if (mode < 0 || len < hdr + 8u || len - hdr > 65535u) {
+	if (mode < 0 || len < hdr + 8u || len - hdr > 65535u)
 		mode = -1;
-		len = hdr;
-	}
-	f.mode = mode;
+	uintptr_t lo = (uintptr_t)f.eth + hdr - pre;
+	uintptr_t base = lo & ~(uintptr_t)15;
+	uint32_t span_end = len + pre - hdr + (uint32_t)(lo - base); /* hi - base */
+	f.base = (const uint8_t *)base;
 	f.udp_len = len - hdr;
-	f.lo = (uintptr_t)f.eth + hdr - pre;
-	f.hi = mode < 0 ? f.lo : (uintptr_t)f.eth + len;
-	f.base = f.lo & ~(uintptr_t)15;
+	f.odd = (uint32_t)lo & 1u;
+	f.head = (uint32_t)(lo - base);
+	f.nchunks = (span_end + 15) >> 4;
+	f.tail = (f.nchunks << 4) - span_end;
+	if (mode < 0 || !present)
+		f.nchunks = 0;
+	f.mode = present ? mode : -2;
 	return f;
 }
 
@@ -111,36 +129,51 @@ static __device__ __forceinline__ uint32_t byte_mask(int lo, int hi)
 
 static __device__ __forceinline__ int clamp4(int x) { return x < 0 ? 0 : (x > 4 ? 4 : x); }
 
-/* accumulate one 16-byte chunk at address `a` into E (even bytes), O (odd) */
-static __device__ __forceinline__ void accum(u32x4 v, uintptr_t a, const Frame &f,
-					     uint32_t &E, uint32_t &O)
+/* whole 16-byte chunk into E (bytes at even addresses) and O (odd) */
+static __device__ __forceinline__ void accum(u32x4 v, uint32_t &E, uint32_t &O)
 {
-	if (a >= f.lo && a + 16 <= f.hi) {
-		E = dot_even(v.x, E); O = dot_odd(v.x, O);
-		E = dot_even(v.y, E); O = dot_odd(v.y, O);
-		E = dot_even(v.z, E); O = dot_odd(v.z, O);
-		E = dot_even(v.w, E); O = dot_odd(v.w, O);
-	} else if (a < f.hi && a + 16 > f.lo) {
-		int lo = a >= f.lo ? 0 : (int)(f.lo - a);
-		int hi = f.hi >= a + 16 ? 16 : (int)(f.hi - a);
-		uint32_t w;
-		w = v.x & byte_mask(clamp4(lo), clamp4(hi));
-		E = dot_even(w, E); O = dot_odd(w, O);
-		w = v.y & byte_mask(clamp4(lo - 4), clamp4(hi - 4));
-		E = dot_even(w, E); O = dot_odd(w, O);
-		w = v.z & byte_mask(clamp4(lo - 8), clamp4(hi - 8));
-		E = dot_even(w, E); O = dot_odd(w, O);
-		w = v.w & byte_mask(clamp4(lo - 12), clamp4(hi - 12));
-		E = dot_even(w, E); O = dot_odd(w, O);
-	}
+	E = dot_even(v.x, E); O = dot_odd(v.x, O);
+	E = dot_even(v.y, E); O = dot_odd(v.y, O);
+	E = dot_even(v.z, E); O = dot_odd(v.z, O);
+	E = dot_even(v.w, E); O = dot_odd(v.w, O);
 }
 
+/* take bytes [lo, hi) of a chunk back out of E and O */
+static __device__ __forceinline__ void drop(u32x4 v, int lo, int hi, uint32_t &E, uint32_t &O)
+{
+	uint32_t w;
+	w = v.x & byte_mask(clamp4(lo), clamp4(hi));
+	E -= dot_even(w, 0u); O -= dot_odd(w, 0u);
+	w = v.y & byte_mask(clamp4(lo - 4), clamp4(hi - 4));
+	E -= dot_even(w, 0u); O -= dot_odd(w, 0u);
+	w = v.z & byte_mask(clamp4(lo - 8), clamp4(hi - 8));
+	E -= dot_even(w, 0u); O -= dot_odd(w, 0u);
+	w = v.w & byte_mask(clamp4(lo - 12), clamp4(hi - 12));
+	E -= dot_even(w, 0u); O -= dot_odd(w, 0u);
+}
+
+/* Sum over each aligned group of G lanes, result in every lane of the group.
+ * DPP adds within a 16-lane row (quad_perm xor 1, xor 2, row_half_mirror,
+ * row_mirror), then gfx950's v_permlane16_swap / v_permlane32_swap across
+ * rows: ~8 VALU instructions for 64 lanes, no LDS round trip.  Must run with
+ * every lane of the wave active. */
 template <int G>
 static __device__ __forceinline__ uint32_t seg_sum(uint32_t v)
 {
-#pragma unroll
-	for (int m = G / 2; m >= 1; m >>= 1)
-		v += __shfl_xor(v, m, G);
+	v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false);  /* ^1 */
+	v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, false);  /* ^2 */
+	if (G >= 8)
+		v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x141, 0xF, 0xF, false);
+	if (G >= 16)
+		v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x140, 0xF, 0xF, false);
+	if (G >= 32) {
+		auto p = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+		v = p[0] + p[1];
+	}
+	if (G >= 64) {
+		auto q = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+		v = q[0] + q[1];
+	}
 	return v;
 }
 
@@ -212,6 +245,69 @@ static __device__ __forceinline__ void finalize(const CsumArgs &a, const Frame &
 }
 
 template <int G, int U, int K>
+static __device__ __forceinline__ void issue(const Frame (&f)[U], uint32_t lane,
+					     u32x4 (&v)[U][K])
+{
+	const uint8_t *zero = (const uint8_t *)g_zero_chunk;
+#pragma unroll
+	for (int u = 0; u < U; u++)
+#pragma unroll
+		for (int k = 0; k < K; k++) {
+			uint32_t c = lane + k * G;
+			v[u][k] = load_chunk(c < f[u].nchunks ? f[u].base + 16u * c : zero);
+		}
+}
+
+/* accumulate, reduce and finalize the U frames of one iteration */
+template <int G, int U, int K, bool TAIL>
+static __device__ __forceinline__ void consume(const CsumArgs &a, const Frame (&fc)[U],
+					       const u32x4 (&vc)[U][K], uint32_t lane,
+					       uint32_t p0, uint32_t nseg)
+{
+#pragma unroll
+	for (int u = 0; u < U; u++) {
+		const Frame &f = fc[u];
+		const uint32_t last = f.nchunks - 1;
+		uint32_t E = 0, O = 0;
+		if (!TAIL || f.nchunks <= K * G) {
+#pragma unroll
+			for (int k = 0; k < K; k++)
+				accum(vc[u][k], E, O);
+			if (lane == 0 && f.head)
+				drop(vc[u][0], 0, (int)f.head, E, O);
+			if (f.tail && lane == (last & (G - 1))) {
+#pragma unroll
+				for (int k = 0; k < K; k++)
+					if ((last / G) == (uint32_t)k)
+						drop(vc[u][k], 16 - (int)f.tail, 16, E, O);
+			}
+		} else {
+			/* jumbo frame: plain strided walk over all its chunks */
+			for (uint32_t c = lane; c < f.nchunks; c += G) {
+				u32x4 v = load_chunk(f.base + 16u * c);
+				accum(v, E, O);
+				if (c == 0)
+					drop(v, 0, (int)f.head, E, O);
+				if (c == last)
+					drop(v, 16 - (int)f.tail, 16, E, O);
+			}
+		}
+		uint32_t s = f.odd ? (O << 8) + E : (E << 8) + O;
+		s = seg_sum<G>(s);
+		if (lane == 0 && f.mode != -2)
+			finalize(a, f, p0 + u * nseg, s);
+	}
+}
+
+/*
+ * Persistent grid; segment s (G lanes) owns frames s, s + nseg, ... and
+ * handles U of them per iteration.  Two-stage software pipeline: while
+ * iteration i's chunks are reduced, iteration i+1's chunks are in flight and
+ * iteration i+2's descriptors are loading.  Descriptor loads are issued
+ * BEFORE the chunk loads of the same step, so the in-order vmcnt wait for
+ * them never waits on chunk data.
+ */
+template <int G, int U, int K>
 __global__ void __launch_bounds__(256) csum_kernel(CsumArgs a)
 {
 	const uint32_t lane = threadIdx.x & (G - 1);
@@ -219,66 +315,96 @@ __global__ void __launch_bounds__(256) csum_kernel(CsumArgs a)
 	const uint32_t nseg = gridDim.x * (256u / G);
 	if (G == 64)
 		seg = __builtin_amdgcn_readfirstlane(seg);
-
 	const uint32_t step = nseg * U;
-	u32x4 dcur[U];
+
+	u32x4 d[U];
+	Frame fc[U];
+	u32x4 vc[U][K];
 #pragma unroll
 	for (int u = 0; u < U; u++)
-		dcur[u] = load_desc(a, seg + u * nseg);
+		d[u] = load_desc<G == 64>(a, seg + u * nseg);
+#pragma unroll
+	for (int u = 0; u < U; u++)
+		fc[u] = resolve(a, d[u], seg + u * nseg < a.n);
+#pragma unroll
+	for (int u = 0; u < U; u++)
+		d[u] = load_desc<G == 64>(a, seg + step + u * nseg);
+	issue<G, U, K>(fc, lane, vc);
 
 	for (uint32_t p0 = seg; p0 < a.n; p0 += step) {
-		Frame f[U];
-		u32x4 v[U][K];
+		Frame fn[U];
+		u32x4 vn[U][K];
 #pragma unroll
 		for (int u = 0; u < U; u++)
-			f[u] = resolve(a, dcur[u], p0 + u * nseg < a.n);
-#pragma unroll
-		for (int u = 0; u < U; u++) {
-#pragma unroll
-			for (int k = 0; k < K; k++) {
-				uintptr_t addr = f[u].base + 16u * (lane + k * G);
-				v[u][k] = addr < f[u].hi ? load_chunk(addr) : u32x4{0, 0, 0, 0};
-			}
-		}
-		/* next iteration's descriptors fly while this one reduces */
+			fn[u] = resolve(a, d[u], p0 + step + u * nseg < a.n);
 #pragma unroll
 		for (int u = 0; u < U; u++)
-			dcur[u] = load_desc(a, p0 + step + u * nseg);
+			d[u] = load_desc<G == 64>(a, p0 + 2 * step + u * nseg);
+		issue<G, U, K>(fn, lane, vn);
+
+		/* wave-uniform split: the jumbo path lives in its own copy of the
+		 * body, so its drains never merge into the common path's vmcnt
+		 * bookkeeping (which keeps the next iteration in flight) */
+		bool big = false;
+#pragma unroll
+		for (int u = 0; u < U; u++)
+			big |= fc[u].nchunks > K * G;
+		if (__builtin_amdgcn_ballot_w64(big))
+			consume<G, U, K, true>(a, fc, vc, lane, p0, nseg);
+		else
+			consume<G, U, K, false>(a, fc, vc, lane, p0, nseg);
 #pragma unroll
 		for (int u = 0; u < U; u++) {
-			uint32_t E = 0, O = 0;
+			fc[u] = fn[u];
 #pragma unroll
 			for (int k = 0; k < K; k++)
-				accum(v[u][k], f[u].base + 16u * (lane + k * G), f[u], E, O);
-			for (uintptr_t addr = f[u].base + 16u * (lane + K * G); addr < f[u].hi;
-			     addr += 16u * G)
-				accum(load_chunk(addr), addr, f[u], E, O);
-			uint32_t s = (f[u].lo & 1) ? (O << 8) + E : (E << 8) + O;
-			s = seg_sum<G>(s);
-			if (lane == 0 && f[u].mode != -2)
-				finalize(a, f[u], p0 + u * nseg, s);
+				vc[u][k] = vn[u][k];
 		}
 	}
 }
 
+/* Geometry from the typical frame length (bytes): enough lanes x chunks to
+ * cover a typical frame in one preload (frames beyond K*G chunks still work,
+ * through the jumbo path), as few lanes per frame as that allows (per-frame
+ * work is amortised over the 64/G frames a wave handles at once).  Measured
+ * on MI355X: tools/sweep.py, profiles/README.md. */
 Geometry pick_geometry(uint32_t len_hint)
 {
-	if (len_hint == 0 || len_hint >= 768)
-		return Geometry{64, 2, 2};
-	if (len_hint >= 384)
-		return Geometry{32, 2, 2};
-	if (len_hint >= 160)
-		return Geometry{16, 2, 2};
-	return Geometry{8, 4, 1};
+	if (len_hint == 0)
+		return Geometry{16, 1, 6};
+	uint32_t chunks = (len_hint + 15) / 16 + 1; /* span <= len - 22, + alignment */
+	if (chunks <= 8)
+		return Geometry{4, 1, 2};   /* 64-byte payloads: 2.6 TB/s algorithmic */
+	if (chunks <= 16)
+		return Geometry{8, 1, 2};
+	if (chunks <= 32)
+		return Geometry{16, 1, 2};
+	if (chunks <= 48)
+		return Geometry{16, 1, 3};
+	if (chunks <= 96)
+		return Geometry{16, 1, 6};  /* MTU frames: 6.2 TB/s */
+	return Geometry{64, 1, 9};          /* jumbo / mixed up to 9 KB: 6.0 TB/s */
 }
 
 template <int G, int U, int K>
-static hipError_t launch_t(const CsumArgs &a, int max_blocks, hipStream_t s)
+static hipError_t launch_t(const CsumArgs &a, int cus, hipStream_t s)
 {
+	/* persistent grid = what the device keeps resident (no second wave of
+	 * late blocks); $XCSUM_BLOCKS_PER_CU overrides for sweeps */
+	static int per_cu = 0;
+	if (!per_cu) {
+		const char *e = getenv("XCSUM_BLOCKS_PER_CU");
+		int nb = e ? atoi(e) : 0;
+		if (nb <= 0 && hipOccupancyMaxActiveBlocksPerMultiprocessor(
+				       &nb, csum_kernel<G, U, K>, 256, 0) != hipSuccess)
+			nb = 4;
+		per_cu = nb > 0 ? nb : 1;
+	}
 	uint64_t segs = ((uint64_t)a.n + U - 1) / U;
 	uint64_t blocks = (segs * G + 255) / 256;
-	if (blocks > (uint64_t)max_blocks)
-		blocks = max_blocks;
+	uint64_t cap = (uint64_t)cus * per_cu;
+	if (blocks > cap)
+		blocks = cap;
 	if (blocks == 0)
 		blocks = 1;
 	hipLaunchKernelGGL((csum_kernel<G, U, K>), dim3((unsigned)blocks), dim3(256), 0, s, a);
@@ -286,8 +412,9 @@ static hipError_t launch_t(const CsumArgs &a, int max_blocks, hipStream_t s)
 }
 
 #define XCSUM_GEOMETRIES(X) \
-	X(64, 2, 2) X(64, 1, 2) X(64, 4, 2) X(64, 1, 4) X(64, 2, 4) \
-	X(32, 2, 2) X(32, 4, 1) X(16, 2, 2) X(16, 4, 1) X(8, 4, 1) X(8, 2, 1) X(8, 8, 1)
+	X(64, 1, 2) X(64, 1, 9) X(32, 1, 3) X(32, 1, 6) \
+	X(16, 1, 2) X(16, 1, 3) X(16, 1, 6) X(16, 2, 6) X(16, 1, 12) \
+	X(8, 1, 2) X(8, 2, 1) X(8, 1, 12) X(4, 2, 2) X(4, 4, 2) X(4, 1, 2)
 
 bool geometry_supported(Geometry g)
 {
@@ -297,12 +424,12 @@ bool geometry_supported(Geometry g)
 	return false;
 }
 
-hipError_t launch_csum(const CsumArgs &a, Geometry g, int max_blocks, hipStream_t s)
+hipError_t launch_csum(const CsumArgs &a, Geometry g, int cus, hipStream_t s)
 {
 	if (a.n == 0)
 		return hipSuccess;
 #define X(g_, u_, k_) \
-	if (g.G == g_ && g.U == u_ && g.K == k_) return launch_t<g_, u_, k_>(a, max_blocks, s);
+	if (g.G == g_ && g.U == u_ && g.K == k_) return launch_t<g_, u_, k_>(a, cus, s);
 	XCSUM_GEOMETRIES(X)
 #undef X
 	return hipErrorInvalidValue;

@@ -14,8 +14,7 @@ from conftest import golden_desc
 
 pytestmark = pytest.mark.gpu
 
-GEOMETRIES = [(64, 2, 2), (64, 1, 2), (64, 4, 2), (64, 1, 4), (64, 2, 4), (32, 2, 2),
-              (32, 4, 1), (16, 2, 2), (16, 4, 1), (8, 4, 1), (8, 2, 1), (8, 8, 1)]
+GEOMETRIES = X.GEOMETRIES
 
 
 def run_device(torch, eng, umem, desc, mode, flags=0, len_hint=0, out=True):

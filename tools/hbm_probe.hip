@@ -1,0 +1,51 @@
+/*
+ * hbm_probe.hip -- measuring stick, not product code: the best plain
+ * streaming READ rate this MI355X sustains (global_load_dwordx4, grid-stride,
+ * per-thread u32 sum written once), to put the checksum kernel's HBM rate in
+ * context next to the 8 TB/s spec.  Built by tools/Makefile into
+ * tools/libhbmprobe.so; driven by tools/hbm_probe.py.
+ */
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(1))) const u32x4 gu32x4;
+
+template <bool NT, int UNROLL>
+__global__ void __launch_bounds__(256) stream_read(const u32x4 *p, uint64_t n16, uint32_t *out)
+{
+	uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+	const uint64_t stride = (uint64_t)gridDim.x * 256;
+	uint32_t acc = 0;
+	for (; i + (UNROLL - 1) * stride < n16; i += UNROLL * stride) {
+		u32x4 v[UNROLL];
+#pragma unroll
+		for (int u = 0; u < UNROLL; u++)
+			v[u] = NT ? __builtin_nontemporal_load((gu32x4 *)(p + i + u * stride))
+				  : *((gu32x4 *)(p + i + u * stride));
+#pragma unroll
+		for (int u = 0; u < UNROLL; u++)
+			acc += v[u].x ^ v[u].y ^ v[u].z ^ v[u].w;
+	}
+	for (; i < n16; i += stride) {
+		u32x4 v = *((gu32x4 *)(p + i));
+		acc += v.x ^ v.y ^ v.z ^ v.w;
+	}
+	out[(uint64_t)blockIdx.x * 256 + threadIdx.x] = acc;
+}
+
+extern "C" int probe_stream_read(const void *p, uint64_t nbytes, uint32_t *out, int blocks,
+				 int nt, int unroll, void *stream)
+{
+	uint64_t n16 = nbytes / 16;
+	hipStream_t s = (hipStream_t)stream;
+	const u32x4 *q = (const u32x4 *)p;
+#define L(NT_, U_) hipLaunchKernelGGL((stream_read<NT_, U_>), dim3(blocks), dim3(256), 0, s, q, n16, out)
+	if (nt) {
+		if (unroll == 1) L(true, 1); else if (unroll == 2) L(true, 2); else if (unroll == 4) L(true, 4); else L(true, 8);
+	} else {
+		if (unroll == 1) L(false, 1); else if (unroll == 2) L(false, 2); else if (unroll == 4) L(false, 4); else L(false, 8);
+	}
+#undef L
+	return hipGetLastError() == hipSuccess ? 0 : -1;
+}

@@ -1,0 +1,49 @@
+#!/usr/bin/env python3
+"""Achievable streaming-read HBM rate on this GPU (context for the roofline).
+Prints one JSON line per (blocks/CU, nt, unroll) and a best line."""
+import ctypes
+import json
+import os
+
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def main():
+    L = ctypes.CDLL(os.path.join(HERE, "libhbmprobe.so"))
+    L.probe_stream_read.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
+                                    ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
+    dev = torch.device("cuda:0")
+    cus = torch.cuda.get_device_properties(dev).multi_processor_count
+    nbytes = 2 << 30  # 2 GiB >> 256 MiB Infinity Cache
+    buf = torch.randint(0, 255, (nbytes,), dtype=torch.uint8, device=dev)
+    out = torch.empty(cus * 32 * 256, dtype=torch.int32, device=dev)
+    s = torch.cuda.current_stream(dev)
+    best = None
+    for per_cu in (2, 4, 8, 16):
+        for nt in (0, 1):
+            for unroll in (1, 2, 4, 8):
+                blocks = cus * per_cu
+                ts = []
+                for r in range(8):
+                    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(
+                        enable_timing=True)
+                    a.record(s)
+                    L.probe_stream_read(buf.data_ptr(), nbytes, out.data_ptr(), blocks, nt,
+                                        unroll, s.cuda_stream)
+                    b.record(s)
+                    torch.cuda.synchronize()
+                    ts.append(a.elapsed_time(b))
+                t = sorted(ts)[len(ts) // 2]
+                gbs = nbytes / (t * 1e-3) / 1e9
+                rec = {"blocks_per_cu": per_cu, "nt": nt, "unroll": unroll, "ms": round(t, 4),
+                       "GBps": round(gbs, 1)}
+                print(json.dumps(rec), flush=True)
+                if best is None or gbs > best["GBps"]:
+                    best = rec
+    print(json.dumps({"best_stream_read": best}))
+
+
+if __name__ == "__main__":
+    main()

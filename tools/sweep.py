@@ -18,8 +18,7 @@ sys.path.insert(0, ROOT)
 import libxudp_amd as X  # noqa: E402
 import bench  # noqa: E402
 
-GEOMS = [(64, 2, 2), (64, 1, 2), (64, 4, 2), (64, 1, 4), (64, 2, 4), (32, 2, 2), (32, 4, 1),
-         (16, 2, 2), (16, 4, 1), (8, 4, 1), (8, 2, 1), (8, 8, 1)]
+GEOMS = X.GEOMETRIES
 
 
 def main():
