@@ -58,18 +58,23 @@ def dist_env():
     return world, rank, local
 
 
+def rank_slice(cfg, rank, world):
+    """(first global frame index, frame count) owned by `rank`.  Config 5 is
+    one 8M-frame job split by bytes over the ranks (strong scaling); the others
+    give every rank its own full batch (weak scaling).  No data-path
+    collective: a frame's checksum depends on that frame only."""
+    n = cfg["n"]
+    if cfg["shard"]:
+        full, _ = X.gen_layout(n, cfg["family"], cfg["pmin"], cfg["pmax"],
+                               seed=SEED_BASE ^ cfg["id"])
+        return X.shard_by_bytes(full, world, rank)
+    return rank * n, n
+
+
 def build_batch(cfg, rank, world, torch, dev, eng, stream):
     """Descriptors + frames for this rank, generated on the device."""
     seed = SEED_BASE ^ cfg["id"]
-    n = cfg["n"]
-    if cfg["shard"]:
-        # strong scaling: the config's n frames split by bytes over the ranks
-        full, _ = X.gen_layout(n, cfg["family"], cfg["pmin"], cfg["pmax"], seed=seed)
-        first, count = X.shard_by_bytes(full, world, rank)
-        del full
-    else:
-        # weak scaling: every rank owns its own n frames (global index rank*n..)
-        first, count = rank * n, n
+    first, count = rank_slice(cfg, rank, world)
     desc, nbytes = X.gen_layout(count, cfg["family"], cfg["pmin"], cfg["pmax"], seed=seed,
                                 first_index=first)
     d_desc = torch.from_numpy(desc.view(np.uint8)).to(dev)

@@ -234,3 +234,93 @@ class Engine:
     def gen_fill_device(self, d_umem, d_desc, n, family, seed=0, first_index=0, stream=None):
         _check(lib().xcsum_gen_fill_device(_ptr(d_umem), _ptr(d_desc), n, family, seed,
                                            first_index, _ptr(stream)), "xcsum_gen_fill_device")
+
+
+# ---- packet.c mirror (include/xudp_packet.h) ------------------------------
+
+AF_INET = 2
+AF_INET6 = 10
+
+
+class SockaddrIn(ctypes.Structure):
+    _fields_ = [("sin_family", ctypes.c_uint16), ("sin_port", ctypes.c_uint16),
+                ("sin_addr", ctypes.c_uint8 * 4), ("sin_zero", ctypes.c_uint8 * 8)]
+
+
+class SockaddrIn6(ctypes.Structure):
+    _fields_ = [("sin6_family", ctypes.c_uint16), ("sin6_port", ctypes.c_uint16),
+                ("sin6_flowinfo", ctypes.c_uint32), ("sin6_addr", ctypes.c_uint8 * 16),
+                ("sin6_scope_id", ctypes.c_uint32)]
+
+
+class _FromUnion(ctypes.Union):
+    _fields_ = [("_from", SockaddrIn), ("_from6", SockaddrIn6)]
+
+
+class PacketInfo(ctypes.Structure):
+    """struct packet_info (xudp/packet.h:28-53, include/xudp_packet.h)."""
+    _fields_ = [("family", ctypes.c_uint8), ("dmac", ctypes.c_void_p), ("smac", ctypes.c_void_p),
+                ("to", ctypes.c_void_p), ("from_", ctypes.c_void_p), ("u", _FromUnion),
+                ("head", ctypes.c_void_p), ("data", ctypes.c_void_p),
+                ("payload", ctypes.c_void_p), ("payload_size", ctypes.c_int),
+                ("packet", ctypes.c_void_p), ("len", ctypes.c_int)]
+
+
+def htons(p):
+    return ((p & 0xff) << 8) | (p >> 8)
+
+
+class PacketArgs:
+    """Keeps the buffers a PacketInfo points to alive."""
+
+    def __init__(self, family, payload, smac, dmac, saddr, sport, daddr, dport, headroom=64,
+                 tailroom=64, buf=None, offset=0):
+        self.family = family
+        self.smac = (ctypes.c_uint8 * 6)(*smac)
+        self.dmac = (ctypes.c_uint8 * 6)(*dmac)
+        if family == 6:
+            self.src = SockaddrIn6(AF_INET6, htons(sport), 0, (ctypes.c_uint8 * 16)(*saddr), 0)
+            self.dst = SockaddrIn6(AF_INET6, htons(dport), 0, (ctypes.c_uint8 * 16)(*daddr), 0)
+        else:
+            self.src = SockaddrIn(AF_INET, htons(sport), (ctypes.c_uint8 * 4)(*saddr))
+            self.dst = SockaddrIn(AF_INET, htons(dport), (ctypes.c_uint8 * 4)(*daddr))
+        self.payload = np.frombuffer(bytes(payload) + b"\0", dtype=np.uint8).copy()
+        if buf is None:
+            buf = np.zeros(headroom + len(payload) + tailroom, dtype=np.uint8)
+        self.buf = buf
+        self.info = PacketInfo()
+        self.info.family = AF_INET6 if family == 6 else AF_INET
+        self.info.dmac = ctypes.addressof(self.dmac)
+        self.info.smac = ctypes.addressof(self.smac)
+        self.info.to = ctypes.addressof(self.dst)
+        self.info.from_ = ctypes.addressof(self.src)
+        self.info.head = buf.ctypes.data + offset
+        self.info.data = buf.ctypes.data + offset + HDR6 + 2  # == head + XUDP_TX_HEADROOM
+        self.info.payload = self.payload.ctypes.data
+        self.info.payload_size = len(payload)
+
+    def frame(self):
+        """Frame bytes [packet, packet + len) after a build."""
+        off = self.info.packet - self.buf.ctypes.data
+        return self.buf[off:off + self.info.len].copy()
+
+
+def packet_build_headers(pa):
+    lib().xudp_packet_build_headers(ctypes.byref(pa.info))
+
+
+def packet_udp_payload(pa):
+    lib().xudp_packet_udp_payload(ctypes.byref(pa.info))
+
+
+def packet_udp(pa):
+    lib().xudp_packet_udp(ctypes.byref(pa.info))
+
+
+def packet_udp_batch(engine, pas, flags=0):
+    arr = (PacketInfo * len(pas))(*[p.info for p in pas])
+    _check(lib().xudp_packet_udp_batch(engine.ctx if engine else None, arr, len(pas), flags),
+           "xudp_packet_udp_batch")
+    for p, a in zip(pas, arr):
+        p.info.packet = a.packet
+        p.info.len = a.len

@@ -1,0 +1,135 @@
+"""CPU: the C-ABI library loads and exports exactly what include/*.h declares;
+argument validation works without touching a GPU."""
+import ctypes
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+import libxudp_amd as X
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def declared_functions():
+    names = set()
+    for h in ("xcsum.h", "xudp_packet.h"):
+        src = open(os.path.join(ROOT, "include", h)).read()
+        src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+        for m in re.finditer(r"^[a-z][\w \*]*?\b(\w+)\s*\(", src, flags=re.M):
+            names.add(m.group(1))
+    return sorted(names)
+
+
+def exported_symbols():
+    out = subprocess.run(["nm", "-D", "--defined-only", X.LIB_PATH], capture_output=True,
+                         text=True, check=True).stdout
+    return {l.split()[-1] for l in out.splitlines() if " T " in l}
+
+
+def test_library_loads():
+    assert X.lib() is not None
+
+
+def test_every_declared_function_is_exported():
+    decl = declared_functions()
+    assert len(decl) == 18, decl
+    missing = sorted(set(decl) - exported_symbols())
+    assert not missing, missing
+
+
+def test_python_binding_covers_the_abi():
+    assert set(declared_functions()) <= set(X._SIGS)
+
+
+def test_struct_layouts_match_c():
+    """struct xcsum_desc == struct xdp_desc (16 B); struct packet_info matches
+    xudp/packet.h:28-53 as compiled by gcc from include/xudp_packet.h."""
+    src = r'''
+#include <stdio.h>
+#include <stddef.h>
+#include <linux/if_xdp.h>
+#include "xudp_packet.h"
+int main(void) {
+  printf("%zu %zu %zu %zu %zu %zu %zu %zu\n", sizeof(struct xcsum_desc),
+         sizeof(struct xdp_desc), offsetof(struct xdp_desc, len),
+         sizeof(struct packet_info), offsetof(struct packet_info, head),
+         offsetof(struct packet_info, payload_size), offsetof(struct packet_info, packet),
+         offsetof(struct packet_info, len));
+  return 0; }'''
+    import tempfile
+    with tempfile.TemporaryDirectory() as d:
+        c = os.path.join(d, "l.c")
+        open(c, "w").write(src)
+        subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), c, "-o",
+                        os.path.join(d, "l")], check=True)
+        vals = [int(v) for v in subprocess.run([os.path.join(d, "l")], capture_output=True,
+                                               text=True, check=True).stdout.split()]
+    assert vals[0] == vals[1] == 16 and vals[2] == 8
+    P = X.PacketInfo
+    assert vals[3:] == [ctypes.sizeof(P), P.head.offset, P.payload_size.offset, P.packet.offset,
+                        P.len.offset]
+
+
+REF_PACKET_H = "/root/reference/xudp/packet.h"
+
+
+@pytest.mark.skipif(not os.path.exists(REF_PACKET_H), reason="reference not present")
+def test_packet_info_layout_equals_reference():
+    """Compile the reference's packet.h and ours side by side (build container only)."""
+    import tempfile
+    prog = r'''
+#include <stdio.h>
+#include <stddef.h>
+#include HDR
+int main(void){ printf("%zu %zu %zu %zu %zu %zu %zu\n", sizeof(struct packet_info),
+ offsetof(struct packet_info, dmac), offsetof(struct packet_info, head),
+ offsetof(struct packet_info, data), offsetof(struct packet_info, payload_size),
+ offsetof(struct packet_info, packet), offsetof(struct packet_info, len)); return 0; }'''
+    outs = []
+    with tempfile.TemporaryDirectory() as d:
+        c = os.path.join(d, "p.c")
+        open(c, "w").write(prog)
+        for hdr, inc in (('"packet.h"', ["-I", "/root/reference/xudp", "-I",
+                                         "/root/reference/common"]),
+                         ('"xudp_packet.h"', ["-I", os.path.join(ROOT, "include")])):
+            exe = os.path.join(d, "p%d" % len(outs))
+            subprocess.run(["gcc", f"-DHDR={hdr}", *inc, c, "-o", exe], check=True)
+            outs.append(subprocess.run([exe], capture_output=True, text=True).stdout)
+    assert outs[0] == outs[1]
+
+
+def test_ctx_create_without_gpu_reports_nodev():
+    try:
+        import torch
+        if torch.cuda.is_available():
+            pytest.skip("a GPU is present")
+    except ImportError:
+        pass
+    with pytest.raises(X.XcsumError) as e:
+        X.Engine(0)
+    assert e.value.rc == -X.ERR_NODEV
+
+
+def test_argument_validation_without_gpu():
+    L = X.lib()
+    assert L.xcsum_batch_device(None, None, None, 0, None, 0, 0, 0, None) == -X.ERR_INVAL
+    assert L.xcsum_batch_host(None, None, None, 1, None, 0, 0) == -X.ERR_INVAL
+    assert L.xcsum_ctx_set_geometry(None, 16, 1, 6) == -X.ERR_INVAL
+    assert L.xcsum_ctx_create(0, None) == -X.ERR_INVAL
+    assert L.xcsum_ctx_device(None) == -X.ERR_INVAL
+    n = ctypes.c_uint64(0)
+    d = np.zeros(4, dtype=X.DESC_DTYPE)
+    assert L.xcsum_gen_layout(4, 5, 0, 10, 0, 0, 8, 0, 0, d.ctypes.data, ctypes.byref(n)) \
+        == -X.ERR_INVAL                                   # family must be 4 or 6
+    assert L.xcsum_gen_layout(4, 4, 10, 5, 0, 0, 8, 0, 0, d.ctypes.data, ctypes.byref(n)) \
+        == -X.ERR_INVAL                                   # pmin > pmax
+    assert L.xcsum_gen_layout(4, 4, 0, 5000, 0, 0, 8, 4096, 342, d.ctypes.data,
+                              ctypes.byref(n)) == -X.ERR_INVAL  # frame exceeds stride
+    f, c = ctypes.c_uint32(), ctypes.c_uint32()
+    assert L.xcsum_shard_by_bytes(d.ctypes.data, 4, 2, 2, ctypes.byref(f), ctypes.byref(c)) \
+        == -X.ERR_INVAL
+    assert L.xcsum_unregister_umem(None, None) == -X.ERR_INVAL
+    assert L.xudp_packet_udp_batch(None, None, 0, 0) == 0       # empty batch is a no-op

@@ -1,0 +1,77 @@
+"""CPU, world_size 2 (gloo): the multi-GPU path's partitioning, exercised
+exactly as bench.py does it (rank_slice -> per-rank generation -> per-rank
+checksums, no data-path collective), checked against one single-process run.
+Only the timing reduction (MAX of elapsed) and the byte count (SUM) cross
+ranks, as in bench.py."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+import bench
+import libxudp_amd as X
+import oracle
+
+CFG_SMALL = dict(n=6000, family=4, pmin=64, pmax=9000, mode=0, shard=True, id=5, name="t")
+CFG_WEAK = dict(n=500, family=6, pmin=1472, pmax=1472, mode=2, shard=False, id=4, name="t")
+
+
+def free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def rank_outputs(cfg, rank, world):
+    first, count = bench.rank_slice(cfg, rank, world)
+    umem, desc = X.gen_frames_host(count, cfg["family"], cfg["pmin"], cfg["pmax"],
+                                   seed=bench.SEED_BASE ^ cfg["id"], first_index=first)
+    return first, oracle.batch(umem, desc, cfg["mode"]), X.alg_bytes(desc, cfg["family"])
+
+
+def worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    res = {}
+    for name, cfg in (("strong", CFG_SMALL), ("weak", CFG_WEAK)):
+        first, out, alg = rank_outputs(cfg, rank, world)
+        t = torch.tensor([float(rank + 1)], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        b = torch.tensor([float(alg), float(len(out))], dtype=torch.float64)
+        dist.all_reduce(b, op=dist.ReduceOp.SUM)
+        res[name] = (first, out, float(t[0]), b.tolist())
+    q.put((rank, res))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_two_rank_partition_matches_single_process():
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    procs = [ctx.Process(target=worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = dict(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    # strong scaling (config-5 style): shards tile the job, outputs concatenate
+    first0, out0, tmax, sums = got[0]["strong"]
+    first1, out1, _, _ = got[1]["strong"]
+    assert first0 == 0 and first1 == len(out0) and tmax == 2.0
+    whole = rank_outputs(CFG_SMALL, 0, 1)
+    assert np.array_equal(np.concatenate([out0, out1]), whole[1])
+    assert sums == [float(whole[2]), float(CFG_SMALL["n"])]
+    # weak scaling: each rank owns its own n frames, rank r starts at r*n
+    assert got[0]["weak"][0] == 0 and got[1]["weak"][0] == CFG_WEAK["n"]
+    big = dict(CFG_WEAK, n=2 * CFG_WEAK["n"])
+    whole = rank_outputs(big, 0, 1)
+    assert np.array_equal(np.concatenate([got[0]["weak"][1], got[1]["weak"][1]]), whole[1])

@@ -1,0 +1,98 @@
+"""GPU: full BASELINE sizes.  Frames generated on the device, checksummed by
+the kernel, SHA-256 of the output array compared with the digest the
+REFERENCE produced over the same frames (tests/golden/digests.json), plus
+size-independent properties (verify-after-write, geometry independence)."""
+import hashlib
+
+import numpy as np
+import pytest
+
+import bench
+import libxudp_amd as X
+
+pytestmark = [pytest.mark.gpu, pytest.mark.slow]
+
+
+def device_batch(torch, engine, cid, first=0, count=None):
+    cfg = dict(bench.CONFIGS[cid], id=cid)
+    count = cfg["n"] if count is None else count
+    desc, nbytes = X.gen_layout(count, cfg["family"], cfg["pmin"], cfg["pmax"],
+                                seed=bench.SEED_BASE ^ cid, first_index=first)
+    dev = torch.device("cuda:0")
+    d_desc = torch.from_numpy(desc.view(np.uint8)).to(dev)
+    d_umem = torch.empty(nbytes + 64, dtype=torch.uint8, device=dev)
+    engine.gen_fill_device(d_umem, d_desc, count, cfg["family"], bench.SEED_BASE ^ cid, first)
+    return cfg, desc, d_desc, d_umem
+
+
+def run(torch, engine, d_umem, d_desc, n, mode, flags=0, hint=0):
+    out = torch.empty(n, dtype=torch.int16, device="cuda:0")
+    engine.batch_device(d_umem, d_desc, n, out, mode, flags, hint)
+    torch.cuda.synchronize()
+    return out.cpu().numpy().view(np.uint16)
+
+
+def sha(a):
+    return hashlib.sha256(np.ascontiguousarray(a, dtype="<u2").tobytes()).hexdigest()
+
+
+@pytest.mark.parametrize("cid", [2, 3, 4])
+def test_config_digest(torch_cuda, engine, digests, cid):
+    cfg, desc, d_desc, d_umem = device_batch(torch_cuda, engine, cid)
+    dg = digests[f"config{cid}"]
+    hint = int(desc["len"].mean())
+    assert sha(run(torch_cuda, engine, d_umem, d_desc, len(desc), cfg["mode"], 0, hint)) \
+        == dg["sha256_out"]
+    if cfg["family"] == 4:
+        assert sha(run(torch_cuda, engine, d_umem, d_desc, len(desc), X.MODE_V4_RFC, 0, hint)) \
+            == dg["sha256_out_v4_rfc"]
+    # the frames themselves equal the host generator's (which equals the
+    # reference builder's, tests/test_generator.py)
+    h = hashlib.sha256()
+    host = d_umem.cpu().numpy()
+    for d in desc:
+        h.update(host[d["addr"]:d["addr"] + d["len"]].tobytes())
+    assert h.hexdigest() == dg["sha256_frames"]
+
+
+def test_config2_every_geometry_same_digest(torch_cuda, engine, digests):
+    cfg, desc, d_desc, d_umem = device_batch(torch_cuda, engine, 2)
+    for g in X.GEOMETRIES:
+        engine.set_geometry(*g)
+        try:
+            got = run(torch_cuda, engine, d_umem, d_desc, len(desc), cfg["mode"])
+        finally:
+            engine.set_geometry(0)
+        assert sha(got) == digests["config2"]["sha256_out"], g
+
+
+def test_config5_digest_8m_mixed(torch_cuda, engine, digests):
+    """8M frames of U[64, 9000] bytes (38 GB algorithmic) on one GPU, and the
+    byte-balanced 8-way shards of bench.py concatenated."""
+    dg = digests["config5"]
+    cfg, desc, d_desc, d_umem = device_batch(torch_cuda, engine, 5)
+    out = run(torch_cuda, engine, d_umem, d_desc, len(desc), cfg["mode"], 0,
+              int(desc["len"].mean()))
+    assert sha(out) == dg["sha256_out"]
+    assert X.alg_bytes(desc, 4) == dg["alg_bytes"]
+    del d_umem, d_desc
+    torch_cuda.cuda.empty_cache()
+    parts = []
+    for r in range(8):
+        first, count = bench.rank_slice(cfg, r, 8)
+        c, dsc, dd, du = device_batch(torch_cuda, engine, 5, first, count)
+        parts.append(run(torch_cuda, engine, du, dd, count, cfg["mode"]))
+        del du, dd
+    assert sha(np.concatenate(parts)) == dg["sha256_out"]
+
+
+@pytest.mark.parametrize("cid,mode", [(2, X.MODE_V4_RFC), (4, X.MODE_V6)])
+def test_verify_after_inplace_write(torch_cuda, engine, cid, mode):
+    """RFC property: once udp->check holds the checksum, the one's complement
+    sum over the span (check included) is 0xffff, so a second pass yields
+    ~0 -> mapped 0xffff for every frame."""
+    cfg, desc, d_desc, d_umem = device_batch(torch_cuda, engine, cid)
+    first = run(torch_cuda, engine, d_umem, d_desc, len(desc), mode, X.F_INPLACE)
+    second = run(torch_cuda, engine, d_umem, d_desc, len(desc), mode)
+    assert (second == 0xffff).all()
+    assert (first != 0).all()

@@ -1,0 +1,171 @@
+"""GPU: host-resident batches (frames in a UMEM-like host buffer) and the
+packet.c-level mirror, through the C ABI, against the reference fixtures and
+the oracle."""
+import socket
+
+import numpy as np
+import pytest
+
+import libxudp_amd as X
+import oracle
+from conftest import golden_desc
+from test_oracle import KAT3, KAT4
+
+pytestmark = pytest.mark.gpu
+
+
+def host_batch(engine, umem, desc, mode, flags=0):
+    out = np.full(len(desc), 0x5a5a, dtype=np.uint16)
+    engine.batch_host(umem, desc, out, mode, flags)
+    return out
+
+
+@pytest.mark.parametrize("mode,col,fam", [(X.MODE_V4_LEGACY, "exp_legacy", 4),
+                                          (X.MODE_V4_RFC, "exp_rfc", 4),
+                                          (X.MODE_V6, "exp_v6", 6)])
+def test_host_batch_golden(engine, golden, mode, col, fam):
+    sel = np.nonzero(golden["family"] == fam)[0]
+    got = host_batch(engine, golden["umem"], golden_desc(golden, sel), mode)
+    assert np.array_equal(got, golden[col][sel])
+
+
+def check_inplace(golden, after, desc):
+    fam = golden["family"]
+    for i, d in enumerate(desc):
+        a = int(d["addr"])
+        f = after[a:a + int(d["len"])]
+        if fam[i] == 6:
+            assert int(f[60:62].view("<u2")[0]) == golden["exp_v6"][i]
+        else:
+            assert int(f[40:42].view("<u2")[0]) == golden["exp_legacy"][i]
+            assert int(f[24:26].view("<u2")[0]) == golden["exp_iphdr"][i]
+
+
+@pytest.mark.parametrize("how", ["pageable", "registered", "zerocopy"])
+def test_host_batch_inplace(engine, golden, how):
+    umem = golden["umem"].copy()
+    desc = golden_desc(golden)
+    flags = X.F_INPLACE | X.F_IPHDR
+    if how != "pageable":
+        engine.register_umem(umem)
+    if how == "zerocopy":
+        flags |= X.F_ZEROCOPY
+    try:
+        got = host_batch(engine, umem, desc, X.MODE_AUTO, flags)
+    finally:
+        if how != "pageable":
+            engine.unregister_umem(umem)
+    fam = golden["family"]
+    assert np.array_equal(got, np.where(fam == 6, golden["exp_v6"], golden["exp_legacy"]))
+    check_inplace(golden, umem, desc)
+
+
+def test_zerocopy_needs_registration(engine, golden):
+    with pytest.raises(X.XcsumError) as e:
+        host_batch(engine, golden["umem"], golden_desc(golden), X.MODE_AUTO, X.F_ZEROCOPY)
+    assert e.value.rc == -X.ERR_NOT_REGISTERED
+
+
+@pytest.mark.parametrize("shuffle", [False, True])
+def test_host_batch_many_chunks(engine, shuffle):
+    """> 65536 frames and > 32 MiB of UMEM: several double-buffered chunks."""
+    umem, desc = X.gen_frames_host(150000, 4, 0, 1472, seed=21, align=8)
+    if shuffle:
+        desc = desc[np.random.default_rng(0).permutation(len(desc))]
+    exp = oracle.batch(umem, desc, X.MODE_V4_LEGACY)
+    assert np.array_equal(host_batch(engine, umem, desc, X.MODE_V4_LEGACY), exp)
+    engine.register_umem(umem)
+    try:
+        assert np.array_equal(host_batch(engine, umem, desc, X.MODE_V4_LEGACY), exp)
+        assert np.array_equal(host_batch(engine, umem, desc, X.MODE_V4_LEGACY, X.F_ZEROCOPY),
+                              exp)
+    finally:
+        engine.unregister_umem(umem)
+
+
+def test_host_batch_umem_mirror_layout(engine):
+    """xudp's own TX layout: 4096-byte chunks, eth at F+342 (IPv4)."""
+    umem, desc = X.gen_frames_host(5000, 4, 0, 1458, seed=8, stride=4096, offset=342)
+    got = host_batch(engine, umem, desc, X.MODE_V4_LEGACY)
+    assert np.array_equal(got, oracle.batch(umem, desc, X.MODE_V4_LEGACY))
+
+
+# ---- packet.c mirror --------------------------------------------------------
+
+MAC1, MAC2 = bytes.fromhex("020000000001"), bytes.fromhex("020000000002")
+A6 = lambda s: socket.inet_pton(socket.AF_INET6, s)
+
+
+def kat_args():
+    v6 = X.PacketArgs(6, b"abcdef", MAC1, MAC2, A6("1000:2000:3000:4000::2"), 3487,
+                      A6("1000:2000:3000:4000::1"), 40000)
+    v4 = X.PacketArgs(4, b"abcdef", MAC1, MAC2, socket.inet_aton("10.0.35.2"), 3486,
+                      socket.inet_aton("10.0.35.1"), 40000)
+    return v6, v4
+
+
+def test_packet_udp_payload_kat3_kat4(torch_cuda):
+    """xudp_packet_udp_payload (packet.c:196) frame bytes == Appendix A, checksums
+    from the kernel."""
+    v6, v4 = kat_args()
+    X.packet_udp_payload(v6)
+    X.packet_udp_payload(v4)
+    assert v6.frame().tobytes().hex() == KAT3
+    assert v4.frame().tobytes().hex() == KAT4
+
+
+def test_packet_udp_single(torch_cuda):
+    v6, v4 = kat_args()
+    for pa in (v6, v4):
+        pa.buf[64:70] = np.frombuffer(b"abcdef", dtype=np.uint8)
+        X.packet_udp(pa)
+    assert v6.frame().tobytes().hex() == KAT3
+    assert v4.frame().tobytes().hex() == KAT4
+
+
+@pytest.mark.parametrize("register", [False, True])
+def test_packet_udp_batch_random(engine, register):
+    """Many frames in one UMEM-like buffer, mixed families, one batch."""
+    rng = np.random.default_rng(5)
+    umem = np.zeros(4096 * 300, dtype=np.uint8)
+    pas = []
+    for i in range(300):
+        fam = 6 if i % 3 == 0 else 4
+        L = int(rng.integers(0, 1439))
+        alen = 16 if fam == 6 else 4
+        pa = X.PacketArgs(fam, rng.integers(0, 256, L, dtype=np.uint8).tobytes(),
+                          rng.integers(0, 256, 6, dtype=np.uint8).tobytes(),
+                          rng.integers(0, 256, 6, dtype=np.uint8).tobytes(),
+                          rng.integers(0, 256, alen, dtype=np.uint8).tobytes(),
+                          int(rng.integers(0, 65536)),
+                          rng.integers(0, 256, alen, dtype=np.uint8).tobytes(),
+                          int(rng.integers(0, 65536)), buf=umem, offset=4096 * i + 320)
+        umem[4096 * i + 320 + 64:4096 * i + 320 + 64 + L] = pa.payload[:L]
+        pas.append(pa)
+    if register:
+        engine.register_umem(umem)
+    try:
+        X.packet_udp_batch(engine, pas)
+    finally:
+        if register:
+            engine.unregister_umem(umem)
+    for pa in pas:
+        f = pa.frame()
+        z = f.copy()
+        desc = np.zeros(1, dtype=X.DESC_DTYPE)
+        desc["len"] = len(f)
+        if pa.family == 6:
+            z[60:62] = 0
+            assert int(f[60:62].view("<u2")[0]) == oracle.batch(z, desc, X.MODE_V6)[0]
+        else:
+            assert f[40:42].tobytes() == b"\0\0"          # packet.c:125, udp->check = 0
+            assert int(f[24:26].view("<u2")[0]) == oracle.ip_header_rfc(f)
+    # opt-in RFC UDP checksum for IPv4
+    X.packet_udp_batch(engine, pas[1:3], X.F_V4_RFC)
+    for pa in pas[1:3]:
+        f = pa.frame()
+        z = f.copy()
+        z[40:42] = 0
+        desc = np.zeros(1, dtype=X.DESC_DTYPE)
+        desc["len"] = len(f)
+        assert int(f[40:42].view("<u2")[0]) == oracle.batch(z, desc, X.MODE_V4_RFC)[0]
