@@ -372,7 +372,9 @@ Geometry pick_geometry(uint32_t len_hint)
 {
 	if (len_hint == 0)
 		return Geometry{16, 1, 6};
-	uint32_t chunks = (len_hint + 15) / 16 + 1; /* span <= len - 22, + alignment */
+	/* worst-case chunks of a frame of len_hint bytes: span <= len - 22,
+	 * plus up to 15 bytes of 16-byte misalignment */
+	uint32_t chunks = (len_hint + 8) / 16;
 	if (chunks <= 8)
 		return Geometry{4, 1, 2};   /* 64-byte payloads: 2.6 TB/s algorithmic */
 	if (chunks <= 16)

@@ -1,0 +1,88 @@
+#!/usr/bin/env python3
+"""End-to-end rate of the host-resident path (frames start and end in host
+memory, like xudp's AF_XDP UMEM): xcsum_batch_host() = chunked double-buffered
+hipMemcpyAsync H2D -> kernel -> 2-byte results D2H, for
+  pageable   -- plain malloc'ed UMEM (runtime stages the copies),
+  registered -- UMEM page-locked with xcsum_register_umem (direct DMA),
+  zerocopy   -- registered UMEM read in place by the kernel over PCIe,
+and each of them with XCSUM_F_INPLACE (udp->check written into the host
+frames).  Also the raw pinned H2D copy rate for context.  One JSON line per
+variant.  Usage: python tools/bench_e2e.py [--config 2] [--reps 5]"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import bench  # noqa: E402
+import libxudp_amd as X  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", type=int, default=2)
+    ap.add_argument("--reps", type=int, default=5)
+    args = ap.parse_args()
+    import torch
+    cfg = dict(bench.CONFIGS[args.config], id=args.config)
+    n = min(cfg["n"], 1 << 20)
+    umem, desc = X.gen_frames_host(n, cfg["family"], cfg["pmin"], cfg["pmax"],
+                                   seed=bench.SEED_BASE ^ args.config)
+    alg = X.alg_bytes(desc, cfg["family"])
+    out = np.zeros(n, dtype=np.uint16)
+    eng = X.Engine(0)
+    import oracle
+    exp = oracle.batch(umem, desc, cfg["mode"])
+
+    # raw pinned H2D rate of the same bytes
+    pin = torch.empty(umem.nbytes, dtype=torch.uint8).pin_memory()
+    pin.numpy()[:] = umem
+    dst = torch.empty(umem.nbytes, dtype=torch.uint8, device="cuda:0")
+    dst.copy_(pin, non_blocking=True)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.reps):
+        dst.copy_(pin, non_blocking=True)
+    torch.cuda.synchronize()
+    h2d = umem.nbytes * args.reps / (time.perf_counter() - t0) / 1e9
+    print(json.dumps({"variant": "raw_pinned_h2d_copy", "GBps": round(h2d, 1),
+                      "bytes": umem.nbytes}), flush=True)
+    del pin, dst
+
+    for variant in ("pageable", "registered", "zerocopy"):
+        for inplace in (False, True):
+            flags = X.F_INPLACE if inplace else 0
+            if variant != "pageable":
+                eng.register_umem(umem)
+            if variant == "zerocopy":
+                flags |= X.F_ZEROCOPY
+            eng.batch_host(umem, desc, out, cfg["mode"], flags)  # warm-up
+            ok = bool(np.array_equal(out, exp))
+            t0 = time.perf_counter()
+            for _ in range(args.reps):
+                eng.batch_host(umem, desc, out, cfg["mode"], flags)
+            dt = (time.perf_counter() - t0) / args.reps
+            if variant != "pageable":
+                eng.unregister_umem(umem)
+            if inplace:  # restore check fields for the next variant
+                off = 60 if cfg["family"] == 6 else 40
+                for d in desc[:0]:
+                    pass
+                umem2, _ = X.gen_frames_host(n, cfg["family"], cfg["pmin"], cfg["pmax"],
+                                             seed=bench.SEED_BASE ^ args.config)
+                umem[:] = umem2
+            print(json.dumps({"variant": variant, "inplace": inplace, "frames": n,
+                              "ms": round(dt * 1e3, 3),
+                              "GiBps_alg": round(alg / dt / 2**30, 1),
+                              "GBps_frames": round(umem.nbytes / dt / 1e9, 1),
+                              "mpps": round(n / dt / 1e6, 1), "parity": ok}), flush=True)
+    eng.close()
+
+
+if __name__ == "__main__":
+    main()

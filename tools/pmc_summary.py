@@ -1,0 +1,64 @@
+#!/usr/bin/env python3
+"""Summarise rocprofv3 --pmc counter CSVs for the checksum kernel into
+profiles/pmc_config<C>.json (read by bench.py for roofline.traffic).
+
+HBM bytes per launch follow MI355X_MICROARCH.md 'HBM' / cdna_hip_programming.md
+section 7: FETCH_SIZE and WRITE_SIZE are in KiB; on gfx950 FETCH_SIZE counts
+exactly half the bytes of a wide coalesced streaming read, so
+    hbm_bytes = (2 * FETCH_SIZE + WRITE_SIZE) * 1024.
+The two counters come from separate --pmc passes (they cannot share one).
+
+Usage: python tools/pmc_summary.py --config 2 --fetch <csv> --write <csv>
+           --alg-bytes <per launch> [--out profiles/pmc_config2.json]
+"""
+import argparse
+import csv
+import json
+import os
+import statistics
+
+KERNEL = "csum_kernel"
+
+
+def counter_values(path, name):
+    vals = {}
+    with open(path) as f:
+        for row in csv.DictReader(f):
+            if KERNEL not in row.get("Kernel_Name", ""):
+                continue
+            if row.get("Counter_Name") != name:
+                continue
+            key = row.get("Dispatch_Id") or row.get("Correlation_Id")
+            vals[key] = vals.get(key, 0.0) + float(row["Counter_Value"])
+    return list(vals.values())
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", type=int, required=True)
+    ap.add_argument("--fetch", required=True)
+    ap.add_argument("--write", required=True)
+    ap.add_argument("--alg-bytes", type=float, required=True)
+    ap.add_argument("--out", default="")
+    args = ap.parse_args()
+    fetch = counter_values(args.fetch, "FETCH_SIZE")
+    write = counter_values(args.write, "WRITE_SIZE")
+    if not fetch or not write:
+        raise SystemExit("no csum_kernel counter rows found")
+    f_kib = statistics.median(fetch)
+    w_kib = statistics.median(write)
+    hbm = (2 * f_kib + w_kib) * 1024
+    rec = {"config": args.config, "kernel": KERNEL, "dispatches": [len(fetch), len(write)],
+           "FETCH_SIZE_KiB_median": f_kib, "WRITE_SIZE_KiB_median": w_kib,
+           "hbm_bytes_per_launch": round(hbm), "alg_bytes_per_launch": args.alg_bytes,
+           "traffic_over_alg": round(hbm / args.alg_bytes, 4),
+           "formula": "(2*FETCH_SIZE + WRITE_SIZE) * 1024  (gfx950 FETCH_SIZE = half of "
+                      "wide streaming read bytes, MI355X_MICROARCH.md HBM)"}
+    out = args.out or os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(
+        __file__))), "profiles", f"pmc_config{args.config}.json")
+    json.dump(rec, open(out, "w"), indent=1)
+    print(json.dumps(rec))
+
+
+if __name__ == "__main__":
+    main()
