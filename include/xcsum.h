@@ -94,6 +94,9 @@ int xcsum_ctx_take_errors(xcsum_ctx *ctx, uint64_t *count);
  * len_hint).  Results never depend on the geometry.  -XCSUM_ERR_INVAL if the
  * combination is not compiled in. */
 int xcsum_ctx_set_geometry(xcsum_ctx *ctx, int G, int U, int K);
+/* Cap the persistent grid at `blocks_per_cu` 256-thread blocks per CU
+ * (tuning; 0 = the per-geometry default, the occupancy limit at most). */
+int xcsum_ctx_set_launch(xcsum_ctx *ctx, int blocks_per_cu);
 
 /* ---- device-resident batch ------------------------------------------------
  * Replaces the per-frame checksum work of the xudp_frame_send loop

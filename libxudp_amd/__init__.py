@@ -14,7 +14,8 @@ import os
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libxcsum.so")
+# XCSUM_LIB selects an A/B build variant of the library (tuning only)
+LIB_PATH = os.environ.get("XCSUM_LIB") or os.path.join(HERE, "libxcsum.so")
 
 # include/xcsum.h
 MODE_V4_LEGACY = 0
@@ -67,6 +68,7 @@ _SIGS = {
     "xcsum_ctx_take_errors": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64)]),
     "xcsum_ctx_set_geometry": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
                                               ctypes.c_int]),
+    "xcsum_ctx_set_launch": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     "xcsum_batch_device": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                           ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint32,
                                           ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p]),
@@ -205,6 +207,9 @@ class Engine:
 
     def set_geometry(self, G=0, U=0, K=0):
         _check(lib().xcsum_ctx_set_geometry(self._ctx, G, U, K), "xcsum_ctx_set_geometry")
+
+    def set_launch(self, blocks_per_cu=0):
+        _check(lib().xcsum_ctx_set_launch(self._ctx, blocks_per_cu), "xcsum_ctx_set_launch")
 
     def take_errors(self):
         c = ctypes.c_uint64(0)

@@ -26,9 +26,9 @@ static Geometry env_geometry()
 {
 	const char *s = getenv("XCSUM_GEOMETRY");
 	int G, U, K;
-	if (s && sscanf(s, "%d,%d,%d", &G, &U, &K) == 3 && geometry_supported(Geometry{G, U, K}))
-		return Geometry{G, U, K};
-	return Geometry{0, 0, 0};
+	if (s && sscanf(s, "%d,%d,%d", &G, &U, &K) == 3 && geometry_supported(Geometry{G, U, K, 0}))
+		return Geometry{G, U, K, 0};
+	return Geometry{0, 0, 0, 0};
 }
 
 extern "C" int xcsum_ctx_create(int device, xcsum_ctx **out)
@@ -74,6 +74,7 @@ extern "C" int xcsum_ctx_create(int device, xcsum_ctx **out)
 	c->frame_cap = 0;
 	c->desc_cap = 0;
 	c->geom = env_geometry();
+	c->blocks_per_cu = 0;
 	*out = c;
 	return 0;
 }
@@ -132,7 +133,10 @@ extern "C" int xcsum_ctx_take_errors(xcsum_ctx *c, uint64_t *count)
 
 static Geometry geometry_for(const xcsum_ctx *c, uint32_t len_hint)
 {
-	return c->geom.G ? c->geom : pick_geometry(len_hint);
+	Geometry g = c->geom.G ? c->geom : pick_geometry(len_hint);
+	if (c->blocks_per_cu > 0)
+		g.B = c->blocks_per_cu;
+	return g;
 }
 
 extern "C" int xcsum_ctx_set_geometry(xcsum_ctx *c, int G, int U, int K)
@@ -140,12 +144,24 @@ extern "C" int xcsum_ctx_set_geometry(xcsum_ctx *c, int G, int U, int K)
 	if (!c)
 		return -XCSUM_ERR_INVAL;
 	if (G == 0) {
-		c->geom = Geometry{0, 0, 0};
+		c->geom = Geometry{0, 0, 0, 0};
 		return 0;
 	}
-	if (!geometry_supported(Geometry{G, U, K}))
+	if (!geometry_supported(Geometry{G, U, K, 0}))
 		return -XCSUM_ERR_INVAL;
-	c->geom = Geometry{G, U, K};
+	c->geom = pick_geometry(0);
+	c->geom.G = G;
+	c->geom.U = U;
+	c->geom.K = K;
+	c->geom.B = 0;
+	return 0;
+}
+
+extern "C" int xcsum_ctx_set_launch(xcsum_ctx *c, int blocks_per_cu)
+{
+	if (!c || blocks_per_cu < 0 || blocks_per_cu > 32)
+		return -XCSUM_ERR_INVAL;
+	c->blocks_per_cu = blocks_per_cu;
 	return 0;
 }
 

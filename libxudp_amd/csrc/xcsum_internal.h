@@ -26,6 +26,7 @@ struct CsumArgs {
  * in flight, and each lane preloads K 16-byte chunks per frame. */
 struct Geometry {
 	int G, U, K;
+	int B; /* 256-thread blocks per CU (0: occupancy limit) */
 };
 
 Geometry pick_geometry(uint32_t len_hint);
@@ -50,6 +51,7 @@ struct Ctx {
 	int cus;
 	int max_blocks;
 	Geometry geom;                 /* forced geometry, G == 0: automatic */
+	int blocks_per_cu;             /* forced grid cap, 0: automatic */
 	unsigned long long *d_err;
 	std::vector<Region> regions;
 

@@ -68,9 +68,16 @@ typedef __attribute__((address_space(1))) const u32x4 gu32x4;
  * accumulation needs no data masking (one select per chunk) */
 __device__ u32x4 g_zero_chunk[4];
 
+/* XCSUM_NT=0 builds a variant with default-policy chunk loads (A/B only) */
+#ifndef XCSUM_NT
+#define XCSUM_NT 1
+#endif
+
 static __device__ __forceinline__ u32x4 load_chunk(const uint8_t *p)
 {
-	return __builtin_nontemporal_load((gu32x4 *)p);
+	if (XCSUM_NT)
+		return __builtin_nontemporal_load((gu32x4 *)p);
+	return *((gu32x4 *)p);
 }
 
 /* Descriptor of frame p (clamped so the load is unconditional; validity is
@@ -92,6 +99,11 @@ static __device__ __forceinline__ u32x4 load_desc(const CsumArgs &a, uint32_t p)
 static __device__ __forceinline__ Frame resolve(const CsumArgs &a, u32x4 d, bool present)
 {
 	Frame f;
+	/* d.w (xdp_desc.options) is unused; keeping it "used" here stops the
+	 * register allocator from recycling that VGPR as a temporary right after
+	 * the prefetch is issued, which would force a full vmcnt(0) drain of the
+	 * software pipeline every iteration */
+	asm volatile("" ::"v"(d.w));
 	uint64_t addr = (((uint64_t)d.y << 32) | d.x) - a.bias;
 	uint32_t len = d.z;
 	int mode = (int)a.mode;
@@ -160,8 +172,10 @@ static __device__ __forceinline__ void drop(u32x4 v, int lo, int hi, uint32_t &E
 template <int G>
 static __device__ __forceinline__ uint32_t seg_sum(uint32_t v)
 {
-	v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false);  /* ^1 */
-	v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, false);  /* ^2 */
+	if (G >= 2)
+		v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false); /* ^1 */
+	if (G >= 4)
+		v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, false); /* ^2 */
 	if (G >= 8)
 		v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x141, 0xF, 0xF, false);
 	if (G >= 16)
@@ -329,6 +343,10 @@ __global__ void __launch_bounds__(256) csum_kernel(CsumArgs a)
 #pragma unroll
 	for (int u = 0; u < U; u++)
 		d[u] = load_desc<G == 64>(a, seg + step + u * nseg);
+	/* keep every descriptor load older than the chunk loads it shares a
+	 * vmcnt queue with: the next wait for the descriptors then leaves all
+	 * chunk loads in flight */
+	__builtin_amdgcn_sched_barrier(0);
 	issue<G, U, K>(fc, lane, vc);
 
 	for (uint32_t p0 = seg; p0 < a.n; p0 += step) {
@@ -340,6 +358,7 @@ __global__ void __launch_bounds__(256) csum_kernel(CsumArgs a)
 #pragma unroll
 		for (int u = 0; u < U; u++)
 			d[u] = load_desc<G == 64>(a, p0 + 2 * step + u * nseg);
+		__builtin_amdgcn_sched_barrier(0);
 		issue<G, U, K>(fn, lane, vn);
 
 		/* wave-uniform split: the jumbo path lives in its own copy of the
@@ -371,37 +390,37 @@ __global__ void __launch_bounds__(256) csum_kernel(CsumArgs a)
 Geometry pick_geometry(uint32_t len_hint)
 {
 	if (len_hint == 0)
-		return Geometry{16, 1, 6};
+		return Geometry{16, 1, 6, 3};
 	/* worst-case chunks of a frame of len_hint bytes: span <= len - 22,
 	 * plus up to 15 bytes of 16-byte misalignment */
 	uint32_t chunks = (len_hint + 8) / 16;
 	if (chunks <= 8)
-		return Geometry{4, 1, 2};   /* 64-byte payloads: 2.6 TB/s algorithmic */
+		return Geometry{4, 1, 2, 0};   /* 64-byte payloads: 2.6 TB/s algorithmic */
 	if (chunks <= 16)
-		return Geometry{8, 1, 2};
+		return Geometry{8, 1, 2, 0};
 	if (chunks <= 32)
-		return Geometry{16, 1, 2};
+		return Geometry{16, 1, 2, 0};
 	if (chunks <= 48)
-		return Geometry{16, 1, 3};
+		return Geometry{16, 1, 3, 0};
 	if (chunks <= 96)
-		return Geometry{16, 1, 6};  /* MTU frames: 6.2 TB/s */
-	return Geometry{64, 1, 9};          /* jumbo / mixed up to 9 KB: 6.0 TB/s */
+		return Geometry{16, 1, 6, 3};  /* MTU frames: 6.2 TB/s at 3 blocks/CU */
+	return Geometry{64, 1, 9, 0};          /* jumbo / mixed up to 9 KB: 6.0 TB/s */
 }
 
 template <int G, int U, int K>
-static hipError_t launch_t(const CsumArgs &a, int cus, hipStream_t s)
+static hipError_t launch_t(const CsumArgs &a, int cus, int bpc, hipStream_t s)
 {
-	/* persistent grid = what the device keeps resident (no second wave of
-	 * late blocks); $XCSUM_BLOCKS_PER_CU overrides for sweeps */
-	static int per_cu = 0;
-	if (!per_cu) {
-		const char *e = getenv("XCSUM_BLOCKS_PER_CU");
-		int nb = e ? atoi(e) : 0;
-		if (nb <= 0 && hipOccupancyMaxActiveBlocksPerMultiprocessor(
-				       &nb, csum_kernel<G, U, K>, 256, 0) != hipSuccess)
+	/* persistent grid: at most what the device keeps resident, so no second
+	 * wave of late blocks; fewer per CU when that streams better (Geometry.B) */
+	static int occ = 0;
+	if (!occ) {
+		int nb = 0;
+		if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, csum_kernel<G, U, K>, 256, 0) !=
+			    hipSuccess || nb <= 0)
 			nb = 4;
-		per_cu = nb > 0 ? nb : 1;
+		occ = nb;
 	}
+	int per_cu = (bpc > 0 && bpc < occ) ? bpc : occ;
 	uint64_t segs = ((uint64_t)a.n + U - 1) / U;
 	uint64_t blocks = (segs * G + 255) / 256;
 	uint64_t cap = (uint64_t)cus * per_cu;
@@ -416,7 +435,8 @@ static hipError_t launch_t(const CsumArgs &a, int cus, hipStream_t s)
 #define XCSUM_GEOMETRIES(X) \
 	X(64, 1, 2) X(64, 1, 9) X(32, 1, 3) X(32, 1, 6) \
 	X(16, 1, 2) X(16, 1, 3) X(16, 1, 6) X(16, 2, 6) X(16, 1, 12) \
-	X(8, 1, 2) X(8, 2, 1) X(8, 1, 12) X(4, 2, 2) X(4, 4, 2) X(4, 1, 2)
+	X(8, 1, 2) X(8, 2, 1) X(8, 1, 12) X(4, 2, 2) X(4, 4, 2) X(4, 1, 2) \
+	X(2, 1, 4) X(2, 2, 4) X(1, 1, 6) X(1, 1, 8) X(1, 2, 6)
 
 bool geometry_supported(Geometry g)
 {
@@ -431,7 +451,7 @@ hipError_t launch_csum(const CsumArgs &a, Geometry g, int cus, hipStream_t s)
 	if (a.n == 0)
 		return hipSuccess;
 #define X(g_, u_, k_) \
-	if (g.G == g_ && g.U == u_ && g.K == k_) return launch_t<g_, u_, k_>(a, cus, s);
+	if (g.G == g_ && g.U == u_ && g.K == k_) return launch_t<g_, u_, k_>(a, cus, g.B, s);
 	XCSUM_GEOMETRIES(X)
 #undef X
 	return hipErrorInvalidValue;

@@ -27,6 +27,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--launches", type=int, default=20)
     ap.add_argument("--geoms", default="")
+    ap.add_argument("--bpc", default="0", help="blocks per CU to try, e.g. 2,3,4 (0: default)")
     args = ap.parse_args()
     import torch
     dev = torch.device("cuda:0")
@@ -38,10 +39,13 @@ def main():
     alg = X.alg_bytes(desc, cfg["family"])
     geoms = GEOMS if not args.geoms else [tuple(int(v) for v in g.split(","))
                                           for g in args.geoms.split(";")]
+    bpcs = [int(b) for b in args.bpc.split(",")]
+    geoms = [(g, b) for g in geoms for b in bpcs]
     times = {g: [] for g in geoms}
     for r in range(args.rounds):
-        for g in geoms:
+        for g, b in geoms:
             eng.set_geometry(*g)
+            eng.set_launch(b)
             for k in range(3):
                 eng.batch_device(bufs[k % len(bufs)], d_desc, count, out, cfg["mode"],
                                  stream=s.cuda_stream)
@@ -53,10 +57,10 @@ def main():
                                  stream=s.cuda_stream)
                 evs[k][1].record(s)
             torch.cuda.synchronize()
-            times[g] += [a.elapsed_time(b) for a, b in evs]
-    for g in geoms:
-        t = np.array(times[g])
-        print(json.dumps({"config": args.config, "geometry": g, "median_ms": round(float(
+            times[(g, b)] += [e0.elapsed_time(e1) for e0, e1 in evs]
+    for g, b in geoms:
+        t = np.array(times[(g, b)])
+        print(json.dumps({"config": args.config, "geometry": g, "bpc": b, "median_ms": round(float(
             np.median(t)), 4), "min_ms": round(float(t.min()), 4), "GBps_median": round(
             alg / (np.median(t) * 1e-3) / 1e9, 1), "GBps_best": round(alg / (t.min() * 1e-3) / 1e9,
                                                                       1)}), flush=True)
