@@ -60,6 +60,13 @@ enum xcsum_mode {
 #define XCSUM_F_V4_RFC   0x4u /* AUTO mode: IPv4 frames use V4_RFC */
 #define XCSUM_F_ZEROCOPY 0x8u /* host batches: kernel reads the registered UMEM
 				 through its device mapping instead of copying */
+#define XCSUM_F_VERIFY   0x10u /* receive side (group/channel.c:231-255 parses but
+				 never verifies): check the checksum already in each
+				 frame, RFC 768/2460 rules in every mode: out[i] = 0
+				 if it verifies (IPv4 check 0 = "no checksum" = valid;
+				 IPv6 check 0 = invalid), nonzero otherwise (malformed
+				 frames: 0xffff).  With XCSUM_F_IPHDR the IPv4 header
+				 must verify too for out[i] to be 0.  Never writes. */
 
 /* Error codes (returned negated). */
 enum {

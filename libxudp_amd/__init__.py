@@ -27,6 +27,7 @@ F_INPLACE = 0x1
 F_IPHDR = 0x2
 F_V4_RFC = 0x4
 F_ZEROCOPY = 0x8
+F_VERIFY = 0x10
 
 ERR_INVAL = 9000
 ERR_HIP = 9001

@@ -183,7 +183,9 @@ extern "C" int xcsum_batch_device(xcsum_ctx *c, uint8_t *d_umem, const struct xc
 	a.out = d_out;
 	a.out_ip = nullptr;
 	a.mode = mode;
-	a.flags = flags & (XCSUM_F_INPLACE | XCSUM_F_IPHDR | XCSUM_F_V4_RFC);
+	a.flags = flags & (XCSUM_F_INPLACE | XCSUM_F_IPHDR | XCSUM_F_V4_RFC | XCSUM_F_VERIFY);
+	if (a.flags & XCSUM_F_VERIFY)
+		a.flags &= ~XCSUM_F_INPLACE; /* verifying never writes frames */
 	a.bias = 0;
 	a.err = c->d_err;
 	HIPCHK(launch_csum(a, geometry_for(c, len_hint), c->cus, (hipStream_t)stream));
@@ -317,6 +319,8 @@ int batch_host_impl(xcsum_ctx *c, uint8_t *h_umem, const struct xcsum_desc *h_de
 		return 0;
 	if (!h_desc || (!h_out && !h_out_ip && !(flags & XCSUM_F_INPLACE)))
 		return -XCSUM_ERR_INVAL;
+	if (flags & XCSUM_F_VERIFY)
+		flags &= ~XCSUM_F_INPLACE; /* verifying never writes frames */
 	HIPCHK(hipSetDevice(c->device));
 	int rc = ensure_staging(c);
 	if (rc)
@@ -376,7 +380,8 @@ int batch_host_impl(xcsum_ctx *c, uint8_t *h_umem, const struct xcsum_desc *h_de
 		if (zc) {
 			a.umem = zc->dev + (h_umem - zc->host);
 			a.bias = 0;
-			a.flags = flags & (XCSUM_F_INPLACE | XCSUM_F_IPHDR | XCSUM_F_V4_RFC);
+			a.flags = flags & (XCSUM_F_INPLACE | XCSUM_F_IPHDR | XCSUM_F_V4_RFC |
+					   XCSUM_F_VERIFY);
 		} else {
 			/* 16-byte aligned copy of [lo, hi) keeps every frame's address
 			 * parity and 16-byte phase identical to the host UMEM */
@@ -385,7 +390,8 @@ int batch_host_impl(xcsum_ctx *c, uint8_t *h_umem, const struct xcsum_desc *h_de
 					      hipMemcpyHostToDevice, st));
 			a.umem = c->d_frames[slot];
 			a.bias = alo;
-			a.flags = flags & (XCSUM_F_IPHDR | XCSUM_F_V4_RFC); /* device copy is scratch */
+			/* the device copy is scratch: in-place writes happen on the host */
+			a.flags = flags & (XCSUM_F_IPHDR | XCSUM_F_V4_RFC | XCSUM_F_VERIFY);
 		}
 		HIPCHK(hipMemcpyAsync(c->d_desc[slot], h_desc + i, cnt * sizeof(struct xcsum_desc),
 				      hipMemcpyHostToDevice, st));

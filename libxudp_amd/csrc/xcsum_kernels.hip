@@ -206,16 +206,17 @@ static __device__ __forceinline__ void store_u16(uint8_t *p, uint16_t v)
 	}
 }
 
-/* IPv4 header checksum (RFC 1071 over the 20-byte header, check field as 0);
- * equals xudp_checksum_half() (packet.c:43-66) on every header iph_build()
- * writes (ihl is always 5 there, packet.c:21, and the frame-layout contract
- * of xcsum.h).  Returns the memory-order value for iph->check. */
-static __device__ uint16_t ip_header_csum(const uint8_t *iph)
+/* IPv4 header checksum (RFC 1071 over the 20-byte header) with the check
+ * field as 0 -- equals xudp_checksum_half() (packet.c:43-66) on every header
+ * iph_build() writes (ihl is always 5 there, packet.c:21, and the
+ * frame-layout contract of xcsum.h) -- or, to VERIFY a received header, with
+ * the check field included (0 = valid).  Returns the memory-order value. */
+static __device__ uint16_t ip_header_csum(const uint8_t *iph, bool verify)
 {
 	uint32_t sum = 0;
 #pragma unroll
 	for (uint32_t i = 0; i < 20; i += 2)
-		if (i != 10)
+		if (verify || i != 10)
 			sum += ((uint32_t)iph[i] << 8) | iph[i + 1];
 	sum = (sum & 0xffffu) + (sum >> 16);
 	sum = (sum & 0xffffu) + (sum >> 16);
@@ -229,6 +230,27 @@ static __device__ __forceinline__ void finalize(const CsumArgs &a, const Frame &
 	if (f.mode >= 0) {
 		uint32_t S = s + 17u + (f.udp_len >> 16) + (f.udp_len & 0xffffu);
 		uint32_t r;
+		if (a.flags & XCSUM_F_VERIFY) {
+			/* the frame's check field was summed with everything else:
+			 * a valid RFC checksum folds to 0xffff, i.e. r == 0 */
+			uint32_t t = (S & 0xffffu) + (S >> 16);
+			t = (t & 0xffffu) + (t >> 16);
+			r = ~t & 0xffffu;
+			const uint8_t *ck = f.eth + (f.mode == 2 ? 60 : 40);
+			if ((ck[0] | ck[1]) == 0)  /* no checksum: IPv4 ok, IPv6 invalid */
+				r = f.mode == 2 ? 0xffffu : 0u;
+			wire = bswap16(r);
+			if ((a.flags & XCSUM_F_IPHDR) && f.mode != 2) {
+				uint16_t ipr = ip_header_csum(f.eth + 14, true);
+				if (a.out_ip)
+					a.out_ip[p] = ipr;
+				if (wire == 0)
+					wire = ipr;  /* 0 only if both verify */
+			}
+			if (a.out)
+				a.out[p] = wire;
+			return;
+		}
 		if (f.mode == 0) {
 			/* checksum.h:100-104: one fold, carry dropped by the u16 cast */
 			r = ~((S & 0xffffu) + (S >> 16)) & 0xffffu;
@@ -243,7 +265,7 @@ static __device__ __forceinline__ void finalize(const CsumArgs &a, const Frame &
 		if (a.flags & XCSUM_F_INPLACE)
 			store_u16(f.eth + (f.mode == 2 ? 60 : 40), wire);
 		if ((a.flags & XCSUM_F_IPHDR) && f.mode != 2) {
-			uint16_t ipc = ip_header_csum(f.eth + 14);
+			uint16_t ipc = ip_header_csum(f.eth + 14, false);
 			if (a.flags & XCSUM_F_INPLACE)
 				store_u16(f.eth + 24, ipc);
 			if (a.out_ip)
@@ -251,6 +273,8 @@ static __device__ __forceinline__ void finalize(const CsumArgs &a, const Frame &
 		}
 	} else {
 		atomicAdd(a.err, 1ull);
+		if (a.flags & XCSUM_F_VERIFY)
+			wire = 0xffffu;  /* a malformed frame never verifies */
 	}
 	if (a.out)
 		a.out[p] = wire;

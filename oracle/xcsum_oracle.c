@@ -227,6 +227,52 @@ static u16 orc_udp_csum4_rfc(const u8 *udp, u32 size, const u8 *saddr4, const u8
 	return c;
 }
 
+#define ORC_FLAG_IPHDR  0x2u   /* == XCSUM_F_IPHDR */
+#define ORC_FLAG_VERIFY 0x10u  /* == XCSUM_F_VERIFY */
+
+/* RFC 1071 residue of a received IPv4 header, check field included:
+ * 0 if it verifies (memory order). */
+static u16 orc_ip_header_verify(const u8 *iph)
+{
+	u32 i, sum = 0;
+	for (i = 0; i < 20; i += 2)
+		sum += ((u32)iph[i] << 8) | iph[i + 1];
+	while (sum >> 16)
+		sum = (sum & 0xffff) + (sum >> 16);
+	return orc_bswap16((u16)~sum);
+}
+
+/* Receive-side verify (the reference has none: group/channel.c:231-255
+ * parses but never checks).  The frame's check field is summed with the
+ * rest through the reference's own do_csum/sum32/csum_fold
+ * (checksum.h:142-229); a valid RFC 768 checksum folds to 0xffff, so
+ * csum_fold() returns 0.  udp->check == 0: IPv4 "no checksum" (valid),
+ * IPv6 invalid (RFC 2460 8.1). */
+static u16 orc_verify(const u8 *frame, u32 len, int fam6, u32 flags)
+{
+	u32 hdr = fam6 ? 54 : 34, size, sum;
+	const u8 *ip = frame + 14, *udp = frame + hdr;
+	u16 r;
+	if (len < hdr + 8 || len - hdr > 0xffff)
+		return 0xffff;
+	size = len - hdr;
+	sum = orc_do_csum(udp, size);
+	if (fam6) {
+		sum = orc_udp6_hdr_csum(sum, ip + 8, ip + 24, size);
+	} else {
+		sum = orc_sum32(sum, orc_load32(ip + 12));
+		sum = orc_sum32(sum, orc_load32(ip + 16));
+		sum = orc_sum32(sum, orc_bswap32(size));
+		sum = orc_sum32(sum, orc_bswap32(ORC_IPPROTO_UDP));
+	}
+	r = orc_csum_fold(sum);
+	if (orc_load16(udp + 6) == 0)
+		r = fam6 ? 0xffff : 0;
+	if (r == 0 && !fam6 && (flags & ORC_FLAG_IPHDR))
+		r = orc_ip_header_verify(ip);
+	return r;
+}
+
 static u16 orc_one(const u8 *frame, u32 len, int mode, u32 flags)
 {
 	int fam6;
@@ -237,9 +283,11 @@ static u16 orc_one(const u8 *frame, u32 len, int mode, u32 flags)
 		else if (proto == 0x86DD)
 			mode = ORC_MODE_V6;
 		else
-			return 0;
+			return (flags & ORC_FLAG_VERIFY) ? 0xffff : 0;
 	}
 	fam6 = mode == ORC_MODE_V6;
+	if (flags & ORC_FLAG_VERIFY)
+		return orc_verify(frame, len, fam6, flags);
 	if (len < (fam6 ? 62u : 42u))
 		return 0;
 	if (fam6) {

@@ -96,3 +96,11 @@ def test_verify_after_inplace_write(torch_cuda, engine, cid, mode):
     second = run(torch_cuda, engine, d_umem, d_desc, len(desc), mode)
     assert (second == 0xffff).all()
     assert (first != 0).all()
+
+
+@pytest.mark.parametrize("cid,mode", [(2, X.MODE_V4_RFC), (4, X.MODE_V6)])
+def test_verify_flag_after_inplace_write(torch_cuda, engine, cid, mode):
+    cfg, desc, d_desc, d_umem = device_batch(torch_cuda, engine, cid)
+    run(torch_cuda, engine, d_umem, d_desc, len(desc), mode, X.F_INPLACE | X.F_IPHDR)
+    ok = run(torch_cuda, engine, d_umem, d_desc, len(desc), mode, X.F_VERIFY | X.F_IPHDR)
+    assert (ok == 0).all()

@@ -185,3 +185,46 @@ def test_bad_arguments(engine):
         engine.batch_device(1, 1, 5, 1, 7)
     with pytest.raises(X.XcsumError):
         engine.set_geometry(7, 1, 1)
+
+
+# ---- receive-side verify --------------------------------------------------
+
+from test_oracle import filled_golden  # noqa: E402
+
+
+@pytest.mark.parametrize("len_hint", [0, 100, 1500])
+def test_verify_matches_oracle(torch_cuda, engine, golden, len_hint):
+    desc = golden_desc(golden)
+    fam = golden["family"]
+    good = filled_golden(golden)
+    legacy = filled_golden(golden, "exp_legacy")
+    rng = np.random.default_rng(2)
+    bad = good.copy()
+    for i, d in enumerate(desc):
+        a, ln = int(d["addr"]), int(d["len"])
+        bad[int(rng.integers(a + 22, a + ln))] ^= 0x10
+    zero = good.copy()
+    for i, d in enumerate(desc):
+        a = int(d["addr"])
+        zero[a + (60 if fam[i] == 6 else 40):a + (62 if fam[i] == 6 else 42)] = 0
+    for umem in (good, legacy, bad, zero):
+        for flags in (X.F_VERIFY, X.F_VERIFY | X.F_IPHDR, X.F_VERIFY | X.F_INPLACE):
+            got, after = run_device(torch_cuda, engine, umem, desc, X.MODE_AUTO, flags,
+                                    len_hint)
+            exp = oracle.batch(umem, desc, X.MODE_AUTO, flags & ~X.F_INPLACE)
+            assert np.array_equal(got, exp)
+            assert np.array_equal(after, umem)   # verify never writes
+    assert (run_device(torch_cuda, engine, good, desc, X.MODE_AUTO, X.F_VERIFY | X.F_IPHDR)[0]
+            == 0).all()
+
+
+def test_verify_host_path(engine, golden):
+    desc = golden_desc(golden)
+    good = filled_golden(golden)
+    out = np.full(len(desc), 7, dtype=np.uint16)
+    engine.batch_host(good, desc, out, X.MODE_AUTO, X.F_VERIFY | X.F_IPHDR)
+    assert (out == 0).all()
+    bad = good.copy()
+    bad[int(desc["addr"][0]) + 28] ^= 0xff  # saddr byte: inside the span
+    engine.batch_host(bad, desc, out, X.MODE_AUTO, X.F_VERIFY)
+    assert out[0] != 0 and (out[1:] == 0).all()

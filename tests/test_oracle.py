@@ -221,3 +221,64 @@ def test_oracle_reproduces_fullsize_digest_prefix(digests, cid):
     if oracle.have_ref():
         assert np.array_equal(out, oracle.ref_batch(umem, desc, mode))
     assert out.dtype == np.uint16 and len(out) == 1 << 16
+
+
+# ---- receive-side verify (the reference never verifies) --
+
+def filled_golden(golden, v4_col="exp_rfc"):
+    """Golden frames with their expected checksums written into the frames."""
+    umem = golden["umem"].copy()
+    for i, fam in enumerate(golden["family"]):
+        a = int(golden["addr"][i])
+        if fam == 6:
+            umem[a + 60:a + 62] = np.array([golden["exp_v6"][i]], "<u2").view(np.uint8)
+        else:
+            umem[a + 40:a + 42] = np.array([golden[v4_col][i]], "<u2").view(np.uint8)
+            umem[a + 24:a + 26] = np.array([golden["exp_iphdr"][i]], "<u2").view(np.uint8)
+    return umem
+
+
+VERIFY, IPHDR = 0x10, 0x2
+
+
+def test_verify_accepts_reference_checksums(golden):
+    umem = filled_golden(golden)
+    out = oracle.batch(umem, golden_desc(golden), oracle.MODE_AUTO, VERIFY | IPHDR)
+    assert (out == 0).all()
+
+
+def test_verify_rejects_udp_checksum_quirk_values(golden):
+    """checksum.h's udp_checksum() (single fold) writes values an RFC 768
+    receiver rejects -- exactly on the frames where legacy != RFC."""
+    umem = filled_golden(golden, "exp_legacy")
+    out = oracle.batch(umem, golden_desc(golden), oracle.MODE_AUTO, VERIFY)
+    fam = golden["family"]
+    quirk = (fam == 4) & (golden["exp_legacy"] != golden["exp_rfc"])
+    # a legacy value of 0 means "no checksum" to a receiver: accepted
+    quirk &= golden["exp_legacy"] != 0
+    assert (out[quirk] != 0).all() and (out[~quirk] == 0).all()
+
+
+def test_verify_zero_check_and_corruption(golden):
+    umem = filled_golden(golden)
+    desc = golden_desc(golden)
+    fam = golden["family"]
+    z = umem.copy()
+    for i, d in enumerate(desc):
+        a = int(d["addr"])
+        z[a + (60 if fam[i] == 6 else 40):a + (62 if fam[i] == 6 else 42)] = 0
+    out = oracle.batch(z, desc, oracle.MODE_AUTO, VERIFY)
+    assert (out[fam == 4] == 0).all() and (out[fam == 6] != 0).all()
+    rng = np.random.default_rng(1)
+    c = umem.copy()
+    for i, d in enumerate(desc):       # flip one bit somewhere in each span
+        a, ln = int(d["addr"]), int(d["len"])
+        lo = a + (22 if fam[i] == 6 else 26)
+        c[int(rng.integers(lo, a + ln))] ^= 1 << int(rng.integers(0, 8))
+    out = oracle.batch(c, desc, oracle.MODE_AUTO, VERIFY)
+    assert (out != 0).all()
+    bad_ip = umem.copy()
+    for i in np.nonzero(fam == 4)[0]:
+        bad_ip[int(desc["addr"][i]) + 22] ^= 0x01          # TTL byte
+    assert (oracle.batch(bad_ip, desc, oracle.MODE_AUTO, VERIFY | IPHDR)[fam == 4] != 0).all()
+    assert (oracle.batch(bad_ip, desc, oracle.MODE_AUTO, VERIFY)[fam == 4] == 0).all()
