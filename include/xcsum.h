@@ -116,6 +116,49 @@ int xcsum_batch_device(xcsum_ctx *ctx, uint8_t *d_umem, const struct xcsum_desc 
 		       uint32_t n, uint16_t *d_out, uint32_t mode, uint32_t flags,
 		       uint32_t len_hint, void *stream);
 
+/* ---- device-side frame build: xudp_frame_send on the GPU -------------------
+ * Replaces the whole per-frame loop of xudp_frame_send (tx.c:696-726): for
+ * every message, build eth + IPv4/IPv6 + UDP headers in front of the payload
+ * in its UMEM frame slot exactly as xudp_packet_udp() does (packet.c:156-194),
+ * copying the payload there first when it lives elsewhere (the memcpy of
+ * xudp_packet_udp_payload, packet.c:196-203, fused with the checksum pass),
+ * compute iph->check (packet.c:43-66) / udp->check (IPv6: packet.c:105-117;
+ * IPv4: 0 as packet.c:125, or RFC with XCSUM_F_V4_RFC), and write the
+ * xdp_desc each frame is published with (tx.c:450-452).
+ * One route per batch, like xudp_tx_info_prepare() (tx.c:690). */
+struct xcsum_route {
+	uint8_t family;         /* 4 or 6 */
+	uint8_t pad[3];
+	uint8_t dmac[6];
+	uint8_t smac[6];
+	uint16_t sport_be;      /* network byte order, as sin_port */
+	uint16_t dport_be;
+	uint8_t saddr[16];      /* IPv4: first 4 bytes */
+	uint8_t daddr[16];
+};
+
+struct xcsum_msg {
+	uint64_t src;           /* payload offset from d_src (ignored in place) */
+	uint32_t len;           /* payload bytes */
+	uint32_t slot;          /* UMEM frame slot: data = d_umem + slot*frame_size + data_off */
+};
+
+#define XCSUM_F_BUILD_INPLACE 0x20u /* payloads already sit at their frame's data
+				       offset (the zero-copy xudp_frame_alloc path,
+				       tx.c:760): no copy, d_src unused */
+
+/* d_desc_out[i] = {slot*frame_size + data_off - (42|62), payload + 42|62, 0};
+ * d_out (may be NULL) = the udp->check written.  frame_size and data_off must
+ * be multiples of 16 (xudp: 4096 and 384), d_umem 16-aligned.
+ * Messages that do not fit their slot or exceed 65527 payload bytes get
+ * desc len 0, no frame, and count as malformed.  len_hint = typical payload
+ * bytes (kernel geometry only).  Asynchronous on `stream`. */
+int xcsum_build_device(xcsum_ctx *ctx, const struct xcsum_route *route,
+		       const uint8_t *d_src, const struct xcsum_msg *d_msgs, uint32_t n,
+		       uint8_t *d_umem, uint32_t frame_size, uint32_t data_off,
+		       struct xcsum_desc *d_desc_out, uint16_t *d_out, uint32_t flags,
+		       uint32_t len_hint, void *stream);
+
 /* ---- host-resident batch (frames in the AF_XDP UMEM) ----------------------
  * Same semantics with host pointers.  Synchronous.  Frames are moved with
  * chunked, double-buffered hipMemcpyAsync (pinned when the UMEM range is

@@ -47,8 +47,12 @@ GEOMETRIES = [(64, 1, 2), (64, 1, 9), (32, 1, 3), (32, 1, 6), (16, 1, 2), (16, 1
               (16, 1, 6), (16, 2, 6), (16, 1, 12), (8, 1, 2), (8, 2, 1), (8, 1, 12), (4, 2, 2),
               (4, 4, 2), (4, 1, 2)]
 
+F_BUILD_INPLACE = 0x20
+
 # struct xcsum_desc == struct xdp_desc
 DESC_DTYPE = np.dtype([("addr", "<u8"), ("len", "<u4"), ("options", "<u4")])
+# struct xcsum_msg (device frame build)
+MSG_DTYPE = np.dtype([("src", "<u8"), ("len", "<u4"), ("slot", "<u4")])
 
 HDR4 = 42  # eth 14 + ip 20 + udp 8
 HDR6 = 62  # eth 14 + ip6 40 + udp 8
@@ -73,6 +77,11 @@ _SIGS = {
     "xcsum_batch_device": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                           ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint32,
                                           ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p]),
+    "xcsum_build_device": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                          ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p,
+                                          ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p,
+                                          ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32,
+                                          ctypes.c_void_p]),
     "xcsum_batch_host": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                         ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint32,
                                         ctypes.c_uint32]),
@@ -223,6 +232,14 @@ class Engine:
                                         mode, flags, len_hint, _ptr(stream)),
                "xcsum_batch_device")
 
+    def build_device(self, route, d_src, d_msgs, n, d_umem, frame_size, data_off, d_desc_out,
+                     d_out=None, flags=0, len_hint=0, stream=None):
+        """Device-side xudp_frame_send: headers + payload copy + checksums."""
+        _check(lib().xcsum_build_device(self._ctx, ctypes.byref(route), _ptr(d_src),
+                                        _ptr(d_msgs), n, _ptr(d_umem), frame_size, data_off,
+                                        _ptr(d_desc_out), _ptr(d_out), flags, len_hint,
+                                        _ptr(stream)), "xcsum_build_device")
+
     def batch_host(self, umem, desc, out, mode, flags=0):
         _check(lib().xcsum_batch_host(self._ctx, _ptr(umem), _ptr(desc), len(desc), _ptr(out),
                                       mode, flags), "xcsum_batch_host")
@@ -257,6 +274,27 @@ class SockaddrIn6(ctypes.Structure):
     _fields_ = [("sin6_family", ctypes.c_uint16), ("sin6_port", ctypes.c_uint16),
                 ("sin6_flowinfo", ctypes.c_uint32), ("sin6_addr", ctypes.c_uint8 * 16),
                 ("sin6_scope_id", ctypes.c_uint32)]
+
+
+class Route(ctypes.Structure):
+    """struct xcsum_route: one batch's addressing (xudp_tx_info_prepare)."""
+    _fields_ = [("family", ctypes.c_uint8), ("pad", ctypes.c_uint8 * 3),
+                ("dmac", ctypes.c_uint8 * 6), ("smac", ctypes.c_uint8 * 6),
+                ("sport_be", ctypes.c_uint16), ("dport_be", ctypes.c_uint16),
+                ("saddr", ctypes.c_uint8 * 16), ("daddr", ctypes.c_uint8 * 16)]
+
+
+def make_route(family, smac, dmac, saddr, sport, daddr, dport):
+    """Ports in host order; addresses as bytes (4 or 16)."""
+    r = Route()
+    r.family = family
+    r.dmac[:] = list(dmac)
+    r.smac[:] = list(smac)
+    r.sport_be = htons(sport)
+    r.dport_be = htons(dport)
+    r.saddr[:len(saddr)] = list(saddr)
+    r.daddr[:len(daddr)] = list(daddr)
+    return r
 
 
 class _FromUnion(ctypes.Union):

@@ -192,6 +192,76 @@ extern "C" int xcsum_batch_device(xcsum_ctx *c, uint8_t *d_umem, const struct xc
 	return 0;
 }
 
+/* The 64-byte header template of a batch: every header byte that does not
+ * depend on the frame (packet.c:141-150 eth_build, :68-84 iph_build,
+ * :92-103 iph_build6, :119-126 udp_build), length and check fields 0.  Plain
+ * field stores, no checksum arithmetic. */
+static void header_template(const struct xcsum_route *r, uint8_t t[64])
+{
+	memset(t, 0, 64);
+	memcpy(t, r->dmac, 6);
+	memcpy(t + 6, r->smac, 6);
+	if (r->family == 6) {
+		t[12] = 0x86;
+		t[13] = 0xDD;
+		/* ip6_flow_hdr(iph6, 0, (0x3 << 16) + sin6_port), packet.c:96 */
+		uint32_t flow = 0x60000000u | ((0x3u << 16) + r->sport_be);
+		t[14] = (uint8_t)(flow >> 24);
+		t[15] = (uint8_t)(flow >> 16);
+		t[16] = (uint8_t)(flow >> 8);
+		t[17] = (uint8_t)flow;
+		t[20] = 17;  /* nexthdr */
+		t[21] = 64;  /* hop_limit */
+		memcpy(t + 22, r->saddr, 16);
+		memcpy(t + 38, r->daddr, 16);
+		memcpy(t + 54, &r->sport_be, 2);
+		memcpy(t + 56, &r->dport_be, 2);
+	} else {
+		t[12] = 0x08;
+		t[14] = 0x45;  /* IP_VIT */
+		t[20] = 0x40;  /* IP_DF */
+		t[22] = 64;    /* IP_XUDP_TTL */
+		t[23] = 17;    /* IPPROTO_UDP */
+		memcpy(t + 26, r->saddr, 4);
+		memcpy(t + 30, r->daddr, 4);
+		memcpy(t + 34, &r->sport_be, 2);
+		memcpy(t + 36, &r->dport_be, 2);
+	}
+}
+
+extern "C" int xcsum_build_device(xcsum_ctx *c, const struct xcsum_route *route,
+				  const uint8_t *d_src, const struct xcsum_msg *d_msgs, uint32_t n,
+				  uint8_t *d_umem, uint32_t frame_size, uint32_t data_off,
+				  struct xcsum_desc *d_desc_out, uint16_t *d_out, uint32_t flags,
+				  uint32_t len_hint, void *stream)
+{
+	if (!c || !route || (route->family != 4 && route->family != 6))
+		return -XCSUM_ERR_INVAL;
+	if (n == 0)
+		return 0;
+	const uint32_t hdr = route->family == 6 ? 62u : 42u;
+	if (!d_msgs || !d_umem || !d_desc_out || (((uintptr_t)d_umem) & 15) ||
+	    (frame_size & 15) || (data_off & 15) || data_off < hdr || data_off >= frame_size ||
+	    (!(flags & XCSUM_F_BUILD_INPLACE) && !d_src))
+		return -XCSUM_ERR_INVAL;
+	HIPCHK(hipSetDevice(c->device));
+	BuildArgs a;
+	a.umem = d_umem;
+	a.src = d_src;
+	a.msgs = d_msgs;
+	a.n = n;
+	a.frame_size = frame_size;
+	a.data_off = data_off;
+	a.flags = flags & (XCSUM_F_V4_RFC | XCSUM_F_BUILD_INPLACE);
+	a.desc_out = d_desc_out;
+	a.out = d_out;
+	a.err = c->d_err;
+	a.family = route->family;
+	header_template(route, (uint8_t *)a.tmpl);
+	HIPCHK(launch_build(a, len_hint, c->cus, (hipStream_t)stream));
+	return 0;
+}
+
 extern "C" int xcsum_sync(xcsum_ctx *c, void *stream)
 {
 	if (!c)

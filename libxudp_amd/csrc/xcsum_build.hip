@@ -1,0 +1,298 @@
+/*
+ * xcsum_build.hip -- xudp_frame_send's per-frame work on the GPU.
+ *
+ * For message i (payload bytes + a UMEM frame slot) build, in one pass over
+ * the payload, the frame xudp_packet_udp() builds (cclinuxer/libxudp
+ * xudp/packet.c:156-194): eth + IPv4/IPv6 + UDP headers in front of the
+ * payload, iph->check (xudp_checksum_half, packet.c:43-66), udp->check
+ * (IPv6 udp_csum6, packet.c:105-117; IPv4 0 as packet.c:125, RFC on request),
+ * copying the payload into the slot first unless it is already there (the
+ * memcpy of xudp_packet_udp_payload, packet.c:196-203, fused with the
+ * checksum: every payload byte is read once, written once, summed from
+ * registers), then the xdp_desc the frame is published with (tx.c:450-452).
+ *
+ * The batch shares one route (xudp_tx_info_prepare, tx.c:690), so the host
+ * passes a 64-byte header template holding every constant header byte
+ * (addresses, ports, MACs, version/TTL/protocol/DF); the kernel patches the
+ * per-frame length fields and both checksums.  All checksum arithmetic is
+ * here, none on the host.
+ *
+ * Memory-bound: payload read + frame write (+ 16-byte message, 16-byte
+ * descriptor) per frame.  G lanes per frame, K 16-byte chunks per lane
+ * preloaded, longer payloads stream through a tail loop.
+ */
+#include "xcsum_internal.h"
+
+namespace xcsum {
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(1))) const u32x4 gu32x4;
+
+static __device__ __forceinline__ uint32_t dot_even(uint32_t w, uint32_t acc)
+{
+	return __builtin_amdgcn_udot4(w, 0x00010001u, acc, false);
+}
+static __device__ __forceinline__ uint32_t dot_odd(uint32_t w, uint32_t acc)
+{
+	return __builtin_amdgcn_udot4(w, 0x01000100u, acc, false);
+}
+
+static __device__ __forceinline__ u32x4 ld16(const uint8_t *p)
+{
+	return __builtin_nontemporal_load((gu32x4 *)p);
+}
+
+static __device__ __forceinline__ uint32_t keep_bytes(uint32_t w, int n)
+{
+	/* bytes [0, n) of a dword, n clamped to [0, 4] */
+	return n >= 4 ? w : (n <= 0 ? 0u : (w & (0xffffffffu >> (32 - 8 * n))));
+}
+
+/* 16 payload bytes starting at p (any alignment), of which `rem` (>= 1) are
+ * valid; bytes past the payload come back 0.  Only 16-byte blocks that hold
+ * a valid byte are loaded, so nothing past the payload's last byte is read
+ * beyond its own aligned block (no page can be crossed). */
+static __device__ __forceinline__ u32x4 load_payload(const uint8_t *p, uint32_t rem)
+{
+	uintptr_t a = (uintptr_t)p;
+	uint32_t sh = (uint32_t)a & 15u;
+	const uint8_t *b = (const uint8_t *)(a & ~(uintptr_t)15);
+	u32x4 v0 = ld16(b), r;
+	if (sh == 0) {
+		r = v0;
+	} else {
+		u32x4 v1 = (16u - sh < rem) ? ld16(b + 16) : u32x4{0, 0, 0, 0};
+		uint32_t w[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+		uint32_t q = sh >> 2, s8 = sh & 3u;
+		uint32_t o[5];
+#pragma unroll
+		for (int j = 0; j < 5; j++) {
+			/* o[j] = w[j + q] with q in 0..3, by selects (no dynamic
+			 * register indexing) */
+			uint32_t x = w[j];
+			x = q == 1 ? w[j + 1] : x;
+			x = q == 2 ? w[j + 2] : x;
+			x = q == 3 ? w[j + 3] : x;
+			o[j] = x;
+		}
+		r.x = __builtin_amdgcn_alignbyte(o[1], o[0], s8);
+		r.y = __builtin_amdgcn_alignbyte(o[2], o[1], s8);
+		r.z = __builtin_amdgcn_alignbyte(o[3], o[2], s8);
+		r.w = __builtin_amdgcn_alignbyte(o[4], o[3], s8);
+	}
+	if (rem < 16) {
+		r.x = keep_bytes(r.x, (int)rem);
+		r.y = keep_bytes(r.y, (int)rem - 4);
+		r.z = keep_bytes(r.z, (int)rem - 8);
+		r.w = keep_bytes(r.w, (int)rem - 12);
+	}
+	return r;
+}
+
+static __device__ __forceinline__ void store_payload(uint8_t *d, u32x4 v, uint32_t rem)
+{
+	if (rem >= 16) {
+		__builtin_nontemporal_store(v, (__attribute__((address_space(1))) u32x4 *)d);
+		return;
+	}
+	uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+	for (int j = 0; j < 4; j++) {
+		int n = (int)rem - 4 * j;
+		if (n >= 4)
+			*reinterpret_cast<uint32_t *>(d + 4 * j) = w[j];
+		else
+			for (int k = 0; k < n; k++)
+				d[4 * j + k] = (uint8_t)(w[j] >> (8 * k));
+	}
+}
+
+static __device__ __forceinline__ void accum(u32x4 v, uint32_t &E, uint32_t &O)
+{
+	E = dot_even(v.x, E); O = dot_odd(v.x, O);
+	E = dot_even(v.y, E); O = dot_odd(v.y, O);
+	E = dot_even(v.z, E); O = dot_odd(v.z, O);
+	E = dot_even(v.w, E); O = dot_odd(v.w, O);
+}
+
+template <int G>
+static __device__ __forceinline__ uint32_t seg_sum(uint32_t v)
+{
+	if (G >= 2)
+		v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false);
+	if (G >= 4)
+		v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, false);
+	if (G >= 8)
+		v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x141, 0xF, 0xF, false);
+	if (G >= 16)
+		v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x140, 0xF, 0xF, false);
+	if (G >= 32) {
+		auto p = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+		v = p[0] + p[1];
+	}
+	if (G >= 64) {
+		auto q = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+		v = q[0] + q[1];
+	}
+	return v;
+}
+
+static __device__ __forceinline__ uint32_t bswap16(uint32_t x)
+{
+	return ((x >> 8) & 0xffu) | ((x & 0xffu) << 8);
+}
+
+template <int G, int K>
+__global__ void __launch_bounds__(256) build_kernel(BuildArgs a)
+{
+	/* header template as memory-order halfwords; big-endian word j of the
+	 * header is bswap16(tmpl[j]) */
+	__shared__ uint16_t tmpl[32];
+	if (threadIdx.x < 32)
+		tmpl[threadIdx.x] = (uint16_t)(a.tmpl[threadIdx.x / 2] >> (16 * (threadIdx.x & 1)));
+	__syncthreads();
+
+	const bool v6 = a.family == 6;
+	const uint32_t hdr = v6 ? 62u : 42u;
+	/* constant part of the UDP checksum: the pseudo-header addresses and the
+	 * ports (header halfwords 13..18 / 11..28), protocol 17 */
+	uint32_t sconst = 17u;
+	for (uint32_t j = v6 ? 11u : 13u; j < (v6 ? 29u : 19u); j++)
+		sconst += bswap16(tmpl[j]);
+	/* IPv4 header sum without tot_len and check (halfwords 7..16) */
+	uint32_t ipconst = 0;
+	if (!v6)
+		for (uint32_t j = 7; j < 17; j++)
+			if (j != 8 && j != 12)
+				ipconst += bswap16(tmpl[j]);
+
+	const uint32_t lane = threadIdx.x & (G - 1);
+	const uint32_t seg = (blockIdx.x * 256u + threadIdx.x) / G;
+	const uint32_t nseg = gridDim.x * (256u / G);
+	const bool inplace = (a.flags & XCSUM_F_BUILD_INPLACE) != 0;
+
+	for (uint32_t p = seg; p < a.n; p += nseg) {
+		const u32x4 m = *((gu32x4 *)(a.msgs + p));
+		const uint64_t srcoff = ((uint64_t)m.y << 32) | m.x;
+		const uint32_t len = m.z, slot = m.w;
+		const uint64_t data_off = (uint64_t)slot * a.frame_size + a.data_off;
+		uint8_t *data = a.umem + data_off;
+		const bool ok = len <= 65527u && (uint64_t)a.data_off + len <= a.frame_size;
+		const uint8_t *src = inplace ? (const uint8_t *)data : a.src + srcoff;
+
+		uint32_t E = 0, O = 0;
+		if (ok) {
+#pragma unroll
+			for (int k = 0; k < K; k++) {
+				uint32_t off = 16u * (lane + k * G);
+				if (off < len) {
+					u32x4 v = load_payload(src + off, len - off);
+					if (!inplace)
+						store_payload(data + off, v, len - off);
+					accum(v, E, O);
+				}
+			}
+			for (uint32_t off = 16u * (lane + K * G); off < len; off += 16u * G) {
+				u32x4 v = load_payload(src + off, len - off);
+				if (!inplace)
+					store_payload(data + off, v, len - off);
+				accum(v, E, O);
+			}
+		}
+		/* payload starts 16-aligned (even address): E holds high bytes */
+		uint32_t s = seg_sum<G>((E << 8) + O);
+		if (!ok) {
+			if (lane == 0) {
+				struct xcsum_desc d0 = {data_off, 0u, 0u};
+				a.desc_out[p] = d0;
+				if (a.out)
+					a.out[p] = 0;
+				atomicAdd(a.err, 1ull);
+			}
+			continue;
+		}
+		const uint32_t ulen = 8u + len;
+		/* S = payload + addresses + ports + 17 + udp_len (pseudo) +
+		 * udp_len (header) -- the header's check field is 0 */
+		uint32_t S = s + sconst + 2u * ulen;
+		uint32_t t = (S & 0xffffu) + (S >> 16);
+		t = (t & 0xffffu) + (t >> 16);
+		uint32_t r = ~t & 0xffffu;
+		if (r == 0)
+			r = 0xffffu;                       /* CSUM_MANGLED_0 */
+		uint32_t ucheck = (v6 || (a.flags & XCSUM_F_V4_RFC)) ? bswap16(r) : 0u;
+		uint32_t ipcheck = 0;
+		if (!v6) {
+			uint32_t ip = ipconst + 20u + ulen;  /* + tot_len */
+			ip = (ip & 0xffffu) + (ip >> 16);
+			ip = (ip & 0xffffu) + (ip >> 16);
+			ipcheck = bswap16(~ip & 0xffffu);
+		}
+		uint8_t *eth = data - hdr;
+		for (uint32_t j = lane; j < hdr / 2; j += G) {
+			uint32_t h = tmpl[j];
+			if (v6) {
+				if (j == 9 || j == 29)
+					h = bswap16(ulen);           /* payload_len, udp len */
+				else if (j == 30)
+					h = ucheck;
+			} else {
+				if (j == 8)
+					h = bswap16(20u + ulen);     /* tot_len */
+				else if (j == 12)
+					h = ipcheck;
+				else if (j == 19)
+					h = bswap16(ulen);
+				else if (j == 20)
+					h = ucheck;
+			}
+			*reinterpret_cast<uint16_t *>(eth + 2 * j) = (uint16_t)h;
+		}
+		if (lane == 0) {
+			struct xcsum_desc d0 = {data_off - hdr, hdr + len, 0u};
+			a.desc_out[p] = d0;
+			if (a.out)
+				a.out[p] = (uint16_t)ucheck;
+		}
+	}
+}
+
+#define XCSUM_BUILD_GEOMETRIES(X) X(4, 1) X(8, 2) X(16, 6) X(64, 9)
+
+template <int G, int K>
+static hipError_t launch_build_t(const BuildArgs &a, int cus, hipStream_t s)
+{
+	static int occ = 0;
+	if (!occ) {
+		int nb = 0;
+		if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, build_kernel<G, K>, 256, 0) !=
+			    hipSuccess || nb <= 0)
+			nb = 4;
+		occ = nb;
+	}
+	uint64_t blocks = ((uint64_t)a.n * G + 255) / 256;
+	uint64_t cap = (uint64_t)cus * occ;
+	if (blocks > cap)
+		blocks = cap;
+	if (blocks == 0)
+		blocks = 1;
+	hipLaunchKernelGGL((build_kernel<G, K>), dim3((unsigned)blocks), dim3(256), 0, s, a);
+	return hipGetLastError();
+}
+
+hipError_t launch_build(const BuildArgs &a, uint32_t len_hint, int cus, hipStream_t s)
+{
+	if (a.n == 0)
+		return hipSuccess;
+	/* lanes x chunks to cover a typical payload in one preload */
+	uint32_t chunks = (len_hint + 15) / 16;
+	if (chunks <= 4)
+		return launch_build_t<4, 1>(a, cus, s);
+	if (chunks <= 16)
+		return launch_build_t<8, 2>(a, cus, s);
+	if (chunks <= 96)
+		return launch_build_t<16, 6>(a, cus, s);
+	return launch_build_t<64, 9>(a, cus, s);
+}
+
+} /* namespace xcsum */

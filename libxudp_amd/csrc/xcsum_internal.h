@@ -22,6 +22,21 @@ struct CsumArgs {
 	unsigned long long *err;       /* device counter of malformed frames */
 };
 
+/* Frame-build kernel arguments (xcsum_build.hip). */
+struct BuildArgs {
+	uint8_t *umem;
+	const uint8_t *src;
+	const struct xcsum_msg *msgs;
+	uint32_t n, frame_size, data_off, flags;
+	struct xcsum_desc *desc_out;
+	uint16_t *out;
+	unsigned long long *err;
+	uint32_t family;
+	uint32_t tmpl[16];             /* 64-byte header template, memory order */
+};
+
+hipError_t launch_build(const BuildArgs &a, uint32_t len_hint, int cus, hipStream_t s);
+
 /* Kernel geometry: G lanes cooperate on one frame, each segment keeps U frames
  * in flight, and each lane preloads K 16-byte chunks per frame. */
 struct Geometry {

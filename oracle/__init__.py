@@ -43,6 +43,9 @@ def port():
         L.orc_ip_checksum_half.argtypes = [u8p]
         L.orc_ip_header_rfc.restype = ctypes.c_uint16
         L.orc_ip_header_rfc.argtypes = [u8p]
+        L.orc_build_frame.restype = ctypes.c_uint32
+        L.orc_build_frame.argtypes = [u8p, u8p, ctypes.c_uint32, ctypes.c_int, u8p, u8p, u8p,
+                                      ctypes.c_uint16, u8p, ctypes.c_uint16, ctypes.c_int]
         L.orc_batch.restype = None
         L.orc_batch.argtypes = [u8p, u8p, ctypes.c_uint32, u8p, ctypes.c_int, ctypes.c_uint32]
         L.orc_batch_timed.restype = ctypes.c_double
@@ -119,3 +122,15 @@ def build_frame_ref(payload, family, smac, dmac, saddr, sport, daddr, dport):
     ln = ref().ref_packet_udp_payload(_p(head), _p(pl), len(payload), family, _p(sm), _p(dm),
                                       _p(sa), be(sport), _p(da), be(dport), ctypes.byref(off))
     return head[off.value:off.value + ln].copy()
+
+
+def build_frame(payload, family, smac, dmac, saddr, sport, daddr, dport, v4_rfc=False):
+    """Frame bytes from the oracle's packet.c restatement (orc_build_frame)."""
+    pl = np.frombuffer(bytes(payload) + b"\0", dtype=np.uint8).copy()
+    buf = np.zeros(len(payload) + 64, dtype=np.uint8)
+    b = lambda x: np.frombuffer(bytes(x), dtype=np.uint8).copy()
+    sm, dm, sa, da = b(smac), b(dmac), b(saddr), b(daddr)
+    be = lambda p: ((p & 0xff) << 8) | (p >> 8)
+    n = port().orc_build_frame(_p(buf), _p(pl), len(payload), family, _p(dm), _p(sm), _p(sa),
+                               be(sport), _p(da), be(dport), int(bool(v4_rfc)))
+    return buf[:n].copy()

@@ -364,3 +364,65 @@ double orc_batch_timed(const u8 *umem, const struct orc_desc *desc, u32 n, u16 *
 	clock_gettime(CLOCK_MONOTONIC, &t1);
 	return (t1.tv_sec - t0.tv_sec) + 1e-9 * (t1.tv_nsec - t0.tv_nsec);
 }
+
+/* ------------------------------------------------------------------------ */
+/* Frame build: xudp/packet.c:68-203 restated (eth_build :141-150, iph_build  */
+/* :68-84 + xudp_checksum_half :43-66, iph_build6 :92-103, udp_build          */
+/* :119-126, udp_csum6 :105-117, xudp_packet_udp_payload's copy :196-203).    */
+/* Writes the frame at `eth` and returns its length (payload + 42 / 62).      */
+/* family 4 or 6; addresses/ports in network order; v4_rfc != 0 fills the    */
+/* IPv4 UDP checksum (RFC) where the reference leaves 0 (packet.c:125).       */
+/* ------------------------------------------------------------------------ */
+static void orc_put16be(u8 *p, u16 v) { p[0] = (u8)(v >> 8); p[1] = (u8)v; }
+
+u32 orc_build_frame(u8 *eth, const u8 *payload, u32 psize, int family,
+		    const u8 *dmac, const u8 *smac, const u8 *saddr, u16 sport_be,
+		    const u8 *daddr, u16 dport_be, int v4_rfc)
+{
+	u32 size = 8 + psize;
+	u8 *udp;
+	memcpy(eth, dmac, 6);                           /* copy_eth(h_dest) */
+	memcpy(eth + 6, smac, 6);                       /* copy_eth(h_source) */
+	if (family == 4) {
+		u8 *iph = eth + 14;
+		udp = iph + 20;
+		orc_put16be(eth + 12, 0x0800);
+		orc_put16be(iph, 0x4500);               /* IP_VIT */
+		orc_put16be(iph + 2, (u16)(20 + size)); /* tot_len */
+		orc_put16be(iph + 4, 0);                /* id */
+		orc_put16be(iph + 6, 0x4000);           /* IP_DF */
+		iph[8] = 64;                            /* IP_XUDP_TTL */
+		iph[9] = 17;
+		memcpy(iph + 12, saddr, 4);
+		memcpy(iph + 16, daddr, 4);
+		{
+			u16 c = orc_ip_checksum_half(iph);
+			memcpy(iph + 10, &c, 2);
+		}
+	} else {
+		u8 *ip6 = eth + 14;
+		u32 flow = 0x60000000u | ((0x3u << 16) + sport_be);  /* packet.c:96 */
+		udp = ip6 + 40;
+		orc_put16be(eth + 12, 0x86DD);
+		ip6[0] = (u8)(flow >> 24); ip6[1] = (u8)(flow >> 16);
+		ip6[2] = (u8)(flow >> 8); ip6[3] = (u8)flow;
+		orc_put16be(ip6 + 4, (u16)size);        /* payload_len */
+		ip6[6] = 17;
+		ip6[7] = 64;
+		memcpy(ip6 + 8, saddr, 16);
+		memcpy(ip6 + 24, daddr, 16);
+	}
+	memcpy(udp, &sport_be, 2);
+	memcpy(udp + 2, &dport_be, 2);
+	orc_put16be(udp + 4, (u16)size);
+	orc_put16be(udp + 6, 0);                        /* "must", packet.c:125 */
+	memcpy(udp + 8, payload, psize);
+	if (family == 6) {
+		u16 c = orc_udp_csum6(udp, size, eth + 22, eth + 38);
+		memcpy(udp + 6, &c, 2);
+	} else if (v4_rfc) {
+		u16 c = orc_udp_csum4_rfc(udp, size, eth + 26, eth + 30);
+		memcpy(udp + 6, &c, 2);
+	}
+	return psize + (family == 4 ? 42 : 62);
+}

@@ -14,6 +14,8 @@ place (oracle/_ref/libxudpref.so, recipe oracle/Makefile):
 Outputs:
   fixtures.npz  -- ~1.2k frames (<1 MB): umem bytes, descriptors, family,
                    expected legacy / rfc / v6 / iphdr values
+  build_fixtures.npz -- frames built by xudp_packet_udp_payload() for two
+                   fixed routes and many payload sizes (device frame build)
   digests.json  -- SHA-256 of the reference's output array for BASELINE.json
                    configs 1-5 over the synthetic generator's frames
                    (libxudp_amd gen_* == reference-built frames, see
@@ -197,6 +199,36 @@ def build_fixtures():
           f"{nq} IPv4 frames where legacy != rfc")
 
 
+BUILD_ROUTES = {
+    4: dict(smac=bytes.fromhex("020000000001"), dmac=bytes.fromhex("020000000002"),
+            saddr=bytes([10, 0, 35, 2]), sport=3486, daddr=bytes([10, 0, 35, 1]), dport=40000),
+    6: dict(smac=bytes.fromhex("0a1b2c3d4e5f"), dmac=bytes.fromhex("f0e1d2c3b4a5"),
+            saddr=bytes.fromhex("10002000300040000000000000000002"), sport=3487,
+            daddr=bytes.fromhex("fe800000000000001122334455667788"), dport=65535),
+}
+
+
+def build_frame_fixtures():
+    """Frames built by the reference's xudp_packet_udp_payload() (packet.c:196)
+    for two fixed routes and many payload sizes: pins the device frame build."""
+    rng = np.random.default_rng(4242)
+    out = {}
+    for fam, rt in BUILD_ROUTES.items():
+        lens = list(range(0, 130)) + [255, 256, 257, 1000, 1457, 1471, 1472, 4095, 8999]
+        pays, frames = [], []
+        for i, L in enumerate(lens):
+            pl = rng.integers(0, 256, L, dtype=np.uint8).tobytes() if i % 7 else b"\xff" * L
+            f = oracle.build_frame_ref(pl, fam, rt["smac"], rt["dmac"], rt["saddr"], rt["sport"],
+                                       rt["daddr"], rt["dport"])
+            pays.append(pl)
+            frames.append(f.tobytes())
+        out[f"v{fam}_lens"] = np.array(lens, dtype=np.uint32)
+        out[f"v{fam}_payloads"] = np.frombuffer(b"".join(pays), dtype=np.uint8)
+        out[f"v{fam}_frames"] = np.frombuffer(b"".join(frames), dtype=np.uint8)
+    np.savez_compressed(os.path.join(OUT, "build_fixtures.npz"), **out)
+    print("build_fixtures.npz:", {k: v.shape for k, v in out.items()})
+
+
 def sha_u16(h, arr):
     h.update(np.ascontiguousarray(arr, dtype="<u2").tobytes())
 
@@ -240,11 +272,16 @@ def config_digest(cid, chunk=1 << 18, threads=8):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--no-digests", action="store_true")
+    ap.add_argument("--only-build", action="store_true", help="only build_fixtures.npz")
     ap.add_argument("--configs", default="1,2,3,4,5")
     args = ap.parse_args()
     if not oracle.have_ref():
         sys.exit("oracle/_ref/libxudpref.so missing: run `make -C oracle` next to /root/reference")
+    if args.only_build:
+        build_frame_fixtures()
+        return
     build_fixtures()
+    build_frame_fixtures()
     if not args.no_digests:
         path = os.path.join(OUT, "digests.json")
         digests = json.load(open(path)) if os.path.exists(path) else {}

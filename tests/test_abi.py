@@ -35,13 +35,13 @@ def test_library_loads():
 
 def test_every_declared_function_is_exported():
     decl = declared_functions()
-    assert len(decl) == 19, decl
+    assert set(decl) == set(X._SIGS), set(decl) ^ set(X._SIGS)
     missing = sorted(set(decl) - exported_symbols())
     assert not missing, missing
 
 
 def test_python_binding_covers_the_abi():
-    assert set(declared_functions()) <= set(X._SIGS)
+    assert len(declared_functions()) >= 20
 
 
 def test_struct_layouts_match_c():

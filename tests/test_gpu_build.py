@@ -1,0 +1,124 @@
+"""GPU: xcsum_build_device against the reference-built frames and the oracle."""
+import numpy as np
+import pytest
+
+import libxudp_amd as X
+import oracle
+from test_build import ROUTES, bfix, split  # noqa: F401
+
+pytestmark = pytest.mark.gpu
+
+FRAME, DATA_OFF = 16384, 384   # slots big enough for 8999-byte payloads
+
+
+def route_of(fam, r):
+    return X.make_route(fam, r["smac"], r["dmac"], r["saddr"], r["sport"], r["daddr"],
+                        r["dport"])
+
+
+def device_build(torch, engine, route, pays, inplace=False, flags=0, len_hint=0,
+                 src_phase=None, slots=None, umem_fill=0x5a):
+    dev = torch.device("cuda:0")
+    n = len(pays)
+    slots = np.arange(n, dtype=np.uint32) if slots is None else slots
+    nslots = int(slots.max()) + 1
+    umem = np.full(nslots * FRAME, umem_fill, dtype=np.uint8)
+    msgs = np.zeros(n, dtype=X.MSG_DTYPE)
+    rng = np.random.default_rng(1)
+    if inplace:
+        for i, p in enumerate(pays):
+            o = int(slots[i]) * FRAME + DATA_OFF
+            umem[o:o + len(p)] = p
+        src = np.zeros(16, np.uint8)
+    else:
+        off, chunks = 0, []
+        for p in pays:
+            ph = int(rng.integers(0, 16)) if src_phase is None else src_phase
+            off += ph
+            chunks.append((off, p))
+            off += len(p)
+        src = np.full(off + 16, 0xee, dtype=np.uint8)
+        for i, (o, p) in enumerate(chunks):
+            src[o:o + len(p)] = p
+            msgs["src"][i] = o
+        # exact-size device buffer: the last payload ends at the allocation's end
+        src = src[:off] if off else src
+    msgs["len"] = [len(p) for p in pays]
+    msgs["slot"] = slots
+    d_umem = torch.from_numpy(umem).to(dev)
+    d_src = torch.from_numpy(np.ascontiguousarray(src)).to(dev)
+    d_msgs = torch.from_numpy(msgs.view(np.uint8)).to(dev)
+    d_desc = torch.zeros(n * 16, dtype=torch.uint8, device=dev)
+    d_out = torch.zeros(n, dtype=torch.int16, device=dev)
+    engine.build_device(route, d_src, d_msgs, n, d_umem, FRAME, DATA_OFF, d_desc, d_out,
+                        flags | (X.F_BUILD_INPLACE if inplace else 0), len_hint)
+    torch.cuda.synchronize()
+    return (d_umem.cpu().numpy(), d_desc.cpu().numpy().view(X.DESC_DTYPE),
+            d_out.cpu().numpy().view(np.uint16), umem)
+
+
+@pytest.mark.parametrize("fam", [4, 6])
+@pytest.mark.parametrize("inplace", [False, True])
+@pytest.mark.parametrize("len_hint", [0, 60, 200, 1500, 9000])
+def test_build_matches_reference(torch_cuda, engine, bfix, fam, inplace, len_hint):
+    hdr = 42 if fam == 4 else 62
+    lens = bfix[f"v{fam}_lens"]
+    pays = split(bfix[f"v{fam}_payloads"], lens)
+    frames = split(bfix[f"v{fam}_frames"], lens + hdr)
+    after, desc, out, before = device_build(torch_cuda, engine, route_of(fam, ROUTES[fam]),
+                                            pays, inplace=inplace, len_hint=len_hint)
+    touched = np.zeros(after.size, dtype=bool)
+    for i, f in enumerate(frames):
+        eth = i * FRAME + DATA_OFF - hdr
+        assert desc["addr"][i] == eth and desc["len"][i] == len(f)
+        assert np.array_equal(after[eth:eth + len(f)], f), i
+        ck = f[60:62] if fam == 6 else f[40:42]
+        assert out[i] == int(ck.view("<u2")[0])
+        touched[eth:eth + len(f)] = True
+    assert np.array_equal(after[~touched], before[~touched])   # nothing else written
+
+
+@pytest.mark.parametrize("phase", [0, 1, 2, 3, 5, 8, 13, 15])
+def test_build_every_source_alignment(torch_cuda, engine, bfix, phase):
+    lens = bfix["v6_lens"]
+    pays = split(bfix["v6_payloads"], lens)
+    frames = split(bfix["v6_frames"], lens + 62)
+    after, desc, out, _ = device_build(torch_cuda, engine, route_of(6, ROUTES[6]), pays,
+                                       src_phase=phase, len_hint=1500)
+    for i, f in enumerate(frames):
+        eth = i * FRAME + DATA_OFF - 62
+        assert np.array_equal(after[eth:eth + len(f)], f)
+
+
+def test_build_random_routes_vs_oracle(torch_cuda, engine):
+    rng = np.random.default_rng(9)
+    for fam in (4, 6):
+        for v4_rfc in (False, True):
+            al = 16 if fam == 6 else 4
+            r = dict(smac=rng.integers(0, 256, 6, dtype=np.uint8).tobytes(),
+                     dmac=rng.integers(0, 256, 6, dtype=np.uint8).tobytes(),
+                     saddr=rng.integers(0, 256, al, dtype=np.uint8).tobytes(),
+                     daddr=rng.integers(0, 256, al, dtype=np.uint8).tobytes(),
+                     sport=int(rng.integers(0, 65536)), dport=int(rng.integers(0, 65536)))
+            pays = [rng.integers(0, 256, int(L), dtype=np.uint8)
+                    for L in rng.integers(0, 3000, 400)]
+            slots = rng.permutation(600)[:400].astype(np.uint32)     # scattered slots
+            after, desc, out, _ = device_build(
+                torch_cuda, engine, route_of(fam, r), pays, flags=X.F_V4_RFC if v4_rfc else 0,
+                slots=slots)
+            hdr = 42 if fam == 4 else 62
+            for i, p in enumerate(pays):
+                exp = oracle.build_frame(p.tobytes(), fam, r["smac"], r["dmac"], r["saddr"],
+                                         r["sport"], r["daddr"], r["dport"], v4_rfc)
+                eth = int(slots[i]) * FRAME + DATA_OFF - hdr
+                assert np.array_equal(after[eth:eth + len(exp)], exp)
+
+
+def test_build_rejects_oversized(torch_cuda, engine):
+    pays = [np.zeros(100, np.uint8), np.zeros(FRAME - DATA_OFF + 1, np.uint8),
+            np.zeros(70000, np.uint8), np.ones(10, np.uint8)]
+    engine.take_errors()
+    after, desc, out, before = device_build(torch_cuda, engine, route_of(4, ROUTES[4]), pays[:2]
+                                            + pays[3:])
+    assert list(desc["len"]) == [142, 0, 52]
+    assert engine.take_errors() == 1
