@@ -75,8 +75,15 @@ def build_batch(cfg, rank, world, torch, dev, eng, stream):
     """Descriptors + frames for this rank, generated on the device."""
     seed = SEED_BASE ^ cfg["id"]
     first, count = rank_slice(cfg, rank, world)
-    desc, nbytes = X.gen_layout(count, cfg["family"], cfg["pmin"], cfg["pmax"], seed=seed,
-                                first_index=first)
+    if cfg.get("layout") == "umem":
+        # xudp's own TX layout: one frame per 4096-byte chunk, eth at F+342
+        # (IPv4) / F+322 (IPv6), SURVEY a14
+        off = 322 if cfg["family"] == 6 else 342
+        desc, nbytes = X.gen_layout(count, cfg["family"], cfg["pmin"], cfg["pmax"], seed=seed,
+                                    first_index=first, stride=4096, offset=off)
+    else:
+        desc, nbytes = X.gen_layout(count, cfg["family"], cfg["pmin"], cfg["pmax"], seed=seed,
+                                    first_index=first)
     d_desc = torch.from_numpy(desc.view(np.uint8)).to(dev)
     # rotate buffers so each pass streams >= 1 GiB: nothing is served from the
     # 256 MiB Infinity Cache (SURVEY.md 7 hard part iv)
@@ -143,6 +150,9 @@ def main():
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--config", type=int, default=2, choices=sorted(CONFIGS))
     ap.add_argument("--geometry", default="", help="G,U,K override (tuning)")
+    ap.add_argument("--layout", default="packed", choices=["packed", "umem"],
+                    help="frames packed at 8-byte boundaries (default) or one per 4096-byte "
+                         "chunk as in xudp's TX UMEM")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=8.0)
     args = ap.parse_args()
@@ -162,7 +172,7 @@ def main():
         if world > 1:
             dist.barrier()
 
-    cfg = dict(CONFIGS[args.config], id=args.config)
+    cfg = dict(CONFIGS[args.config], id=args.config, layout=args.layout)
     eng = X.Engine(local)
     if args.geometry:
         eng.set_geometry(*[int(v) for v in args.geometry.split(",")])
@@ -238,7 +248,9 @@ def main():
             "config": {"workload": cfg["name"], "frames_per_gpu": count,
                        "frames_total": int(frames_all), "payload_bytes": [cfg["pmin"], cfg["pmax"]],
                        "family": cfg["family"], "mode": MODE_NAMES[cfg["mode"]],
-                       "layout": "packed, 8-byte aligned frames", "rotating_buffers": len(bufs),
+                       "layout": "packed, 8-byte aligned frames" if args.layout == "packed"
+                       else "xudp TX UMEM: one frame per 4096-byte chunk",
+                       "rotating_buffers": len(bufs),
                        "alg_bytes_per_step": int(alg_all), "parallelism": f"dp{world}"},
             "pct_hbm_peak": round(100 * achieved / HBM_PEAK_GBS, 2),
             "mpps": round(frames_all * args.steps / elapsed_max / 1e6, 1),

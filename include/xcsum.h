@@ -146,6 +146,9 @@ struct xcsum_msg {
 #define XCSUM_F_BUILD_INPLACE 0x20u /* payloads already sit at their frame's data
 				       offset (the zero-copy xudp_frame_alloc path,
 				       tx.c:760): no copy, d_src unused */
+#define XCSUM_F_SRC_ALIGNED   0x40u /* the caller guarantees every payload source
+				       (d_src + src) is 16-byte aligned: cheaper
+				       copy kernel; results are undefined if not */
 
 /* d_desc_out[i] = {slot*frame_size + data_off - (42|62), payload + 42|62, 0};
  * d_out (may be NULL) = the udp->check written.  frame_size and data_off must

@@ -48,6 +48,7 @@ GEOMETRIES = [(64, 1, 2), (64, 1, 9), (32, 1, 3), (32, 1, 6), (16, 1, 2), (16, 1
               (4, 4, 2), (4, 1, 2)]
 
 F_BUILD_INPLACE = 0x20
+F_SRC_ALIGNED = 0x40
 
 # struct xcsum_desc == struct xdp_desc
 DESC_DTYPE = np.dtype([("addr", "<u8"), ("len", "<u4"), ("options", "<u4")])

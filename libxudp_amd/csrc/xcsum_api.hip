@@ -252,7 +252,7 @@ extern "C" int xcsum_build_device(xcsum_ctx *c, const struct xcsum_route *route,
 	a.n = n;
 	a.frame_size = frame_size;
 	a.data_off = data_off;
-	a.flags = flags & (XCSUM_F_V4_RFC | XCSUM_F_BUILD_INPLACE);
+	a.flags = flags & (XCSUM_F_V4_RFC | XCSUM_F_BUILD_INPLACE | XCSUM_F_SRC_ALIGNED);
 	a.desc_out = d_desc_out;
 	a.out = d_out;
 	a.err = c->d_err;

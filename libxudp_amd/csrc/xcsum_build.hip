@@ -22,6 +22,8 @@
  * preloaded, longer payloads stream through a tail loop.
  */
 #include "xcsum_internal.h"
+#include <stdio.h>
+#include <stdlib.h>
 
 namespace xcsum {
 
@@ -48,27 +50,70 @@ static __device__ __forceinline__ uint32_t keep_bytes(uint32_t w, int n)
 	return n >= 4 ? w : (n <= 0 ? 0u : (w & (0xffffffffu >> (32 - 8 * n))));
 }
 
-/* 16 payload bytes starting at p (any alignment), of which `rem` (>= 1) are
- * valid; bytes past the payload come back 0.  Only 16-byte blocks that hold
- * a valid byte are loaded, so nothing past the payload's last byte is read
- * beyond its own aligned block (no page can be crossed). */
-static __device__ __forceinline__ u32x4 load_payload(const uint8_t *p, uint32_t rem)
+/* One build message resolved: where its payload comes from (src, 16-byte
+ * aligned block base `blk` and phase `sh`), where its frame goes. */
+struct Msg {
+	const uint8_t *blk;     /* src & ~15 */
+	uint8_t *data;          /* frame slot data pointer (16-aligned) */
+	uint64_t data_off;      /* umem offset of data */
+	uint32_t len, sh;
+	bool ok, present;
+};
+
+static __device__ __forceinline__ Msg resolve_msg(const BuildArgs &a, u32x4 m, bool present,
+						  bool inplace)
 {
-	uintptr_t a = (uintptr_t)p;
-	uint32_t sh = (uint32_t)a & 15u;
-	const uint8_t *b = (const uint8_t *)(a & ~(uintptr_t)15);
-	u32x4 v0 = ld16(b), r;
+	Msg g;
+	const uint64_t srcoff = ((uint64_t)m.y << 32) | m.x;
+	asm volatile("" ::"v"(m.w), "v"(m.z));
+	g.len = m.z;
+	g.data_off = (uint64_t)m.w * a.frame_size + a.data_off;
+	g.data = a.umem + g.data_off;
+	g.ok = present && m.z <= 65527u && (uint64_t)a.data_off + m.z <= a.frame_size;
+	g.present = present;
+	const uint8_t *src = inplace ? (const uint8_t *)g.data : a.src + srcoff;
+	g.sh = (uint32_t)(uintptr_t)src & 15u;
+	g.blk = (const uint8_t *)((uintptr_t)src & ~(uintptr_t)15);
+	if (!g.ok)
+		g.len = 0;
+	return g;
+}
+
+__device__ u32x4 g_zero_block[4];
+
+/* the two aligned 16-byte blocks chunk c of the payload straddles; blocks
+ * holding no payload byte load zeros instead (nothing is read past the
+ * payload's last aligned block) */
+template <int G, int K, bool TWO>
+static __device__ __forceinline__ void issue_blocks(const Msg &g, uint32_t lane,
+						    u32x4 (&v)[K][TWO ? 2 : 1])
+{
+	const uint8_t *zero = (const uint8_t *)g_zero_block;
+#pragma unroll
+	for (int k = 0; k < K; k++) {
+		uint32_t off = 16u * (lane + k * G);
+		bool has = off < g.len;
+		/* second block holds bytes [16 - sh, ...) of the chunk */
+		bool has2 = has && g.sh != 0 && 16u - g.sh < g.len - off;
+		v[k][0] = ld16(has ? g.blk + off : zero);
+		if (TWO)
+			v[k][TWO ? 1 : 0] = ld16(has2 ? g.blk + off + 16 : zero);
+	}
+}
+
+/* the chunk's 16 payload bytes from its two blocks (byte shift by sh), bytes
+ * past the payload cleared */
+static __device__ __forceinline__ u32x4 shift_chunk(u32x4 v0, u32x4 v1, uint32_t sh, uint32_t rem)
+{
+	u32x4 r;
 	if (sh == 0) {
 		r = v0;
 	} else {
-		u32x4 v1 = (16u - sh < rem) ? ld16(b + 16) : u32x4{0, 0, 0, 0};
 		uint32_t w[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
 		uint32_t q = sh >> 2, s8 = sh & 3u;
 		uint32_t o[5];
 #pragma unroll
 		for (int j = 0; j < 5; j++) {
-			/* o[j] = w[j + q] with q in 0..3, by selects (no dynamic
-			 * register indexing) */
 			uint32_t x = w[j];
 			x = q == 1 ? w[j + 1] : x;
 			x = q == 2 ? w[j + 2] : x;
@@ -87,6 +132,15 @@ static __device__ __forceinline__ u32x4 load_payload(const uint8_t *p, uint32_t 
 		r.w = keep_bytes(r.w, (int)rem - 12);
 	}
 	return r;
+}
+
+/* slow path for payloads longer than K*G chunks: plain walk */
+static __device__ __forceinline__ u32x4 load_payload(const uint8_t *blk, uint32_t sh, uint32_t off,
+						     uint32_t rem)
+{
+	u32x4 v0 = ld16(blk + off);
+	u32x4 v1 = (sh != 0 && 16u - sh < rem) ? ld16(blk + off + 16) : u32x4{0, 0, 0, 0};
+	return shift_chunk(v0, v1, sh, rem);
 }
 
 static __device__ __forceinline__ void store_payload(uint8_t *d, u32x4 v, uint32_t rem)
@@ -142,7 +196,75 @@ static __device__ __forceinline__ uint32_t bswap16(uint32_t x)
 	return ((x >> 8) & 0xffu) | ((x & 0xffu) << 8);
 }
 
-template <int G, int K>
+/* header bytes + descriptor + result for one built frame (s = payload sum,
+ * in every lane of the segment) */
+template <int G>
+static __device__ __forceinline__ void finish_frame(const BuildArgs &a, const Msg &g, uint32_t p,
+						    uint32_t s, uint32_t lane, const uint16_t *tmpl,
+						    bool v6, uint32_t hdr, uint32_t sconst,
+						    uint32_t ipconst)
+{
+	if (!g.ok) {
+		if (lane == 0) {
+			struct xcsum_desc d0 = {g.data_off, 0u, 0u};
+			a.desc_out[p] = d0;
+			if (a.out)
+				a.out[p] = 0;
+			atomicAdd(a.err, 1ull);
+		}
+		return;
+	}
+	const uint32_t ulen = 8u + g.len;
+	/* S = payload + addresses + ports + 17 + udp_len (pseudo) + udp_len
+	 * (header); the header's check field is 0 */
+	uint32_t S = s + sconst + 2u * ulen;
+	uint32_t t = (S & 0xffffu) + (S >> 16);
+	t = (t & 0xffffu) + (t >> 16);
+	uint32_t r = ~t & 0xffffu;
+	if (r == 0)
+		r = 0xffffu;                               /* CSUM_MANGLED_0 */
+	uint32_t ucheck = (v6 || (a.flags & XCSUM_F_V4_RFC)) ? bswap16(r) : 0u;
+	uint32_t ipcheck = 0;
+	if (!v6) {
+		uint32_t ip = ipconst + 20u + ulen;        /* + tot_len */
+		ip = (ip & 0xffffu) + (ip >> 16);
+		ip = (ip & 0xffffu) + (ip >> 16);
+		ipcheck = bswap16(~ip & 0xffffu);
+	}
+	uint8_t *eth = g.data - hdr;
+	for (uint32_t j = lane; j < hdr / 2; j += G) {
+		uint32_t h = tmpl[j];
+		if (v6) {
+			if (j == 9 || j == 29)
+				h = bswap16(ulen);                 /* payload_len, udp len */
+			else if (j == 30)
+				h = ucheck;
+		} else {
+			if (j == 8)
+				h = bswap16(20u + ulen);           /* tot_len */
+			else if (j == 12)
+				h = ipcheck;
+			else if (j == 19)
+				h = bswap16(ulen);
+			else if (j == 20)
+				h = ucheck;
+		}
+		*reinterpret_cast<uint16_t *>(eth + 2 * j) = (uint16_t)h;
+	}
+	if (lane == 0) {
+		struct xcsum_desc d0 = {g.data_off - hdr, hdr + g.len, 0u};
+		a.desc_out[p] = d0;
+		if (a.out)
+			a.out[p] = (uint16_t)ucheck;
+	}
+}
+
+/*
+ * Persistent grid, G lanes per message, same two-stage pipeline as the
+ * checksum kernel: message i+2's descriptor and message i+1's payload blocks
+ * are in flight while message i is shifted, stored, summed and headed.
+ */
+template <int G, int K, bool TWO>
 __global__ void __launch_bounds__(256) build_kernel(BuildArgs a)
 {
 	/* header template as memory-order halfwords; big-endian word j of the
@@ -154,7 +276,7 @@ __global__ void __launch_bounds__(256) build_kernel(BuildArgs a)
 
 	const bool v6 = a.family == 6;
 	const uint32_t hdr = v6 ? 62u : 42u;
-	/* constant part of the UDP checksum: the pseudo-header addresses and the
+	/* constant part of the UDP checksum: pseudo-header addresses and the
 	 * ports (header halfwords 13..18 / 11..28), protocol 17 */
 	uint32_t sconst = 17u;
 	for (uint32_t j = v6 ? 11u : 13u; j < (v6 ? 29u : 19u); j++)
@@ -170,103 +292,70 @@ __global__ void __launch_bounds__(256) build_kernel(BuildArgs a)
 	const uint32_t seg = (blockIdx.x * 256u + threadIdx.x) / G;
 	const uint32_t nseg = gridDim.x * (256u / G);
 	const bool inplace = (a.flags & XCSUM_F_BUILD_INPLACE) != 0;
+	const uint32_t last = a.n - 1;
+
+	u32x4 d = *((gu32x4 *)(a.msgs + (seg < a.n ? seg : last)));
+	Msg gc = resolve_msg(a, d, seg < a.n, inplace);
+	d = *((gu32x4 *)(a.msgs + (seg + nseg < a.n ? seg + nseg : last)));
+	__builtin_amdgcn_sched_barrier(0);
+	u32x4 vc[K][TWO ? 2 : 1];
+	issue_blocks<G, K, TWO>(gc, lane, vc);
 
 	for (uint32_t p = seg; p < a.n; p += nseg) {
-		const u32x4 m = *((gu32x4 *)(a.msgs + p));
-		const uint64_t srcoff = ((uint64_t)m.y << 32) | m.x;
-		const uint32_t len = m.z, slot = m.w;
-		const uint64_t data_off = (uint64_t)slot * a.frame_size + a.data_off;
-		uint8_t *data = a.umem + data_off;
-		const bool ok = len <= 65527u && (uint64_t)a.data_off + len <= a.frame_size;
-		const uint8_t *src = inplace ? (const uint8_t *)data : a.src + srcoff;
+		Msg gn = resolve_msg(a, d, p + nseg < a.n, inplace);
+		uint32_t q = p + 2 * nseg;
+		d = *((gu32x4 *)(a.msgs + (q < a.n ? q : last)));
+		__builtin_amdgcn_sched_barrier(0);
+		u32x4 vn[K][TWO ? 2 : 1];
+		issue_blocks<G, K, TWO>(gn, lane, vn);
 
 		uint32_t E = 0, O = 0;
-		if (ok) {
+		if (__builtin_amdgcn_ballot_w64(gc.len > 16u * K * G)) {
+			/* jumbo payloads: plain walk (own copy of the body) */
+			for (uint32_t off = 16u * lane; off < gc.len; off += 16u * G) {
+				u32x4 v = load_payload(gc.blk, gc.sh, off, gc.len - off);
+				if (!inplace)
+					store_payload(gc.data + off, v, gc.len - off);
+				accum(v, E, O);
+			}
+		} else {
 #pragma unroll
 			for (int k = 0; k < K; k++) {
 				uint32_t off = 16u * (lane + k * G);
-				if (off < len) {
-					u32x4 v = load_payload(src + off, len - off);
+				if (off < gc.len) {
+					u32x4 v = TWO ? shift_chunk(vc[k][0], vc[k][TWO ? 1 : 0],
+								    gc.sh, gc.len - off)
+						      : shift_chunk(vc[k][0], vc[k][0], 0u,
+								    gc.len - off);
 					if (!inplace)
-						store_payload(data + off, v, len - off);
+						store_payload(gc.data + off, v, gc.len - off);
 					accum(v, E, O);
 				}
-			}
-			for (uint32_t off = 16u * (lane + K * G); off < len; off += 16u * G) {
-				u32x4 v = load_payload(src + off, len - off);
-				if (!inplace)
-					store_payload(data + off, v, len - off);
-				accum(v, E, O);
 			}
 		}
 		/* payload starts 16-aligned (even address): E holds high bytes */
 		uint32_t s = seg_sum<G>((E << 8) + O);
-		if (!ok) {
-			if (lane == 0) {
-				struct xcsum_desc d0 = {data_off, 0u, 0u};
-				a.desc_out[p] = d0;
-				if (a.out)
-					a.out[p] = 0;
-				atomicAdd(a.err, 1ull);
-			}
-			continue;
-		}
-		const uint32_t ulen = 8u + len;
-		/* S = payload + addresses + ports + 17 + udp_len (pseudo) +
-		 * udp_len (header) -- the header's check field is 0 */
-		uint32_t S = s + sconst + 2u * ulen;
-		uint32_t t = (S & 0xffffu) + (S >> 16);
-		t = (t & 0xffffu) + (t >> 16);
-		uint32_t r = ~t & 0xffffu;
-		if (r == 0)
-			r = 0xffffu;                       /* CSUM_MANGLED_0 */
-		uint32_t ucheck = (v6 || (a.flags & XCSUM_F_V4_RFC)) ? bswap16(r) : 0u;
-		uint32_t ipcheck = 0;
-		if (!v6) {
-			uint32_t ip = ipconst + 20u + ulen;  /* + tot_len */
-			ip = (ip & 0xffffu) + (ip >> 16);
-			ip = (ip & 0xffffu) + (ip >> 16);
-			ipcheck = bswap16(~ip & 0xffffu);
-		}
-		uint8_t *eth = data - hdr;
-		for (uint32_t j = lane; j < hdr / 2; j += G) {
-			uint32_t h = tmpl[j];
-			if (v6) {
-				if (j == 9 || j == 29)
-					h = bswap16(ulen);           /* payload_len, udp len */
-				else if (j == 30)
-					h = ucheck;
-			} else {
-				if (j == 8)
-					h = bswap16(20u + ulen);     /* tot_len */
-				else if (j == 12)
-					h = ipcheck;
-				else if (j == 19)
-					h = bswap16(ulen);
-				else if (j == 20)
-					h = ucheck;
-			}
-			*reinterpret_cast<uint16_t *>(eth + 2 * j) = (uint16_t)h;
-		}
-		if (lane == 0) {
-			struct xcsum_desc d0 = {data_off - hdr, hdr + len, 0u};
-			a.desc_out[p] = d0;
-			if (a.out)
-				a.out[p] = (uint16_t)ucheck;
+		finish_frame<G>(a, gc, p, s, lane, tmpl, v6, hdr, sconst, ipconst);
+
+		gc = gn;
+#pragma unroll
+		for (int k = 0; k < K; k++) {
+			vc[k][0] = vn[k][0];
+			if (TWO)
+				vc[k][TWO ? 1 : 0] = vn[k][TWO ? 1 : 0];
 		}
 	}
 }
 
-#define XCSUM_BUILD_GEOMETRIES(X) X(4, 1) X(8, 2) X(16, 6) X(64, 9)
 
-template <int G, int K>
+template <int G, int K, bool TWO>
 static hipError_t launch_build_t(const BuildArgs &a, int cus, hipStream_t s)
 {
 	static int occ = 0;
 	if (!occ) {
 		int nb = 0;
-		if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, build_kernel<G, K>, 256, 0) !=
-			    hipSuccess || nb <= 0)
+		if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, build_kernel<G, K, TWO>, 256,
+								 0) != hipSuccess || nb <= 0)
 			nb = 4;
 		occ = nb;
 	}
@@ -276,23 +365,42 @@ static hipError_t launch_build_t(const BuildArgs &a, int cus, hipStream_t s)
 		blocks = cap;
 	if (blocks == 0)
 		blocks = 1;
-	hipLaunchKernelGGL((build_kernel<G, K>), dim3((unsigned)blocks), dim3(256), 0, s, a);
+	hipLaunchKernelGGL((build_kernel<G, K, TWO>), dim3((unsigned)blocks), dim3(256), 0, s, a);
 	return hipGetLastError();
 }
+
+#define XCSUM_BUILD_GEOMETRIES(X) \
+	X(4, 1) X(8, 2) X(16, 2) X(16, 3) X(16, 6) X(32, 3) X(64, 2) X(64, 9)
 
 hipError_t launch_build(const BuildArgs &a, uint32_t len_hint, int cus, hipStream_t s)
 {
 	if (a.n == 0)
 		return hipSuccess;
-	/* lanes x chunks to cover a typical payload in one preload */
-	uint32_t chunks = (len_hint + 15) / 16;
-	if (chunks <= 4)
-		return launch_build_t<4, 1>(a, cus, s);
-	if (chunks <= 16)
-		return launch_build_t<8, 2>(a, cus, s);
-	if (chunks <= 96)
-		return launch_build_t<16, 6>(a, cus, s);
-	return launch_build_t<64, 9>(a, cus, s);
+	/* payloads read from 16-byte aligned addresses need one block per chunk */
+	const bool two = !(a.flags & (XCSUM_F_BUILD_INPLACE | XCSUM_F_SRC_ALIGNED));
+	int G, K;
+	const char *e = getenv("XCSUM_BUILD_GEOMETRY"); /* "G,K" for sweeps */
+	if (!(e && sscanf(e, "%d,%d", &G, &K) == 2)) {
+		/* lanes x chunks to cover a typical payload in one preload */
+		uint32_t chunks = (len_hint + 15) / 16;
+		if (chunks <= 4) { G = 4; K = 1; }
+		else if (chunks <= 16) { G = 8; K = 2; }
+		else if (chunks <= 96) {
+			/* MTU payloads, measured (tools/bench_build.py): copies
+			 * 4.1-4.6 TB/s moved at (32,3), in place 4.0 at (16,6) */
+			const bool copy = !(a.flags & XCSUM_F_BUILD_INPLACE);
+			G = copy ? 32 : 16;
+			K = copy ? 3 : 6;
+		}
+		else { G = 64; K = 9; }
+	}
+#define X(g_, k_)                                                                       \
+	if (G == g_ && K == k_)                                                         \
+		return two ? launch_build_t<g_, k_, true>(a, cus, s)                    \
+			   : launch_build_t<g_, k_, false>(a, cus, s);
+	XCSUM_BUILD_GEOMETRIES(X)
+#undef X
+	return hipErrorInvalidValue;
 }
 
 } /* namespace xcsum */

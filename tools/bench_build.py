@@ -1,0 +1,77 @@
+#!/usr/bin/env python3
+"""Throughput of xcsum_build_device (xudp_frame_send on the GPU): 1M messages
+of one payload size into xudp's TX frame layout (4096-byte slots, data at
++384).  Modes: copy from a packed payload buffer (aligned /
+unaligned sources) and in place (payload already in its slot, the
+xudp_frame_alloc path).  Bytes moved per frame: copy = payload read + frame
+(headers + payload) written + 16-byte message + 16-byte descriptor; in place
+= payload read + headers written + message + descriptor.
+One JSON line per mode.  Usage: python tools/bench_build.py [--payload 1472]"""
+import argparse
+import json
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import libxudp_amd as X  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--payload", type=int, default=1472)
+    ap.add_argument("--n", type=int, default=1 << 20)
+    ap.add_argument("--family", type=int, default=4)
+    ap.add_argument("--reps", type=int, default=20)
+    args = ap.parse_args()
+    import torch
+    dev = torch.device("cuda:0")
+    n, L, fam = args.n, args.payload, args.family
+    hdr = 42 if fam == 4 else 62
+    FRAME, DATA_OFF = 4096, 384
+    eng = X.Engine(0)
+    route = X.make_route(fam, b"\x02\0\0\0\0\x01", b"\x02\0\0\0\0\x02",
+                         bytes(range(16)) if fam == 6 else bytes([10, 0, 35, 2]), 3486,
+                         bytes(range(16, 32)) if fam == 6 else bytes([10, 0, 35, 1]), 40000)
+    d_umem = torch.zeros(n * FRAME, dtype=torch.uint8, device=dev)
+    d_desc = torch.zeros(n * 16, dtype=torch.uint8, device=dev)
+    d_out = torch.zeros(n, dtype=torch.int16, device=dev)
+    res = {}
+    for mode in ("copy_aligned", "copy_unaligned", "inplace"):
+        stride = L + (1 if mode == "copy_unaligned" else 0)
+        stride = stride if mode == "copy_unaligned" else (L + 15) // 16 * 16
+        msgs = np.zeros(n, dtype=X.MSG_DTYPE)
+        msgs["src"] = np.arange(n, dtype=np.uint64) * stride
+        msgs["len"] = L
+        msgs["slot"] = np.arange(n, dtype=np.uint32)
+        d_msgs = torch.from_numpy(msgs.view(np.uint8)).to(dev)
+        d_src = torch.randint(0, 255, (n * stride + 16,), dtype=torch.uint8, device=dev)
+        flags = {"inplace": X.F_BUILD_INPLACE, "copy_aligned": X.F_SRC_ALIGNED}.get(mode, 0)
+        s = torch.cuda.current_stream(dev)
+        for _ in range(3):
+            eng.build_device(route, d_src, d_msgs, n, d_umem, FRAME, DATA_OFF, d_desc, d_out,
+                             flags, L, s.cuda_stream)
+        evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+               for _ in range(args.reps)]
+        for e0, e1 in evs:
+            e0.record(s)
+            eng.build_device(route, d_src, d_msgs, n, d_umem, FRAME, DATA_OFF, d_desc, d_out,
+                             flags, L, s.cuda_stream)
+            e1.record(s)
+        torch.cuda.synchronize()
+        t = float(np.median([a.elapsed_time(b) for a, b in evs])) * 1e-3
+        moved = n * ((L + hdr + L + 32) if mode != "inplace" else (L + hdr + 32))
+        rec = {"mode": mode, "geometry": os.environ.get("XCSUM_BUILD_GEOMETRY", "auto"),
+               "payload": L, "family": fam, "frames": n, "ms": round(t * 1e3, 4),
+               "mpps": round(n / t / 1e6, 1), "GBps_moved": round(moved / t / 1e9, 1),
+               "pct_hbm_peak": round(100 * moved / t / 8e12, 1)}
+        print(json.dumps(rec), flush=True)
+        del d_src, d_msgs
+    eng.close()
+
+
+if __name__ == "__main__":
+    main()
