@@ -43,9 +43,13 @@ ERR_NAMES = {ERR_INVAL: "XCSUM_ERR_INVAL", ERR_HIP: "XCSUM_ERR_HIP",
 
 # kernel geometries compiled into libxcsum.so (XCSUM_GEOMETRIES in
 # csrc/xcsum_kernels.hip): (G lanes per frame, U frames per iteration, K chunks)
-GEOMETRIES = [(64, 1, 2), (64, 1, 9), (32, 1, 3), (32, 1, 6), (16, 1, 2), (16, 1, 3),
-              (16, 1, 6), (16, 2, 6), (16, 1, 12), (8, 1, 2), (8, 2, 1), (8, 1, 12), (4, 2, 2),
-              (4, 4, 2), (4, 1, 2)]
+REG_GEOMETRIES = [(64, 1, 2), (64, 1, 9), (32, 1, 3), (32, 1, 6), (16, 1, 2), (16, 1, 3),
+                  (16, 1, 6), (16, 2, 6), (16, 1, 12), (8, 1, 2), (8, 2, 1), (8, 1, 12),
+                  (4, 2, 2), (4, 4, 2), (4, 1, 2), (2, 1, 4), (2, 2, 4), (1, 1, 6), (1, 1, 8),
+                  (1, 2, 6)]
+# LDS-DMA staged variant (csum_lds_kernel<K, D>): G = 16, U = 10 + ring depth D
+LDS_GEOMETRIES = [(16, 12, 6), (16, 13, 6), (16, 12, 3), (16, 14, 3)]
+GEOMETRIES = REG_GEOMETRIES + LDS_GEOMETRIES
 
 F_BUILD_INPLACE = 0x20
 F_SRC_ALIGNED = 0x40

@@ -133,3 +133,17 @@ def test_argument_validation_without_gpu():
         == -X.ERR_INVAL
     assert L.xcsum_unregister_umem(None, None) == -X.ERR_INVAL
     assert L.xudp_packet_udp_batch(None, None, 0, 0) == 0       # empty batch is a no-op
+
+
+def test_geometry_list_matches_kernel_source():
+    """X.GEOMETRIES (what the parity tests sweep) == the instantiations in
+    csrc/xcsum_kernels.hip: the XCSUM_GEOMETRIES table + the LDS dispatch."""
+    import re
+    src = open(os.path.join(ROOT, "libxudp_amd", "csrc", "xcsum_kernels.hip")).read()
+    table = src[src.index("#define XCSUM_GEOMETRIES"):]
+    table = table[:table.index("\n\n")]
+    reg = [tuple(map(int, m)) for m in re.findall(r"X\((\d+), (\d+), (\d+)\)", table)]
+    lds = [tuple(map(int, m)) for m in re.findall(
+        r"g\.G == (\d+) && g\.U == (\d+) && g\.K == (\d+)\) return launch_lds_t", src)]
+    assert reg == X.REG_GEOMETRIES
+    assert sorted(lds) == sorted(X.LDS_GEOMETRIES)

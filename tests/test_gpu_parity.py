@@ -5,6 +5,8 @@ Expected values come from the reference's own checksum.h / packet.c
 inputs, from the oracle restatement (oracle/xcsum_oracle.c), itself pinned
 to the reference by the CPU tests.  Integer work: bit-exact, no tolerance.
 """
+import contextlib
+
 import numpy as np
 import pytest
 
@@ -15,6 +17,19 @@ from conftest import golden_desc
 pytestmark = pytest.mark.gpu
 
 GEOMETRIES = X.GEOMETRIES
+# the default pick plus the LDS-staged variant: the feature tests below run
+# under each, so both kernels see INPLACE/IPHDR/VERIFY, ragged and maximum sizes
+FEATURE_GEOMS = [None] + X.LDS_GEOMETRIES
+
+
+@contextlib.contextmanager
+def geometry(engine, geom):
+    if geom is not None:
+        engine.set_geometry(*geom)
+    try:
+        yield
+    finally:
+        engine.set_geometry(0)
 
 
 def run_device(torch, eng, umem, desc, mode, flags=0, len_hint=0, out=True):
@@ -84,7 +99,13 @@ def test_golden_auto_mixed_families(torch_cuda, engine, golden, len_hint):
     assert np.array_equal(got, exp_rfc)
 
 
-def test_golden_inplace_and_iphdr(torch_cuda, engine, golden):
+@pytest.mark.parametrize("geom", FEATURE_GEOMS)
+def test_golden_inplace_and_iphdr(torch_cuda, engine, golden, geom):
+    with geometry(engine, geom):
+        _test_golden_inplace_and_iphdr_body(torch_cuda, engine, golden)
+
+
+def _test_golden_inplace_and_iphdr_body(torch_cuda, engine, golden):
     """INPLACE writes udp->check, IPHDR writes iph->check == xudp_checksum_half."""
     fam = golden["family"]
     umem = golden["umem"].copy()
@@ -117,7 +138,13 @@ def test_golden_inplace_and_iphdr(torch_cuda, engine, golden):
 
 @pytest.mark.parametrize("family", [4, 6])
 @pytest.mark.parametrize("layout", ["packed8", "packed1", "umem_mirror"])
-def test_generated_vs_oracle(torch_cuda, engine, family, layout):
+@pytest.mark.parametrize("geom", FEATURE_GEOMS)
+def test_generated_vs_oracle(torch_cuda, engine, family, layout, geom):
+    with geometry(engine, geom):
+        _test_generated_vs_oracle_body(torch_cuda, engine, family, layout)
+
+
+def _test_generated_vs_oracle_body(torch_cuda, engine, family, layout):
     kw = dict(align=8)
     if layout == "packed1":
         kw = dict(align=1)
@@ -143,7 +170,13 @@ def test_device_generator_matches_host(torch_cuda, engine):
             assert np.array_equal(d_umem.cpu().numpy(), umem)
 
 
-def test_edge_cases(torch_cuda, engine):
+@pytest.mark.parametrize("geom", FEATURE_GEOMS)
+def test_edge_cases(torch_cuda, engine, geom):
+    with geometry(engine, geom):
+        _test_edge_cases_body(torch_cuda, engine)
+
+
+def _test_edge_cases_body(torch_cuda, engine):
     # empty batch
     dev = torch_cuda.device("cuda:0")
     d = torch_cuda.zeros(16, dtype=torch_cuda.uint8, device=dev)
@@ -193,7 +226,13 @@ from test_oracle import filled_golden  # noqa: E402
 
 
 @pytest.mark.parametrize("len_hint", [0, 100, 1500])
-def test_verify_matches_oracle(torch_cuda, engine, golden, len_hint):
+@pytest.mark.parametrize("geom", FEATURE_GEOMS)
+def test_verify_matches_oracle(torch_cuda, engine, golden, len_hint, geom):
+    with geometry(engine, geom):
+        _test_verify_matches_oracle_body(torch_cuda, engine, golden, len_hint)
+
+
+def _test_verify_matches_oracle_body(torch_cuda, engine, golden, len_hint):
     desc = golden_desc(golden)
     fam = golden["family"]
     good = filled_golden(golden)
