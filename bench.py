@@ -97,7 +97,7 @@ def build_batch(cfg, rank, world, torch, dev, eng, stream):
     return desc, d_desc, bufs, out, first, count
 
 
-def cpu_baseline(cfg, seconds=8.0):
+def cpu_baseline(cfg, seconds=10.0):
     """The reference checksum.h timed on this host over a bounded sample."""
     import oracle  # test infrastructure, used here only as the CPU baseline
     seed = SEED_BASE ^ cfg["id"]
@@ -124,8 +124,16 @@ def cpu_baseline(cfg, seconds=8.0):
     exp = oracle.ref_batch(umem, desc, mode) if kind == "reference" else oracle.batch(umem, desc,
                                                                                         mode)
     assert np.array_equal(out, exp)
+    model = ""
+    try:
+        with open("/proc/cpuinfo") as f:
+            model = next((ln.split(":", 1)[1].strip() for ln in f
+                          if ln.startswith("model name")), "")
+    except OSError:
+        pass
     return {"value": round(res[threads], 3), "unit": "GiB/s", "cores": threads, "kind": kind,
-            "value_1core": round(res[1], 3),
+            "value_1core": round(res[1], 3), "cpu_model": model,
+            "host_cpus": os.cpu_count(),
             "sample": f"{m} frames of the same config ({alg / 1e6:.1f} MB algorithmic), "
                       f"repeated for ~{seconds:.0f} s; xudp/checksum.h "
                       f"{'udp_csum6' if mode == 2 else 'udp_checksum'} compiled -O2 from the "
@@ -159,7 +167,7 @@ def main():
                     help="process group for the barrier / timing reductions (nccl = RCCL)")
     ap.add_argument("--same-device", action="store_true",
                     help="rehearsal only: every rank on cuda:0 (1-GPU box)")
-    ap.add_argument("--cpu-seconds", type=float, default=8.0)
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
     args = ap.parse_args()
 
     import torch

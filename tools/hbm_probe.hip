@@ -49,3 +49,44 @@ extern "C" int probe_stream_read(const void *p, uint64_t nbytes, uint32_t *out, 
 #undef L
 	return hipGetLastError() == hipSuccess ? 0 : -1;
 }
+
+/* Slot-layout probe: read span16*16 bytes at a 16-aligned offset inside each
+ * slot_bytes slot (xudp's UMEM: one frame per 4096-B chunk), nothing else.
+ * off(slot) = off0 + (slot * rot16 % nrot) * 16: rot16 = 0 is xudp's fixed
+ * offset; rot16 != 0 spreads the spans over the slot to see whether the
+ * fixed in-slot offset (and so a fixed subset of HBM channels) costs rate. */
+__global__ void __launch_bounds__(256) slot_read(const uint8_t *p, uint64_t nslots,
+						 uint32_t slot_bytes, uint32_t span16, uint32_t off0,
+						 uint32_t rot16, uint32_t nrot, uint32_t perm_mul,
+						 uint32_t perm_shift, uint32_t *out)
+{
+	const uint64_t total = nslots * span16;
+	uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+	const uint64_t stride = (uint64_t)gridDim.x * 256;
+	uint32_t acc = 0;
+	for (; i < total; i += stride) {
+		uint64_t slot = i / span16;
+		uint32_t w = (uint32_t)(i - slot * span16);
+		if (perm_mul) {	/* visit slot groups of 2^perm_shift in a scattered order */
+			uint64_t grp = slot >> perm_shift, ng = nslots >> perm_shift;
+			slot = (((grp * perm_mul) & (ng - 1)) << perm_shift) |
+			       (slot & ((1ull << perm_shift) - 1));
+		}
+		uint32_t off = off0 + (nrot ? (uint32_t)((slot * rot16) % nrot) * 16 : 0);
+		u32x4 v = __builtin_nontemporal_load(
+			(gu32x4 *)(p + slot * slot_bytes + off + (uint64_t)w * 16));
+		acc += v.x ^ v.y ^ v.z ^ v.w;
+	}
+	out[(uint64_t)blockIdx.x * 256 + threadIdx.x] = acc;
+}
+
+extern "C" int probe_slot_read(const void *p, uint64_t nslots, uint32_t slot_bytes,
+			       uint32_t span16, uint32_t off0, uint32_t rot16, uint32_t nrot,
+			       uint32_t perm_mul, uint32_t perm_shift,
+			       uint32_t *out, int blocks, void *stream)
+{
+	hipLaunchKernelGGL(slot_read, dim3(blocks), dim3(256), 0, (hipStream_t)stream,
+			   (const uint8_t *)p, nslots, slot_bytes, span16, off0, rot16, nrot,
+			   perm_mul, perm_shift, out);
+	return hipGetLastError() == hipSuccess ? 0 : -1;
+}

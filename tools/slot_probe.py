@@ -1,0 +1,60 @@
+#!/usr/bin/env python3
+"""Does xudp's UMEM slot layout (one ~1.5 KB frame at a fixed offset in each
+4096-B chunk) cost HBM read rate by itself, independent of the
+checksum kernel?  Reads only the spans, 1M slots, with (a) packed spans,
+(b) the fixed xudp offset, (c) offsets rotated across the slot, (d) 2048-B
+slots.  One JSON line per case.  Bounds checked on the host: every read ends
+inside the buffer."""
+import ctypes
+import json
+import os
+
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def main():
+    L = ctypes.CDLL(os.path.join(HERE, "libhbmprobe.so"))
+    L.probe_slot_read.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32,
+                                  ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
+                                  ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
+                                  ctypes.c_void_p, ctypes.c_int,
+                                  ctypes.c_void_p]
+    dev = torch.device("cuda:0")
+    cus = torch.cuda.get_device_properties(dev).multi_processor_count
+    nslots = 1 << 20
+    span16 = 1488 // 16 + 1                   # 94 x 16 B: a config-2 span
+    buf = torch.zeros((nslots * 4096 + 4096,), dtype=torch.uint8, device=dev)
+    out = torch.empty(cus * 16 * 256, dtype=torch.int32, device=dev)
+    s = torch.cuda.current_stream(dev)
+    # (name, slot bytes, offset, rot16, nrot, perm_mul, perm_shift)
+    cases = [("packed", span16 * 16, 0, 0, 0, 0, 0),
+             ("xudp_4096_fixed_off_368", 4096, 368, 0, 0, 0, 0),
+             ("4096_rotated_off", 4096, 0, 37, (4096 - span16 * 16) // 16, 0, 0),
+             ("4096_fixed_scattered_slots", 4096, 368, 0, 0, 0x9E3779B1, 0),
+             ("4096_fixed_scattered_groups16", 4096, 368, 0, 0, 0x9E3779B1, 4),
+             ("4096_fixed_scattered_groups256", 4096, 368, 0, 0, 0x9E3779B1, 8),
+             ("xudp_2048_fixed_off_368", 2048, 368, 0, 0, 0, 0),
+             ("2048_rotated_off", 2048, 0, 7, (2048 - span16 * 16) // 16, 0, 0)]
+    for name, slot, off0, rot, nrot, pm, ps in cases:
+        assert (nslots - 1) * slot + off0 + max(nrot - 1, 0) * 16 + span16 * 16 <= buf.numel()
+        for per_cu in (4, 8):
+            ts = []
+            for _ in range(12):
+                a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                a.record(s)
+                assert L.probe_slot_read(buf.data_ptr(), nslots, slot, span16, off0, rot, nrot,
+                                         pm, ps, out.data_ptr(), cus * per_cu, s.cuda_stream) == 0
+                b.record(s)
+                torch.cuda.synchronize()
+                ts.append(a.elapsed_time(b))
+            t = sorted(ts)[len(ts) // 2]
+            print(json.dumps({"case": name, "slot_bytes": slot, "blocks_per_cu": per_cu,
+                              "ms": round(t, 4),
+                              "GBps": round(nslots * span16 * 16 / (t * 1e-3) / 1e9, 1)}),
+                  flush=True)
+
+
+if __name__ == "__main__":
+    main()
