@@ -105,6 +105,14 @@ int xcsum_ctx_set_geometry(xcsum_ctx *ctx, int G, int U, int K);
  * (tuning; 0 = the per-geometry default, the occupancy limit at most). */
 int xcsum_ctx_set_launch(xcsum_ctx *ctx, int blocks_per_cu);
 
+/* Order in which xcsum_batch_device visits the frames (tuning knob; results
+ * never depend on it).  The batch is cut into 2^tile_log2-frame tiles dealt
+ * round-robin from 2^region_log2 equal regions, so the frames in flight come
+ * from regions spread over the whole UMEM rather than one window.
+ * region_log2 = 0: descriptor order; -1: automatic (default).  Env
+ * XCSUM_ORDER="R,T" sets it at context creation. */
+int xcsum_ctx_set_order(xcsum_ctx *ctx, int region_log2, int tile_log2);
+
 /* ---- device-resident batch ------------------------------------------------
  * Replaces the per-frame checksum work of the xudp_frame_send loop
  * (xudp/tx.c:696-726 -> __xudp_frame_send -> xudp_packet_udp, packet.c:156)

@@ -79,6 +79,7 @@ _SIGS = {
     "xcsum_ctx_set_geometry": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
                                               ctypes.c_int]),
     "xcsum_ctx_set_launch": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
+    "xcsum_ctx_set_order": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int]),
     "xcsum_batch_device": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                           ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint32,
                                           ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p]),
@@ -225,6 +226,10 @@ class Engine:
 
     def set_launch(self, blocks_per_cu=0):
         _check(lib().xcsum_ctx_set_launch(self._ctx, blocks_per_cu), "xcsum_ctx_set_launch")
+
+    def set_order(self, region_log2=-1, tile_log2=0):
+        _check(lib().xcsum_ctx_set_order(self._ctx, region_log2, tile_log2),
+               "xcsum_ctx_set_order")
 
     def take_errors(self):
         c = ctypes.c_uint64(0)

@@ -31,6 +31,19 @@ static Geometry env_geometry()
 	return Geometry{0, 0, 0, 0};
 }
 
+/* XCSUM_ORDER="R,T": log2 regions, log2 frames per tile (tuning only) */
+static void env_order(xcsum_ctx *c)
+{
+	c->order_rlog = -1;
+	c->order_tlog = 0;
+	const char *e = getenv("XCSUM_ORDER");
+	int r = 0, t = 0;
+	if (e && sscanf(e, "%d,%d", &r, &t) == 2 && r >= 0 && r <= 12 && t >= 0 && t <= 16) {
+		c->order_rlog = r;
+		c->order_tlog = t;
+	}
+}
+
 extern "C" int xcsum_ctx_create(int device, xcsum_ctx **out)
 {
 	int count = 0;
@@ -75,6 +88,7 @@ extern "C" int xcsum_ctx_create(int device, xcsum_ctx **out)
 	c->desc_cap = 0;
 	c->geom = env_geometry();
 	c->blocks_per_cu = 0;
+	env_order(c);
 	*out = c;
 	return 0;
 }
@@ -131,6 +145,18 @@ extern "C" int xcsum_ctx_take_errors(xcsum_ctx *c, uint64_t *count)
 	return 0;
 }
 
+static void set_order(const xcsum_ctx *c, CsumArgs &a)
+{
+	if (c->order_rlog >= 0) {
+		a.ord = order_regions(a.n, c->order_rlog, c->order_tlog);
+		return;
+	}
+	/* automatic: 32 regions of 16-frame tiles if the kernel finds the batch
+	 * sparse in the UMEM, else descriptor order (profiles/r01/order_*.log) */
+	a.ord = order_regions(a.n, 5, 4);
+	a.ord.sparse_only = a.ord.rshift != 0;
+}
+
 static Geometry geometry_for(const xcsum_ctx *c, uint32_t len_hint)
 {
 	Geometry g = c->geom.G ? c->geom : pick_geometry(len_hint);
@@ -154,6 +180,15 @@ extern "C" int xcsum_ctx_set_geometry(xcsum_ctx *c, int G, int U, int K)
 	c->geom.U = U;
 	c->geom.K = K;
 	c->geom.B = 0;
+	return 0;
+}
+
+extern "C" int xcsum_ctx_set_order(xcsum_ctx *c, int region_log2, int tile_log2)
+{
+	if (!c || region_log2 < -1 || region_log2 > 12 || tile_log2 < 0 || tile_log2 > 16)
+		return -XCSUM_ERR_INVAL;
+	c->order_rlog = region_log2;
+	c->order_tlog = tile_log2;
 	return 0;
 }
 
@@ -188,6 +223,7 @@ extern "C" int xcsum_batch_device(xcsum_ctx *c, uint8_t *d_umem, const struct xc
 		a.flags &= ~XCSUM_F_INPLACE; /* verifying never writes frames */
 	a.bias = 0;
 	a.err = c->d_err;
+	set_order(c, a);
 	HIPCHK(launch_csum(a, geometry_for(c, len_hint), c->cus, (hipStream_t)stream));
 	return 0;
 }
@@ -258,6 +294,15 @@ extern "C" int xcsum_build_device(xcsum_ctx *c, const struct xcsum_route *route,
 	a.err = c->d_err;
 	a.family = route->family;
 	header_template(route, (uint8_t *)a.tmpl);
+	if (c->order_rlog >= 0) {
+		a.ord = order_regions(n, c->order_rlog, c->order_tlog);
+	} else {
+		/* automatic: the frames are sparse when a slot is at least twice
+		 * the frame (xudp: 4096-byte chunks, ~1.5 KB frames) -- then 32
+		 * regions of 16-message tiles, as for the checksum kernel */
+		const uint32_t typ = hdr + (len_hint ? len_hint : 1472u);
+		a.ord = frame_size >= 2u * typ ? order_regions(n, 5, 4) : order_identity(n);
+	}
 	HIPCHK(launch_build(a, len_hint, c->cus, (hipStream_t)stream));
 	return 0;
 }
@@ -443,6 +488,7 @@ int batch_host_impl(xcsum_ctx *c, uint8_t *h_umem, const struct xcsum_desc *h_de
 		CsumArgs a;
 		a.desc = c->d_desc[slot];
 		a.n = cnt;
+		a.ord = order_identity(cnt);
 		a.out = c->d_out[slot];
 		a.out_ip = want_ip ? c->d_out[slot] + cnt : nullptr;
 		a.mode = mode;

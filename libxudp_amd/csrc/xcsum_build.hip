@@ -294,17 +294,19 @@ __global__ void __launch_bounds__(256) build_kernel(BuildArgs a)
 	const bool inplace = (a.flags & XCSUM_F_BUILD_INPLACE) != 0;
 	const uint32_t last = a.n - 1;
 
-	u32x4 d = *((gu32x4 *)(a.msgs + (seg < a.n ? seg : last)));
-	Msg gc = resolve_msg(a, d, seg < a.n, inplace);
-	d = *((gu32x4 *)(a.msgs + (seg + nseg < a.n ? seg + nseg : last)));
+	/* message indices in the batch's visiting order (a.ord); >= n: none */
+	uint32_t ic = frame_of(a.ord, seg), in = frame_of(a.ord, seg + nseg);
+	u32x4 d = *((gu32x4 *)(a.msgs + (ic < a.n ? ic : last)));
+	Msg gc = resolve_msg(a, d, ic < a.n, inplace);
+	d = *((gu32x4 *)(a.msgs + (in < a.n ? in : last)));
 	__builtin_amdgcn_sched_barrier(0);
 	u32x4 vc[K][TWO ? 2 : 1];
 	issue_blocks<G, K, TWO>(gc, lane, vc);
 
-	for (uint32_t p = seg; p < a.n; p += nseg) {
-		Msg gn = resolve_msg(a, d, p + nseg < a.n, inplace);
-		uint32_t q = p + 2 * nseg;
-		d = *((gu32x4 *)(a.msgs + (q < a.n ? q : last)));
+	for (uint32_t p = seg; p < a.ord.nlog; p += nseg) {
+		Msg gn = resolve_msg(a, d, in < a.n, inplace);
+		const uint32_t iq = frame_of(a.ord, p + 2 * nseg);
+		d = *((gu32x4 *)(a.msgs + (iq < a.n ? iq : last)));
 		__builtin_amdgcn_sched_barrier(0);
 		u32x4 vn[K][TWO ? 2 : 1];
 		issue_blocks<G, K, TWO>(gn, lane, vn);
@@ -335,9 +337,12 @@ __global__ void __launch_bounds__(256) build_kernel(BuildArgs a)
 		}
 		/* payload starts 16-aligned (even address): E holds high bytes */
 		uint32_t s = seg_sum<G>((E << 8) + O);
-		finish_frame<G>(a, gc, p, s, lane, tmpl, v6, hdr, sconst, ipconst);
+		if (gc.present)
+			finish_frame<G>(a, gc, ic, s, lane, tmpl, v6, hdr, sconst, ipconst);
 
 		gc = gn;
+		ic = in;
+		in = iq;
 #pragma unroll
 		for (int k = 0; k < K; k++) {
 			vc[k][0] = vn[k][0];
@@ -359,7 +364,7 @@ static hipError_t launch_build_t(const BuildArgs &a, int cus, hipStream_t s)
 			nb = 4;
 		occ = nb;
 	}
-	uint64_t blocks = ((uint64_t)a.n * G + 255) / 256;
+	uint64_t blocks = ((uint64_t)a.ord.nlog * G + 255) / 256;
 	uint64_t cap = (uint64_t)cus * occ;
 	if (blocks > cap)
 		blocks = cap;

@@ -9,6 +9,44 @@
 
 namespace xcsum {
 
+/* Visiting order of a batch.  A kernel walks logical indices [0, nlog);
+ * logical tile t (2^tshift frames) is frame tile (t % R) * q + t / R with
+ * R = 2^rshift, so the frames in flight at any moment come from R regions
+ * spread over the batch instead of one contiguous window (DESIGN.md,
+ * "Visiting order").  rshift == 0: identity, nlog == n.  sparse_only: the
+ * checksum kernel keeps the region order only if it finds the batch sparse
+ * in the UMEM (resolve_order), else falls back to the identity. */
+struct Order {
+	uint32_t nlog, rshift, tshift, q;
+	uint32_t sparse_only;
+};
+
+static __host__ __device__ inline Order order_identity(uint32_t n)
+{
+	return Order{n, 0u, 0u, 0u, 0u};
+}
+
+/* R = 2^rlog regions of 2^tlog-frame tiles; the identity when the batch is
+ * too small to give every region a tile or too large for u32 indices */
+static __host__ __device__ inline Order order_regions(uint32_t n, int rlog, int tlog)
+{
+	if (rlog <= 0 || tlog < 0 || rlog + tlog > 30 || n > (1u << 31) || n < (1u << (rlog + tlog)))
+		return order_identity(n);
+	const uint32_t ntiles = (n + (1u << tlog) - 1) >> tlog;
+	const uint32_t q = (ntiles + (1u << rlog) - 1) >> rlog;
+	return Order{(q << rlog) << tlog, (uint32_t)rlog, (uint32_t)tlog, q, 0u};
+}
+
+/* logical index -> frame index (>= n: no frame) */
+static __device__ __forceinline__ uint32_t frame_of(const Order &o, uint32_t p)
+{
+	if (o.rshift == 0)
+		return p;
+	const uint32_t t = p >> o.tshift;
+	const uint32_t r = t & ((1u << o.rshift) - 1u);
+	return ((r * o.q + (t >> o.rshift)) << o.tshift) | (p & ((1u << o.tshift) - 1u));
+}
+
 /* Kernel arguments (passed by value). */
 struct CsumArgs {
 	uint8_t *umem;                 /* frame i starts at umem + desc[i].addr - bias */
@@ -20,6 +58,7 @@ struct CsumArgs {
 	uint32_t flags;
 	uint64_t bias;
 	unsigned long long *err;       /* device counter of malformed frames */
+	Order ord;
 };
 
 /* Frame-build kernel arguments (xcsum_build.hip). */
@@ -33,6 +72,7 @@ struct BuildArgs {
 	unsigned long long *err;
 	uint32_t family;
 	uint32_t tmpl[16];             /* 64-byte header template, memory order */
+	Order ord;                     /* over messages */
 };
 
 hipError_t launch_build(const BuildArgs &a, uint32_t len_hint, int cus, hipStream_t s);
@@ -67,6 +107,7 @@ struct Ctx {
 	int max_blocks;
 	Geometry geom;                 /* forced geometry, G == 0: automatic */
 	int blocks_per_cu;             /* forced grid cap, 0: automatic */
+	int order_rlog, order_tlog;    /* visiting order, rlog < 0: automatic */
 	unsigned long long *d_err;
 	std::vector<Region> regions;
 

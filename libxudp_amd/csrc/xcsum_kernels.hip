@@ -87,6 +87,30 @@ static __device__ __forceinline__ u32x4 load_chunk(const uint8_t *p)
  * descriptor wait stall on the in-order vmcnt of the chunk loads. */
 typedef __attribute__((address_space(4))) const u32x4 cu32x4;
 
+/* Automatic order (ord.sparse_only): keep the prepared region order only when
+ * the batch is sparse in the UMEM -- the first and last descriptors span more
+ * than twice the bytes of n frames of their mean length.  xudp's TX UMEM (one
+ * ~1.5 KB frame per 4096-B chunk, every frame at the same in-chunk offset)
+ * is the case: visited in descriptor order, the frames in flight hit a
+ * narrow set of HBM channels (tools/slot_probe.py).  Wave-uniform scalar
+ * loads; the result never depends on the order. */
+static __device__ __forceinline__ void resolve_order(CsumArgs &a)
+{
+	if (!a.ord.sparse_only)
+		return;
+	bool sparse = false;
+	if (a.n >= 2) {
+		const u32x4 d0 = *((cu32x4 *)(a.desc));
+		const u32x4 dl = *((cu32x4 *)(a.desc + (a.n - 1)));
+		const uint64_t a0 = ((uint64_t)d0.y << 32) | d0.x;
+		const uint64_t al = ((uint64_t)dl.y << 32) | dl.x;
+		const uint64_t mean = ((uint64_t)d0.z + dl.z) / 2 + 1;
+		sparse = al > a0 && al + dl.z - a0 > 2ull * a.n * mean;
+	}
+	if (!sparse)
+		a.ord = order_identity(a.n);
+}
+
 template <bool UNIFORM>
 static __device__ __forceinline__ u32x4 load_desc(const CsumArgs &a, uint32_t p)
 {
@@ -333,7 +357,7 @@ static __device__ __forceinline__ void consume(const CsumArgs &a, const Frame (&
 		uint32_t s = f.odd ? (O << 8) + E : (E << 8) + O;
 		s = seg_sum<G>(s);
 		if (lane == 0 && f.mode != -2)
-			finalize(a, f, p0 + u * nseg, s);
+			finalize(a, f, frame_of(a.ord, p0 + u * nseg), s);
 	}
 }
 
@@ -348,6 +372,7 @@ static __device__ __forceinline__ void consume(const CsumArgs &a, const Frame (&
 template <int G, int U, int K>
 __global__ void __launch_bounds__(256) csum_kernel(CsumArgs a)
 {
+	resolve_order(a);
 	const uint32_t lane = threadIdx.x & (G - 1);
 	uint32_t seg = (blockIdx.x * 256u + threadIdx.x) / G;
 	const uint32_t nseg = gridDim.x * (256u / G);
@@ -360,28 +385,28 @@ __global__ void __launch_bounds__(256) csum_kernel(CsumArgs a)
 	u32x4 vc[U][K];
 #pragma unroll
 	for (int u = 0; u < U; u++)
-		d[u] = load_desc<G == 64>(a, seg + u * nseg);
+		d[u] = load_desc<G == 64>(a, frame_of(a.ord, seg + u * nseg));
 #pragma unroll
 	for (int u = 0; u < U; u++)
-		fc[u] = resolve(a, d[u], seg + u * nseg < a.n);
+		fc[u] = resolve(a, d[u], frame_of(a.ord, seg + u * nseg) < a.n);
 #pragma unroll
 	for (int u = 0; u < U; u++)
-		d[u] = load_desc<G == 64>(a, seg + step + u * nseg);
+		d[u] = load_desc<G == 64>(a, frame_of(a.ord, seg + step + u * nseg));
 	/* keep every descriptor load older than the chunk loads it shares a
 	 * vmcnt queue with: the next wait for the descriptors then leaves all
 	 * chunk loads in flight */
 	__builtin_amdgcn_sched_barrier(0);
 	issue<G, U, K>(fc, lane, vc);
 
-	for (uint32_t p0 = seg; p0 < a.n; p0 += step) {
+	for (uint32_t p0 = seg; p0 < a.ord.nlog; p0 += step) {
 		Frame fn[U];
 		u32x4 vn[U][K];
 #pragma unroll
 		for (int u = 0; u < U; u++)
-			fn[u] = resolve(a, d[u], p0 + step + u * nseg < a.n);
+			fn[u] = resolve(a, d[u], frame_of(a.ord, p0 + step + u * nseg) < a.n);
 #pragma unroll
 		for (int u = 0; u < U; u++)
-			d[u] = load_desc<G == 64>(a, p0 + 2 * step + u * nseg);
+			d[u] = load_desc<G == 64>(a, frame_of(a.ord, p0 + 2 * step + u * nseg));
 		__builtin_amdgcn_sched_barrier(0);
 		issue<G, U, K>(fn, lane, vn);
 
@@ -596,7 +621,7 @@ static hipError_t launch_t(const CsumArgs &a, int cus, int bpc, hipStream_t s)
 		occ = nb;
 	}
 	int per_cu = (bpc > 0 && bpc < occ) ? bpc : occ;
-	uint64_t segs = ((uint64_t)a.n + U - 1) / U;
+	uint64_t segs = ((uint64_t)a.ord.nlog + U - 1) / U;
 	uint64_t blocks = (segs * G + 255) / 256;
 	uint64_t cap = (uint64_t)cus * per_cu;
 	if (blocks > cap)
@@ -629,11 +654,13 @@ hipError_t launch_csum(const CsumArgs &a, Geometry g, int cus, hipStream_t s)
 {
 	if (a.n == 0)
 		return hipSuccess;
-	/* LDS-staged variant: G = 16, U = 10 + ring depth */
-	if (g.G == 16 && g.U == 12 && g.K == 6) return launch_lds_t<6, 2>(a, cus, g.B, s);
-	if (g.G == 16 && g.U == 13 && g.K == 6) return launch_lds_t<6, 3>(a, cus, g.B, s);
-	if (g.G == 16 && g.U == 14 && g.K == 3) return launch_lds_t<3, 4>(a, cus, g.B, s);
-	if (g.G == 16 && g.U == 12 && g.K == 3) return launch_lds_t<3, 2>(a, cus, g.B, s);
+	/* LDS-staged variant: G = 16, U = 10 + ring depth; identity order */
+	CsumArgs b = a;
+	b.ord = order_identity(a.n);
+	if (g.G == 16 && g.U == 12 && g.K == 6) return launch_lds_t<6, 2>(b, cus, g.B, s);
+	if (g.G == 16 && g.U == 13 && g.K == 6) return launch_lds_t<6, 3>(b, cus, g.B, s);
+	if (g.G == 16 && g.U == 14 && g.K == 3) return launch_lds_t<3, 4>(b, cus, g.B, s);
+	if (g.G == 16 && g.U == 12 && g.K == 3) return launch_lds_t<3, 2>(b, cus, g.B, s);
 #define X(g_, u_, k_) \
 	if (g.G == g_ && g.U == u_ && g.K == k_) return launch_t<g_, u_, k_>(a, cus, g.B, s);
 	XCSUM_GEOMETRIES(X)

@@ -1,0 +1,220 @@
+/*
+ * capi_check.c -- the C ABI used from plain C11, the way libxudp (a C
+ * library) would link it: include/xcsum.h + include/xudp_packet.h, -lxcsum.
+ * Test infrastructure: expected checksums come from the oracle restatement
+ * (oracle/liboracle.so, pinned to the reference by tests/test_oracle.py) and
+ * from the reference's known-answer frames.
+ *
+ * Exit 0 = all checks passed, 77 = no GPU (skip), 1 = a check failed.
+ * Run by tests/test_gpu_capi.py on the GPU box; built by tests/c/Makefile.
+ */
+#define _GNU_SOURCE
+#include <arpa/inet.h>
+#include <netinet/in.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <hip/hip_runtime_api.h>
+
+#include "xcsum.h"
+#include "xudp_packet.h"
+
+/* oracle/xcsum_oracle.c (struct orc_desc has the xdp_desc layout) */
+void orc_batch(const uint8_t *umem, const struct xcsum_desc *desc, uint32_t n, uint16_t *out,
+	       int mode, uint32_t flags);
+
+static int failures;
+static int checks;
+
+#define CHECK(cond, ...)                                                   \
+	do {                                                               \
+		checks++;                                                  \
+		if (!(cond)) {                                             \
+			failures++;                                        \
+			fprintf(stderr, "FAIL %s:%d: ", __FILE__, __LINE__); \
+			fprintf(stderr, __VA_ARGS__);                      \
+			fputc('\n', stderr);                               \
+		}                                                          \
+	} while (0)
+
+static uint32_t count_diff(const uint16_t *a, const uint16_t *b, uint32_t n)
+{
+	uint32_t d = 0;
+	for (uint32_t i = 0; i < n; i++)
+		d += a[i] != b[i];
+	return d;
+}
+
+static int hex_eq(const uint8_t *p, const char *hex)
+{
+	size_t n = strlen(hex) / 2;
+	for (size_t i = 0; i < n; i++) {
+		unsigned v;
+		if (sscanf(hex + 2 * i, "%2x", &v) != 1 || p[i] != (uint8_t)v)
+			return 0;
+	}
+	return 1;
+}
+
+/* Host-resident batches (xcsum_batch_host) and the device path
+ * (xcsum_batch_device on hipMalloc'ed frames) against the oracle. */
+static void check_batches(xcsum_ctx *c, uint32_t family, uint32_t stride, uint32_t offset)
+{
+	const uint32_t n = 4000;
+	struct xcsum_desc *desc = calloc(n, sizeof(*desc));
+	uint64_t bytes = 0;
+	CHECK(xcsum_gen_layout(n, family, 0, 3000, 7 + family, 0, 8, stride, offset, desc,
+			       &bytes) == 0, "gen_layout");
+	uint8_t *umem = calloc(bytes + 64, 1);
+	CHECK(xcsum_gen_fill_host(umem, desc, n, family, 7 + family, 0) == 0, "gen_fill_host");
+	uint16_t *exp = calloc(n, 2), *got = calloc(n, 2);
+	const uint32_t mode = family == 6 ? XCSUM_MODE_V6 : XCSUM_MODE_V4_LEGACY;
+	orc_batch(umem, desc, n, exp, (int)mode, 0);
+
+	/* staged copies */
+	CHECK(xcsum_batch_host(c, umem, desc, n, got, mode, 0) == 0, "batch_host");
+	CHECK(count_diff(got, exp, n) == 0, "batch_host v%u: %u mismatches", family,
+	      count_diff(got, exp, n));
+
+	/* registered UMEM, zero-copy, results written into the frames */
+	CHECK(xcsum_register_umem(c, umem, bytes + 64) == 0, "register_umem");
+	memset(got, 0, 2 * n);
+	CHECK(xcsum_batch_host(c, umem, desc, n, got, mode, XCSUM_F_ZEROCOPY | XCSUM_F_INPLACE) ==
+	      0, "batch_host zerocopy");
+	CHECK(count_diff(got, exp, n) == 0, "zerocopy v%u", family);
+	uint32_t bad = 0;
+	for (uint32_t i = 0; i < n; i++) {
+		uint16_t v;
+		memcpy(&v, umem + desc[i].addr + (family == 6 ? 60 : 40), 2);
+		bad += v != exp[i];
+	}
+	CHECK(bad == 0, "in-place udp->check v%u: %u wrong", family, bad);
+	CHECK(xcsum_unregister_umem(c, umem) == 0, "unregister_umem");
+
+	/* device-resident: the frames as xudp would have them in HBM */
+	uint8_t *d_umem = NULL;
+	struct xcsum_desc *d_desc = NULL;
+	uint16_t *d_out = NULL;
+	CHECK(hipMalloc((void **)&d_umem, bytes + 64) == hipSuccess, "hipMalloc");
+	CHECK(hipMalloc((void **)&d_desc, n * sizeof(*desc)) == hipSuccess, "hipMalloc");
+	CHECK(hipMalloc((void **)&d_out, 2 * n) == hipSuccess, "hipMalloc");
+	CHECK(xcsum_gen_fill_device(d_umem, NULL, 0, family, 0, 0, NULL) == 0, "fill n=0");
+	(void)hipMemcpy(d_desc, desc, n * sizeof(*desc), hipMemcpyHostToDevice);
+	CHECK(xcsum_gen_fill_device(d_umem, d_desc, n, family, 7 + family, 0, NULL) == 0,
+	      "gen_fill_device");
+	CHECK(xcsum_batch_device(c, d_umem, d_desc, n, d_out, mode, 0, 0, NULL) == 0,
+	      "batch_device");
+	CHECK(xcsum_sync(c, NULL) == 0, "sync");
+	memset(got, 0, 2 * n);
+	(void)hipMemcpy(got, d_out, 2 * n, hipMemcpyDeviceToHost);
+	CHECK(count_diff(got, exp, n) == 0, "batch_device v%u: %u mismatches", family,
+	      count_diff(got, exp, n));
+	/* descriptor order must not matter */
+	CHECK(xcsum_ctx_set_order(c, 3, 2) == 0, "set_order");
+	CHECK(xcsum_batch_device(c, d_umem, d_desc, n, d_out, mode, 0, 1500, NULL) == 0,
+	      "batch_device ordered");
+	(void)hipMemcpy(got, d_out, 2 * n, hipMemcpyDeviceToHost);
+	CHECK(count_diff(got, exp, n) == 0, "batch_device ordered v%u", family);
+	CHECK(xcsum_ctx_set_order(c, -1, 0) == 0, "set_order auto");
+	(void)hipFree(d_umem);
+	(void)hipFree(d_desc);
+	(void)hipFree(d_out);
+	free(desc);
+	free(umem);
+	free(exp);
+	free(got);
+}
+
+/* frames xudp_packet_udp_payload() builds
+ * in the reference, byte for byte. */
+static void check_packet_kats(void)
+{
+	unsigned char dmac[6] = {2, 0, 0, 0, 0, 2}, smac[6] = {2, 0, 0, 0, 0, 1};
+	char buf[256];
+	struct sockaddr_in to4 = {0}, from4 = {0};
+	to4.sin_family = from4.sin_family = AF_INET;
+	to4.sin_port = htons(40000);
+	from4.sin_port = htons(3486);
+	inet_pton(AF_INET, "10.0.35.1", &to4.sin_addr);
+	inet_pton(AF_INET, "10.0.35.2", &from4.sin_addr);
+	struct packet_info info;
+	memset(&info, 0, sizeof(info));
+	memset(buf, 0, sizeof(buf));
+	info.family = AF_INET;
+	info.dmac = dmac;
+	info.smac = smac;
+	info.to = &to4;
+	info.from = &from4;
+	info.head = buf;
+	info.payload = "abcdef";
+	info.payload_size = 6;
+	xudp_packet_udp_payload(&info);
+	CHECK(info.len == 48, "KAT4 len %d", info.len);
+	CHECK(hex_eq((uint8_t *)info.packet,
+		     "020000000002020000000001080045000022000040004011e0c80a0023020a0023010d9e"
+		     "9c40000e0000616263646566"),
+	      "KAT4 frame bytes");
+
+	struct sockaddr_in6 to6 = {0}, from6 = {0};
+	to6.sin6_family = from6.sin6_family = AF_INET6;
+	to6.sin6_port = htons(40000);
+	from6.sin6_port = htons(3487);
+	inet_pton(AF_INET6, "1000:2000:3000:4000::1", &to6.sin6_addr);
+	inet_pton(AF_INET6, "1000:2000:3000:4000::2", &from6.sin6_addr);
+	memset(&info, 0, sizeof(info));
+	memset(buf, 0, sizeof(buf));
+	info.family = AF_INET6;
+	info.dmac = dmac;
+	info.smac = smac;
+	info.to6 = &to6;
+	info.from6 = &from6;
+	info.head = buf;
+	info.payload = "abcdef";
+	info.payload_size = 6;
+	xudp_packet_udp_payload(&info);
+	CHECK(info.len == 68, "KAT3 len %d", info.len);
+	CHECK(hex_eq((uint8_t *)info.packet,
+		     "02000000000202000000000186dd60039f0d000e11401000200030004000000000000000"
+		     "0002100020003000400000000000000000010d9f9c40000eebc1616263646566"),
+	      "KAT3 frame bytes");
+}
+
+static void check_errors(xcsum_ctx *c)
+{
+	CHECK(xcsum_batch_device(NULL, NULL, NULL, 1, NULL, 0, 0, 0, NULL) == -XCSUM_ERR_INVAL,
+	      "null ctx");
+	CHECK(xcsum_batch_device(c, NULL, NULL, 5, NULL, 0, 0, 0, NULL) == -XCSUM_ERR_INVAL,
+	      "null buffers");
+	CHECK(xcsum_batch_device(c, NULL, NULL, 0, NULL, 0, 0, 0, NULL) == 0, "empty batch");
+	CHECK(xcsum_ctx_set_geometry(c, 7, 1, 1) == -XCSUM_ERR_INVAL, "bad geometry");
+	CHECK(xcsum_ctx_set_order(c, 13, 0) == -XCSUM_ERR_INVAL, "bad order");
+	CHECK(xcsum_unregister_umem(c, (void *)0x1000) == -XCSUM_ERR_NOT_REGISTERED,
+	      "unregister unknown");
+	uint64_t e = 99;
+	CHECK(xcsum_ctx_take_errors(c, &e) == 0 && e == 0, "error counter %llu",
+	      (unsigned long long)e);
+}
+
+int main(void)
+{
+	xcsum_ctx *c = NULL;
+	int rc = xcsum_ctx_create(-1, &c);
+	if (rc == -XCSUM_ERR_NODEV) {
+		printf("capi_check: no GPU, skipped\n");
+		return 77;
+	}
+	if (rc != 0) {
+		fprintf(stderr, "xcsum_ctx_create: %d\n", rc);
+		return 1;
+	}
+	check_batches(c, 4, 0, 0);
+	check_batches(c, 6, 0, 0);
+	check_batches(c, 4, 4096, 342);   /* xudp TX UMEM layout, SURVEY a14 */
+	check_packet_kats();
+	check_errors(c);
+	xcsum_ctx_destroy(c);
+	printf("capi_check: %d checks, %d failures\n", checks, failures);
+	return failures ? 1 : 0;
+}

@@ -13,11 +13,14 @@ import libxudp_amd as X
 pytestmark = [pytest.mark.gpu, pytest.mark.slow]
 
 
-def device_batch(torch, engine, cid, first=0, count=None):
+def device_batch(torch, engine, cid, first=0, count=None, umem_layout=False):
     cfg = dict(bench.CONFIGS[cid], id=cid)
     count = cfg["n"] if count is None else count
+    # umem_layout: xudp's TX UMEM, one frame per 4096-byte chunk;
+    # the generator keys bytes by frame index, so the frames are identical
+    kw = dict(stride=4096, offset=322 if cfg["family"] == 6 else 342) if umem_layout else {}
     desc, nbytes = X.gen_layout(count, cfg["family"], cfg["pmin"], cfg["pmax"],
-                                seed=bench.SEED_BASE ^ cid, first_index=first)
+                                seed=bench.SEED_BASE ^ cid, first_index=first, **kw)
     dev = torch.device("cuda:0")
     d_desc = torch.from_numpy(desc.view(np.uint8)).to(dev)
     d_umem = torch.empty(nbytes + 64, dtype=torch.uint8, device=dev)
@@ -64,6 +67,28 @@ def test_config2_every_geometry_same_digest(torch_cuda, engine, digests):
         finally:
             engine.set_geometry(0)
         assert sha(got) == digests["config2"]["sha256_out"], g
+
+
+@pytest.mark.parametrize("order", [(4, 6), (6, 3), (3, 8)])
+def test_config2_visiting_order_same_digest(torch_cuda, engine, digests, order):
+    cfg, desc, d_desc, d_umem = device_batch(torch_cuda, engine, 2)
+    engine.set_order(*order)
+    try:
+        got = run(torch_cuda, engine, d_umem, d_desc, len(desc), cfg["mode"])
+    finally:
+        engine.set_order(-1, 0)
+    assert sha(got) == digests["config2"]["sha256_out"]
+
+
+@pytest.mark.parametrize("cid", [2, 3, 4])
+def test_umem_layout_same_digest(torch_cuda, engine, digests, cid):
+    """The same frames in xudp's 4096-byte-chunk UMEM layout: the automatic
+    visiting order switches to regions there (sparse batch) -- same output."""
+    cfg, desc, d_desc, d_umem = device_batch(torch_cuda, engine, cid, umem_layout=True)
+    assert int(desc["addr"][1] - desc["addr"][0]) == 4096
+    for hint in (0, int(desc["len"][0])):
+        got = run(torch_cuda, engine, d_umem, d_desc, len(desc), cfg["mode"], 0, hint)
+        assert sha(got) == digests[f"config{cid}"]["sha256_out"], hint
 
 
 def test_config5_digest_8m_mixed(torch_cuda, engine, digests):

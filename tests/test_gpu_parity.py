@@ -267,3 +267,33 @@ def test_verify_host_path(engine, golden):
     bad[int(desc["addr"][0]) + 28] ^= 0xff  # saddr byte: inside the span
     engine.batch_host(bad, desc, out, X.MODE_AUTO, X.F_VERIFY)
     assert out[0] != 0 and (out[1:] == 0).all()
+
+
+# ---- visiting order (xcsum_ctx_set_order): results never depend on it ----
+
+@pytest.mark.parametrize("order", [(0, 0), (1, 0), (2, 3), (4, 0), (3, 5), (6, 2), (12, 16)])
+def test_visiting_order_same_result(torch_cuda, engine, golden, order):
+    desc = golden_desc(golden)
+    engine.set_order(*order)
+    try:
+        got, after = run_device(torch_cuda, engine, golden["umem"].copy(), desc, X.MODE_AUTO,
+                                X.F_INPLACE | X.F_IPHDR)
+        for family in (4, 6):
+            # ragged: 2999 frames is no multiple of any tile or region count
+            umem, gd = X.gen_frames_host(2999, family, 0, 1500, seed=21 + family)
+            mode = X.MODE_V6 if family == 6 else X.MODE_V4_LEGACY
+            for hint in (0, 100, 1500):
+                g2, _ = run_device(torch_cuda, engine, umem, gd, mode, len_hint=hint)
+                assert np.array_equal(g2, oracle.batch(umem, gd, mode)), (family, hint)
+    finally:
+        engine.set_order(-1, 0)
+    exp, exp_after = run_device(torch_cuda, engine, golden["umem"].copy(), desc, X.MODE_AUTO,
+                                X.F_INPLACE | X.F_IPHDR)
+    assert np.array_equal(got, exp)
+    assert np.array_equal(after, exp_after)
+
+
+def test_visiting_order_bad_arguments(engine):
+    for bad in ((-2, 0), (13, 0), (2, -1), (2, 17)):
+        with pytest.raises(X.XcsumError):
+            engine.set_order(*bad)

@@ -28,10 +28,14 @@ def main():
     ap.add_argument("--launches", type=int, default=20)
     ap.add_argument("--geoms", default="")
     ap.add_argument("--bpc", default="0", help="blocks per CU to try, e.g. 2,3,4 (0: default)")
+    ap.add_argument("--orders", default="-1,0",
+                    help="visiting orders to try, 'R,T;R,T' (log2 regions, log2 tile frames; "
+                         "-1,0 = automatic)")
+    ap.add_argument("--layout", default="packed", choices=["packed", "umem"])
     args = ap.parse_args()
     import torch
     dev = torch.device("cuda:0")
-    cfg = dict(bench.CONFIGS[args.config], id=args.config)
+    cfg = dict(bench.CONFIGS[args.config], id=args.config, layout=args.layout)
     eng = X.Engine(0)
     s = torch.cuda.current_stream(dev)
     desc, d_desc, bufs, out, first, count = bench.build_batch(cfg, 0, 1, torch, dev, eng,
@@ -40,12 +44,14 @@ def main():
     geoms = GEOMS if not args.geoms else [tuple(int(v) for v in g.split(","))
                                           for g in args.geoms.split(";")]
     bpcs = [int(b) for b in args.bpc.split(",")]
-    geoms = [(g, b) for g in geoms for b in bpcs]
+    orders = [tuple(int(v) for v in o.split(",")) for o in args.orders.split(";")]
+    geoms = [(g, b, o) for g in geoms for b in bpcs for o in orders]
     times = {g: [] for g in geoms}
     for r in range(args.rounds):
-        for g, b in geoms:
+        for g, b, o in geoms:
             eng.set_geometry(*g)
             eng.set_launch(b)
+            eng.set_order(*o)
             for k in range(3):
                 eng.batch_device(bufs[k % len(bufs)], d_desc, count, out, cfg["mode"],
                                  stream=s.cuda_stream)
@@ -57,10 +63,11 @@ def main():
                                  stream=s.cuda_stream)
                 evs[k][1].record(s)
             torch.cuda.synchronize()
-            times[(g, b)] += [e0.elapsed_time(e1) for e0, e1 in evs]
-    for g, b in geoms:
-        t = np.array(times[(g, b)])
-        print(json.dumps({"config": args.config, "geometry": g, "bpc": b, "median_ms": round(float(
+            times[(g, b, o)] += [e0.elapsed_time(e1) for e0, e1 in evs]
+    for g, b, o in geoms:
+        t = np.array(times[(g, b, o)])
+        print(json.dumps({"config": args.config, "layout": args.layout, "geometry": g, "bpc": b,
+                          "order": o, "median_ms": round(float(
             np.median(t)), 4), "min_ms": round(float(t.min()), 4), "GBps_median": round(
             alg / (np.median(t) * 1e-3) / 1e9, 1), "GBps_best": round(alg / (t.min() * 1e-3) / 1e9,
                                                                       1)}), flush=True)
