@@ -20,13 +20,13 @@
  * How (memory-bound integer reduction, no MFMA):
  *   - G lanes own one frame; each lane loads aligned 16-byte chunks
  *     (global_load_dwordx4, coalesced: the G lanes of a frame read G*16
- *     consecutive bytes per instruction) and masks the bytes outside the span
- *     only in the frame's first and last chunk;
+ *     consecutive bytes per instruction); the bytes outside the span are
+ *     taken back out only in the frame's first and last chunk;
  *   - per lane, two exact u32 sums with v_dot4_u32_u8: E = bytes at even
  *     addresses, O = bytes at odd addresses (2 VALU per dword);
  *     lane value = 256*E + O (or 256*O + E when the span starts odd);
- *   - G-lane butterfly reduction (ds_swizzle/DPP via __shfl_xor), lane 0 of
- *     the segment finalizes and stores 2 bytes.
+ *   - G-lane reduction with DPP row ops and gfx950 v_permlane{16,32}_swap,
+ *     lane 0 of the segment finalizes and stores 2 bytes.
  *   - persistent grid (<= 8 blocks/CU), frames strided over segments; each
  *     segment keeps U frames' loads in flight (K chunks per lane per frame
  *     preloaded), the rest of a jumbo frame streams in a tail loop.
@@ -49,9 +49,11 @@ static __device__ __forceinline__ uint32_t dot_odd(uint32_t w, uint32_t acc)
 }
 
 /* Per-frame geometry.  The span [lo, hi) is covered by nchunks aligned
- * 16-byte chunks starting at base = lo & ~15; `head` bytes before lo and
- * `tail` bytes after hi inside those chunks are summed and then subtracted
- * again by the one lane that holds the first / last chunk. */
+ * 16-byte chunks starting at base = lo & ~15; the `head` bytes before lo and
+ * the `tail` bytes after hi inside those chunks are summed and then taken out
+ * again by the lanes that hold the first / last chunk.  (Chunks cut from the
+ * span itself -- 2-byte aligned 16-byte loads, one mask -- were measured:
+ * misaligned global_load_dwordx4 runs at under half the rate, DESIGN.md.) */
 struct Frame {
 	const uint8_t *base;
 	uint8_t *eth;
@@ -142,10 +144,10 @@ static __device__ __forceinline__ Frame resolve(const CsumArgs &a, u32x4 d, bool
 	if (mode < 0 || len < hdr + 8u || len - hdr > 65535u)
 		mode = -1;
 	uintptr_t lo = (uintptr_t)f.eth + hdr - pre;
+	f.udp_len = len - hdr;
 	uintptr_t base = lo & ~(uintptr_t)15;
 	uint32_t span_end = len + pre - hdr + (uint32_t)(lo - base); /* hi - base */
 	f.base = (const uint8_t *)base;
-	f.udp_len = len - hdr;
 	f.odd = (uint32_t)lo & 1u;
 	f.head = (uint32_t)(lo - base);
 	f.nchunks = (span_end + 15) >> 4;
@@ -156,14 +158,6 @@ static __device__ __forceinline__ Frame resolve(const CsumArgs &a, u32x4 d, bool
 	return f;
 }
 
-static __device__ __forceinline__ uint32_t byte_mask(int lo, int hi)
-{
-	/* bytes [lo, hi) of a dword, lo/hi already clamped to [0, 4] */
-	int n = hi - lo;
-	return n <= 0 ? 0u : ((0xffffffffu >> (32 - 8 * n)) << (8 * lo));
-}
-
-static __device__ __forceinline__ int clamp4(int x) { return x < 0 ? 0 : (x > 4 ? 4 : x); }
 
 /* whole 16-byte chunk into E (bytes at even addresses) and O (odd) */
 static __device__ __forceinline__ void accum(u32x4 v, uint32_t &E, uint32_t &O)
@@ -174,18 +168,85 @@ static __device__ __forceinline__ void accum(u32x4 v, uint32_t &E, uint32_t &O)
 	E = dot_even(v.w, E); O = dot_odd(v.w, O);
 }
 
-/* take bytes [lo, hi) of a chunk back out of E and O */
-static __device__ __forceinline__ void drop(u32x4 v, int lo, int hi, uint32_t &E, uint32_t &O)
+/* Take bytes back out of E and O: the first n (drop_prefix) or the last n
+ * (drop_suffix) bytes of a chunk, n in [0, 15] (0: nothing).  Branch-free:
+ * byte masks from 64-bit shifts, one dot4 chain per parity. */
+static __device__ __forceinline__ void drop_masked(u32x4 v, uint64_t m0, uint64_t m1,
+						   uint32_t &E, uint32_t &O)
 {
-	uint32_t w;
-	w = v.x & byte_mask(clamp4(lo), clamp4(hi));
-	E -= dot_even(w, 0u); O -= dot_odd(w, 0u);
-	w = v.y & byte_mask(clamp4(lo - 4), clamp4(hi - 4));
-	E -= dot_even(w, 0u); O -= dot_odd(w, 0u);
-	w = v.z & byte_mask(clamp4(lo - 8), clamp4(hi - 8));
-	E -= dot_even(w, 0u); O -= dot_odd(w, 0u);
-	w = v.w & byte_mask(clamp4(lo - 12), clamp4(hi - 12));
-	E -= dot_even(w, 0u); O -= dot_odd(w, 0u);
+	const uint32_t w0 = v.x & (uint32_t)m0, w1 = v.y & (uint32_t)(m0 >> 32);
+	const uint32_t w2 = v.z & (uint32_t)m1, w3 = v.w & (uint32_t)(m1 >> 32);
+	uint32_t e = dot_even(w0, 0u), o = dot_odd(w0, 0u);
+	e = dot_even(w1, e); o = dot_odd(w1, o);
+	e = dot_even(w2, e); o = dot_odd(w2, o);
+	e = dot_even(w3, e); o = dot_odd(w3, o);
+	E -= e;
+	O -= o;
+}
+
+static __device__ __forceinline__ void drop_prefix(u32x4 v, uint32_t n, uint32_t &E, uint32_t &O)
+{
+	const uint64_t m0 = n >= 8 ? ~0ull : (1ull << (8 * (n & 7))) - 1;
+	const uint64_t m1 = n <= 8 ? 0ull : (1ull << (8 * (n & 7))) - 1;
+	drop_masked(v, m0, m1, E, O);
+}
+
+static __device__ __forceinline__ void drop_suffix(u32x4 v, uint32_t n, uint32_t &E, uint32_t &O)
+{
+	const uint64_t m1 = n == 0 ? 0ull : (n >= 8 ? ~0ull : ~0ull << (8 * (8 - n)));
+	const uint64_t m0 = n <= 8 ? 0ull : ~0ull << (8 * ((16 - n) & 7));
+	drop_masked(v, m0, m1, E, O);
+}
+
+/* edge bytes of chunk c of f, for the walking (jumbo) paths */
+static __device__ __forceinline__ void edge_fix_one(const Frame &f, uint32_t c, u32x4 v,
+						    uint32_t &E, uint32_t &O)
+{
+	if (c == 0)
+		drop_prefix(v, f.head, E, O);
+	if (c + 1 == f.nchunks)
+		drop_suffix(v, f.tail, E, O);
+}
+
+/* v_cndmask_b32 through inline asm: a per-lane pick the compiler cannot turn
+ * back into a runtime-indexed read of v[] (which it spills to scratch) */
+static __device__ __forceinline__ u32x4 pick_if(u32x4 a, u32x4 b, uint64_t lanes)
+{
+	u32x4 r;
+	asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r.x) : "v"(a.x), "v"(b.x), "s"(lanes));
+	asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r.y) : "v"(a.y), "v"(b.y), "s"(lanes));
+	asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r.z) : "v"(a.z), "v"(b.z), "s"(lanes));
+	asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r.w) : "v"(a.w), "v"(b.w), "s"(lanes));
+	return r;
+}
+
+/* Edge bytes of a frame whose chunks sit in v[0..K) of its G lanes (chunk
+ * lane + k*G), after all K were accumulated.  The head drop is branch-free
+ * (n = 0 outside lane 0).  The tail drop: with PICK every lane drops a
+ * suffix of the chunk it picks as its last (n = 0 where it holds none);
+ * without, only the lane holding the frame's last chunk does, in one block
+ * per k (1-2% better for K >= 3, tools/ab_libs.sh).  With U > 1 the
+ * compiler merges those blocks into a runtime-indexed read of v[] and spills
+ * it to scratch, so they use PICK.  A one-chunk frame's head and tail are
+ * disjoint bytes of the same chunk. */
+template <int G, int K, bool PICK>
+static __device__ __forceinline__ void edge_fix(const Frame &f, const u32x4 (&v)[K],
+						uint32_t lane, uint32_t &E, uint32_t &O)
+{
+	const uint32_t last = f.nchunks - 1;
+	drop_prefix(v[0], lane == 0 && f.nchunks ? f.head : 0u, E, O);
+	if (PICK) {
+		u32x4 vl = v[0];
+#pragma unroll
+		for (int k = 1; k < K; k++)
+			vl = pick_if(vl, v[k], __builtin_amdgcn_ballot_w64((last / G) == (uint32_t)k));
+		drop_suffix(vl, f.nchunks && lane == (last & (G - 1)) ? f.tail : 0u, E, O);
+	} else if (f.tail && f.nchunks && lane == (last & (G - 1))) {
+#pragma unroll
+		for (int k = 0; k < K; k++)
+			if ((last / G) == (uint32_t)k)
+				drop_suffix(v[k], f.tail, E, O);
+	}
 }
 
 /* Sum over each aligned group of G lanes, result in every lane of the group.
@@ -321,7 +382,13 @@ static __device__ __forceinline__ void issue(const Frame (&f)[U], uint32_t lane,
 }
 
 /* accumulate, reduce and finalize the U frames of one iteration */
-template <int G, int U, int K, bool TAIL>
+template <bool ORD>
+static __device__ __forceinline__ uint32_t fidx(const CsumArgs &a, uint32_t p)
+{
+	return ORD ? frame_of(a.ord, p) : p;
+}
+
+template <int G, int U, int K, bool TAIL, bool ORD>
 static __device__ __forceinline__ void consume(const CsumArgs &a, const Frame (&fc)[U],
 					       const u32x4 (&vc)[U][K], uint32_t lane,
 					       uint32_t p0, uint32_t nseg)
@@ -329,35 +396,24 @@ static __device__ __forceinline__ void consume(const CsumArgs &a, const Frame (&
 #pragma unroll
 	for (int u = 0; u < U; u++) {
 		const Frame &f = fc[u];
-		const uint32_t last = f.nchunks - 1;
 		uint32_t E = 0, O = 0;
 		if (!TAIL || f.nchunks <= K * G) {
 #pragma unroll
 			for (int k = 0; k < K; k++)
 				accum(vc[u][k], E, O);
-			if (lane == 0 && f.head)
-				drop(vc[u][0], 0, (int)f.head, E, O);
-			if (f.tail && lane == (last & (G - 1))) {
-#pragma unroll
-				for (int k = 0; k < K; k++)
-					if ((last / G) == (uint32_t)k)
-						drop(vc[u][k], 16 - (int)f.tail, 16, E, O);
-			}
+			edge_fix<G, K, (K <= 2 || U > 1)>(f, vc[u], lane, E, O);
 		} else {
 			/* jumbo frame: plain strided walk over all its chunks */
 			for (uint32_t c = lane; c < f.nchunks; c += G) {
 				u32x4 v = load_chunk(f.base + 16u * c);
 				accum(v, E, O);
-				if (c == 0)
-					drop(v, 0, (int)f.head, E, O);
-				if (c == last)
-					drop(v, 16 - (int)f.tail, 16, E, O);
+				edge_fix_one(f, c, v, E, O);
 			}
 		}
 		uint32_t s = f.odd ? (O << 8) + E : (E << 8) + O;
 		s = seg_sum<G>(s);
 		if (lane == 0 && f.mode != -2)
-			finalize(a, f, frame_of(a.ord, p0 + u * nseg), s);
+			finalize(a, f, fidx<ORD>(a, p0 + u * nseg), s);
 	}
 }
 
@@ -369,10 +425,9 @@ static __device__ __forceinline__ void consume(const CsumArgs &a, const Frame (&
  * BEFORE the chunk loads of the same step, so the in-order vmcnt wait for
  * them never waits on chunk data.
  */
-template <int G, int U, int K>
-__global__ void __launch_bounds__(256) csum_kernel(CsumArgs a)
+template <int G, int U, int K, bool ORD>
+static __device__ __forceinline__ void csum_loop(const CsumArgs &a)
 {
-	resolve_order(a);
 	const uint32_t lane = threadIdx.x & (G - 1);
 	uint32_t seg = (blockIdx.x * 256u + threadIdx.x) / G;
 	const uint32_t nseg = gridDim.x * (256u / G);
@@ -385,28 +440,28 @@ __global__ void __launch_bounds__(256) csum_kernel(CsumArgs a)
 	u32x4 vc[U][K];
 #pragma unroll
 	for (int u = 0; u < U; u++)
-		d[u] = load_desc<G == 64>(a, frame_of(a.ord, seg + u * nseg));
+		d[u] = load_desc<G == 64>(a, fidx<ORD>(a, seg + u * nseg));
 #pragma unroll
 	for (int u = 0; u < U; u++)
-		fc[u] = resolve(a, d[u], frame_of(a.ord, seg + u * nseg) < a.n);
+		fc[u] = resolve(a, d[u], fidx<ORD>(a, seg + u * nseg) < a.n);
 #pragma unroll
 	for (int u = 0; u < U; u++)
-		d[u] = load_desc<G == 64>(a, frame_of(a.ord, seg + step + u * nseg));
+		d[u] = load_desc<G == 64>(a, fidx<ORD>(a, seg + step + u * nseg));
 	/* keep every descriptor load older than the chunk loads it shares a
 	 * vmcnt queue with: the next wait for the descriptors then leaves all
 	 * chunk loads in flight */
 	__builtin_amdgcn_sched_barrier(0);
 	issue<G, U, K>(fc, lane, vc);
 
-	for (uint32_t p0 = seg; p0 < a.ord.nlog; p0 += step) {
+	for (uint32_t p0 = seg; p0 < (ORD ? a.ord.nlog : a.n); p0 += step) {
 		Frame fn[U];
 		u32x4 vn[U][K];
 #pragma unroll
 		for (int u = 0; u < U; u++)
-			fn[u] = resolve(a, d[u], frame_of(a.ord, p0 + step + u * nseg) < a.n);
+			fn[u] = resolve(a, d[u], fidx<ORD>(a, p0 + step + u * nseg) < a.n);
 #pragma unroll
 		for (int u = 0; u < U; u++)
-			d[u] = load_desc<G == 64>(a, frame_of(a.ord, p0 + 2 * step + u * nseg));
+			d[u] = load_desc<G == 64>(a, fidx<ORD>(a, p0 + 2 * step + u * nseg));
 		__builtin_amdgcn_sched_barrier(0);
 		issue<G, U, K>(fn, lane, vn);
 
@@ -418,9 +473,9 @@ __global__ void __launch_bounds__(256) csum_kernel(CsumArgs a)
 		for (int u = 0; u < U; u++)
 			big |= fc[u].nchunks > K * G;
 		if (__builtin_amdgcn_ballot_w64(big))
-			consume<G, U, K, true>(a, fc, vc, lane, p0, nseg);
+			consume<G, U, K, true, ORD>(a, fc, vc, lane, p0, nseg);
 		else
-			consume<G, U, K, false>(a, fc, vc, lane, p0, nseg);
+			consume<G, U, K, false, ORD>(a, fc, vc, lane, p0, nseg);
 #pragma unroll
 		for (int u = 0; u < U; u++) {
 			fc[u] = fn[u];
@@ -429,6 +484,19 @@ __global__ void __launch_bounds__(256) csum_kernel(CsumArgs a)
 				vc[u][k] = vn[u][k];
 		}
 	}
+}
+
+/* The identity order gets its own copy of the loop, so descriptor-order
+ * batches pay nothing for the region order; which copy runs is decided once
+ * per launch (uniform branch, after resolve_order). */
+template <int G, int U, int K>
+__global__ void __launch_bounds__(256) csum_kernel(CsumArgs a)
+{
+	resolve_order(a);
+	if (a.ord.rshift == 0)
+		csum_loop<G, U, K, false>(a);
+	else
+		csum_loop<G, U, K, true>(a);
 }
 
 /* ---- LDS-staged variant ---------------------------------------------------
@@ -522,29 +590,18 @@ __global__ void __launch_bounds__(256) csum_lds_kernel(CsumArgs a)
 			issue_stage(fn, d);
 			__builtin_amdgcn_sched_barrier(0);
 			const Frame &f = fs[d];
-			const uint32_t last = f.nchunks - 1;
 			uint32_t E = 0, O = 0;
 			if (__builtin_amdgcn_ballot_w64(f.nchunks > K * G)) {
 				for (uint32_t c = lane; c < f.nchunks; c += G) {
 					u32x4 w = load_chunk(f.base + 16u * c);
 					accum(w, E, O);
-					if (c == 0)
-						drop(w, 0, (int)f.head, E, O);
-					if (c == last)
-						drop(w, 16 - (int)f.tail, 16, E, O);
+					edge_fix_one(f, c, w, E, O);
 				}
 			} else {
 #pragma unroll
 				for (int k = 0; k < K; k++)
 					accum(v[k], E, O);
-				if (lane == 0 && f.head)
-					drop(v[0], 0, (int)f.head, E, O);
-				if (f.tail && lane == (last & (G - 1))) {
-#pragma unroll
-					for (int k = 0; k < K; k++)
-						if ((last / G) == (uint32_t)k)
-							drop(v[k], 16 - (int)f.tail, 16, E, O);
-				}
+				edge_fix<G, K, true>(f, v, lane, E, O);
 			}
 			uint32_t sum = f.odd ? (O << 8) + E : (E << 8) + O;
 			sum = seg_sum<G>(sum);
