@@ -48,12 +48,15 @@ static __device__ __forceinline__ uint32_t dot_odd(uint32_t w, uint32_t acc)
 	return __builtin_amdgcn_udot4(w, 0x01000100u, acc, false);
 }
 
-/* Per-frame geometry.  The span [lo, hi) is covered by nchunks aligned
- * 16-byte chunks starting at base = lo & ~15; the `head` bytes before lo and
- * the `tail` bytes after hi inside those chunks are summed and then taken out
- * again by the lanes that hold the first / last chunk.  (Chunks cut from the
- * span itself -- 2-byte aligned 16-byte loads, one mask -- were measured:
- * misaligned global_load_dwordx4 runs at under half the rate, DESIGN.md.) */
+/* Per-frame geometry.  The span [lo, hi) is covered by nchunks 16-byte
+ * chunks laid back from E4 = hi rounded up to 4 bytes: chunk c is
+ * [E4 - 16*(nchunks - c), ...), so every chunk is dword aligned (16-byte
+ * loads from dword-aligned addresses stream at full rate; 2-byte aligned ones
+ * do not, tools/slot_probe.py) and nothing past hi's own dword is read.  The
+ * first chunk starts up to 15 bytes before lo, still inside the frame's
+ * headers.  The `head` bytes before lo (0..15, first chunk) and the `tail`
+ * bytes after hi (0..3, top of the last dword) are masked to zero BEFORE the
+ * chunk is summed. */
 struct Frame {
 	const uint8_t *base;
 	uint8_t *eth;
@@ -145,13 +148,14 @@ static __device__ __forceinline__ Frame resolve(const CsumArgs &a, u32x4 d, bool
 		mode = -1;
 	uintptr_t lo = (uintptr_t)f.eth + hdr - pre;
 	f.udp_len = len - hdr;
-	uintptr_t base = lo & ~(uintptr_t)15;
-	uint32_t span_end = len + pre - hdr + (uint32_t)(lo - base); /* hi - base */
+	const uintptr_t hi = lo + (len + pre - hdr);
+	const uintptr_t e4 = (hi + 3) & ~(uintptr_t)3;
+	f.nchunks = (uint32_t)(e4 - lo + 15) >> 4;
+	const uintptr_t base = e4 - 16u * f.nchunks;
 	f.base = (const uint8_t *)base;
 	f.odd = (uint32_t)lo & 1u;
 	f.head = (uint32_t)(lo - base);
-	f.nchunks = (span_end + 15) >> 4;
-	f.tail = (f.nchunks << 4) - span_end;
+	f.tail = (uint32_t)(e4 - hi);
 	if (mode < 0 || !present)
 		f.nchunks = 0;
 	f.mode = present ? mode : -2;
@@ -168,85 +172,48 @@ static __device__ __forceinline__ void accum(u32x4 v, uint32_t &E, uint32_t &O)
 	E = dot_even(v.w, E); O = dot_odd(v.w, O);
 }
 
-/* Take bytes back out of E and O: the first n (drop_prefix) or the last n
- * (drop_suffix) bytes of a chunk, n in [0, 15] (0: nothing).  Branch-free:
- * byte masks from 64-bit shifts, one dot4 chain per parity. */
-static __device__ __forceinline__ void drop_masked(u32x4 v, uint64_t m0, uint64_t m1,
-						   uint32_t &E, uint32_t &O)
+/* Edge masks, applied to the chunks before they are summed: the first
+ * chunk keeps bytes [head, 16), the last keeps all but the top `tail` bytes
+ * of its last dword.  Built from 64-bit shifts, no branches. */
+static __device__ __forceinline__ u32x4 and_head(u32x4 v, uint32_t head)
 {
-	const uint32_t w0 = v.x & (uint32_t)m0, w1 = v.y & (uint32_t)(m0 >> 32);
-	const uint32_t w2 = v.z & (uint32_t)m1, w3 = v.w & (uint32_t)(m1 >> 32);
-	uint32_t e = dot_even(w0, 0u), o = dot_odd(w0, 0u);
-	e = dot_even(w1, e); o = dot_odd(w1, o);
-	e = dot_even(w2, e); o = dot_odd(w2, o);
-	e = dot_even(w3, e); o = dot_odd(w3, o);
-	E -= e;
-	O -= o;
+	const uint64_t k0 = head >= 8 ? 0ull : ~0ull << (8 * (head & 7));
+	const uint64_t k1 = head <= 8 ? ~0ull : ~0ull << (8 * (head & 7));
+	v.x &= (uint32_t)k0;
+	v.y &= (uint32_t)(k0 >> 32);
+	v.z &= (uint32_t)k1;
+	v.w &= (uint32_t)(k1 >> 32);
+	return v;
 }
 
-static __device__ __forceinline__ void drop_prefix(u32x4 v, uint32_t n, uint32_t &E, uint32_t &O)
+static __device__ __forceinline__ uint32_t tail_keep(uint32_t tail)
 {
-	const uint64_t m0 = n >= 8 ? ~0ull : (1ull << (8 * (n & 7))) - 1;
-	const uint64_t m1 = n <= 8 ? 0ull : (1ull << (8 * (n & 7))) - 1;
-	drop_masked(v, m0, m1, E, O);
+	return 0xffffffffu >> (8 * tail);   /* tail <= 3 */
 }
 
-static __device__ __forceinline__ void drop_suffix(u32x4 v, uint32_t n, uint32_t &E, uint32_t &O)
-{
-	const uint64_t m1 = n == 0 ? 0ull : (n >= 8 ? ~0ull : ~0ull << (8 * (8 - n)));
-	const uint64_t m0 = n <= 8 ? 0ull : ~0ull << (8 * ((16 - n) & 7));
-	drop_masked(v, m0, m1, E, O);
-}
-
-/* edge bytes of chunk c of f, for the walking (jumbo) paths */
-static __device__ __forceinline__ void edge_fix_one(const Frame &f, uint32_t c, u32x4 v,
-						    uint32_t &E, uint32_t &O)
+/* chunk c of f, masked, for the walking (jumbo) paths */
+static __device__ __forceinline__ u32x4 edge_mask_one(const Frame &f, uint32_t c, u32x4 v)
 {
 	if (c == 0)
-		drop_prefix(v, f.head, E, O);
+		v = and_head(v, f.head);
 	if (c + 1 == f.nchunks)
-		drop_suffix(v, f.tail, E, O);
+		v.w &= tail_keep(f.tail);
+	return v;
 }
 
-/* v_cndmask_b32 through inline asm: a per-lane pick the compiler cannot turn
- * back into a runtime-indexed read of v[] (which it spills to scratch) */
-static __device__ __forceinline__ u32x4 pick_if(u32x4 a, u32x4 b, uint64_t lanes)
-{
-	u32x4 r;
-	asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r.x) : "v"(a.x), "v"(b.x), "s"(lanes));
-	asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r.y) : "v"(a.y), "v"(b.y), "s"(lanes));
-	asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r.z) : "v"(a.z), "v"(b.z), "s"(lanes));
-	asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r.w) : "v"(a.w), "v"(b.w), "s"(lanes));
-	return r;
-}
-
-/* Edge bytes of a frame whose chunks sit in v[0..K) of its G lanes (chunk
- * lane + k*G), after all K were accumulated.  The head drop is branch-free
- * (n = 0 outside lane 0).  The tail drop: with PICK every lane drops a
- * suffix of the chunk it picks as its last (n = 0 where it holds none);
- * without, only the lane holding the frame's last chunk does, in one block
- * per k (1-2% better for K >= 3, tools/ab_libs.sh).  With U > 1 the
- * compiler merges those blocks into a runtime-indexed read of v[] and spills
- * it to scratch, so they use PICK.  A one-chunk frame's head and tail are
- * disjoint bytes of the same chunk. */
-template <int G, int K, bool PICK>
-static __device__ __forceinline__ void edge_fix(const Frame &f, const u32x4 (&v)[K],
-						uint32_t lane, uint32_t &E, uint32_t &O)
+/* Edge masks for a frame whose chunks sit in v[0..K) of its G lanes (chunk
+ * lane + k*G): lane 0 masks its first chunk, the lane holding the last
+ * chunk masks that chunk's last dword.  Every lane runs the same code with
+ * all-ones masks where it holds no edge.  A one-chunk frame gets both. */
+template <int G, int K>
+static __device__ __forceinline__ void edge_mask(const Frame &f, u32x4 (&v)[K], uint32_t lane)
 {
 	const uint32_t last = f.nchunks - 1;
-	drop_prefix(v[0], lane == 0 && f.nchunks ? f.head : 0u, E, O);
-	if (PICK) {
-		u32x4 vl = v[0];
+	v[0] = and_head(v[0], lane == 0 ? f.head : 0u);
+	const uint32_t tk = tail_keep(f.tail);
 #pragma unroll
-		for (int k = 1; k < K; k++)
-			vl = pick_if(vl, v[k], __builtin_amdgcn_ballot_w64((last / G) == (uint32_t)k));
-		drop_suffix(vl, f.nchunks && lane == (last & (G - 1)) ? f.tail : 0u, E, O);
-	} else if (f.tail && f.nchunks && lane == (last & (G - 1))) {
-#pragma unroll
-		for (int k = 0; k < K; k++)
-			if ((last / G) == (uint32_t)k)
-				drop_suffix(v[k], f.tail, E, O);
-	}
+	for (int k = 0; k < K; k++)
+		v[k].w &= lane + k * G == last ? tk : 0xffffffffu;
 }
 
 /* Sum over each aligned group of G lanes, result in every lane of the group.
@@ -398,17 +365,18 @@ static __device__ __forceinline__ void consume(const CsumArgs &a, const Frame (&
 		const Frame &f = fc[u];
 		uint32_t E = 0, O = 0;
 		if (!TAIL || f.nchunks <= K * G) {
+			u32x4 v[K];
 #pragma unroll
 			for (int k = 0; k < K; k++)
-				accum(vc[u][k], E, O);
-			edge_fix<G, K, (K <= 2 || U > 1)>(f, vc[u], lane, E, O);
+				v[k] = vc[u][k];
+			edge_mask<G, K>(f, v, lane);
+#pragma unroll
+			for (int k = 0; k < K; k++)
+				accum(v[k], E, O);
 		} else {
 			/* jumbo frame: plain strided walk over all its chunks */
-			for (uint32_t c = lane; c < f.nchunks; c += G) {
-				u32x4 v = load_chunk(f.base + 16u * c);
-				accum(v, E, O);
-				edge_fix_one(f, c, v, E, O);
-			}
+			for (uint32_t c = lane; c < f.nchunks; c += G)
+				accum(edge_mask_one(f, c, load_chunk(f.base + 16u * c)), E, O);
 		}
 		uint32_t s = f.odd ? (O << 8) + E : (E << 8) + O;
 		s = seg_sum<G>(s);
@@ -592,16 +560,13 @@ __global__ void __launch_bounds__(256) csum_lds_kernel(CsumArgs a)
 			const Frame &f = fs[d];
 			uint32_t E = 0, O = 0;
 			if (__builtin_amdgcn_ballot_w64(f.nchunks > K * G)) {
-				for (uint32_t c = lane; c < f.nchunks; c += G) {
-					u32x4 w = load_chunk(f.base + 16u * c);
-					accum(w, E, O);
-					edge_fix_one(f, c, w, E, O);
-				}
+				for (uint32_t c = lane; c < f.nchunks; c += G)
+					accum(edge_mask_one(f, c, load_chunk(f.base + 16u * c)), E, O);
 			} else {
+				edge_mask<G, K>(f, v, lane);
 #pragma unroll
 				for (int k = 0; k < K; k++)
 					accum(v[k], E, O);
-				edge_fix<G, K, true>(f, v, lane, E, O);
 			}
 			uint32_t sum = f.odd ? (O << 8) + E : (E << 8) + O;
 			sum = seg_sum<G>(sum);

@@ -36,6 +36,11 @@ def main():
              ("4096_fixed_scattered_groups16", 4096, 368, 0, 0, 0x9E3779B1, 4),
              ("4096_fixed_scattered_groups256", 4096, 368, 0, 0, 0x9E3779B1, 8),
              ("xudp_2048_fixed_off_368", 2048, 368, 0, 0, 0, 0),
+             # 16-byte loads at 8/4/2-byte aligned addresses (packed 1520-B slots)
+             ("packed1520_align16", 1520, 0, 0, 0, 0, 0),
+             ("packed1520_align8", 1520, 8, 0, 0, 0, 0),
+             ("packed1520_align4", 1520, 4, 0, 0, 0, 0),
+             ("packed1520_align2", 1520, 2, 0, 0, 0, 0),
              ("2048_rotated_off", 2048, 0, 7, (2048 - span16 * 16) // 16, 0, 0)]
     for name, slot, off0, rot, nrot, pm, ps in cases:
         assert (nslots - 1) * slot + off0 + max(nrot - 1, 0) * 16 + span16 * 16 <= buf.numel()
