@@ -48,15 +48,19 @@ static __device__ __forceinline__ uint32_t dot_odd(uint32_t w, uint32_t acc)
 	return __builtin_amdgcn_udot4(w, 0x01000100u, acc, false);
 }
 
-/* Per-frame geometry.  The span [lo, hi) is covered by nchunks 16-byte
- * chunks laid back from E4 = hi rounded up to 4 bytes: chunk c is
- * [E4 - 16*(nchunks - c), ...), so every chunk is dword aligned (16-byte
- * loads from dword-aligned addresses stream at full rate; 2-byte aligned ones
- * do not, tools/slot_probe.py) and nothing past hi's own dword is read.  The
- * first chunk starts up to 15 bytes before lo, still inside the frame's
- * headers.  The `head` bytes before lo (0..15, first chunk) and the `tail`
- * bytes after hi (0..3, top of the last dword) are masked to zero BEFORE the
- * chunk is summed. */
+/* Per-frame geometry: the span [lo, hi) is covered by nchunks 16-byte
+ * chunks from base, with `head` bytes before lo in the first chunk and
+ * `tail` bytes after hi in the last one.  Two chunk grids (template DW):
+ *   DW = true: laid back from E4 = hi rounded up to 4 bytes, chunk c =
+ *     [E4 - 16*(nchunks - c), ...).  Chunks are dword aligned (16-byte loads
+ *     at dword alignment stream at full rate, 2-byte aligned ones do not,
+ *     tools/slot_probe.py); head 0..15 (the first chunk starts inside the
+ *     frame's headers), tail 0..3; both masked to zero BEFORE summing.
+ *   DW = false: 16-byte aligned from lo & ~15; head and tail 0..15, summed
+ *     and then taken back out of E/O by the lanes holding the edge chunks.
+ * Neither reads past the 16-byte block (DW: the dword) holding hi - 1.
+ * DW wins where edge work is a large share (small frames, G = 64); aligned
+ * chunks win by ~1% for MTU frames at G = 16 (profiles/r01/ab). */
 struct Frame {
 	const uint8_t *base;
 	uint8_t *eth;
@@ -125,6 +129,7 @@ static __device__ __forceinline__ u32x4 load_desc(const CsumArgs &a, uint32_t p)
 	return *((gu32x4 *)(a.desc + q));
 }
 
+template <bool DW>
 static __device__ __forceinline__ Frame resolve(const CsumArgs &a, u32x4 d, bool present)
 {
 	Frame f;
@@ -149,13 +154,21 @@ static __device__ __forceinline__ Frame resolve(const CsumArgs &a, u32x4 d, bool
 	uintptr_t lo = (uintptr_t)f.eth + hdr - pre;
 	f.udp_len = len - hdr;
 	const uintptr_t hi = lo + (len + pre - hdr);
-	const uintptr_t e4 = (hi + 3) & ~(uintptr_t)3;
-	f.nchunks = (uint32_t)(e4 - lo + 15) >> 4;
-	const uintptr_t base = e4 - 16u * f.nchunks;
-	f.base = (const uint8_t *)base;
 	f.odd = (uint32_t)lo & 1u;
-	f.head = (uint32_t)(lo - base);
-	f.tail = (uint32_t)(e4 - hi);
+	if (DW) {
+		const uintptr_t e4 = (hi + 3) & ~(uintptr_t)3;
+		f.nchunks = (uint32_t)(e4 - lo + 15) >> 4;
+		const uintptr_t base = e4 - 16u * f.nchunks;
+		f.base = (const uint8_t *)base;
+		f.head = (uint32_t)(lo - base);
+		f.tail = (uint32_t)(e4 - hi);
+	} else {
+		const uintptr_t base = lo & ~(uintptr_t)15;
+		f.nchunks = (uint32_t)(hi - base + 15) >> 4;
+		f.base = (const uint8_t *)base;
+		f.head = (uint32_t)(lo - base);
+		f.tail = (f.nchunks << 4) - (uint32_t)(hi - base);
+	}
 	if (mode < 0 || !present)
 		f.nchunks = 0;
 	f.mode = present ? mode : -2;
@@ -215,6 +228,125 @@ static __device__ __forceinline__ void edge_mask(const Frame &f, u32x4 (&v)[K], 
 	for (int k = 0; k < K; k++)
 		v[k].w &= lane + k * G == last ? tk : 0xffffffffu;
 }
+
+/* ---- aligned grid (DW = false): take edge bytes back out after summing */
+static __device__ __forceinline__ void drop_masked(u32x4 v, uint64_t m0, uint64_t m1,
+						   uint32_t &E, uint32_t &O)
+{
+	const uint32_t w0 = v.x & (uint32_t)m0, w1 = v.y & (uint32_t)(m0 >> 32);
+	const uint32_t w2 = v.z & (uint32_t)m1, w3 = v.w & (uint32_t)(m1 >> 32);
+	uint32_t e = dot_even(w0, 0u), o = dot_odd(w0, 0u);
+	e = dot_even(w1, e); o = dot_odd(w1, o);
+	e = dot_even(w2, e); o = dot_odd(w2, o);
+	e = dot_even(w3, e); o = dot_odd(w3, o);
+	E -= e;
+	O -= o;
+}
+
+/* the first n / last n bytes of a chunk, n in [0, 15] (0: nothing) */
+static __device__ __forceinline__ void drop_prefix(u32x4 v, uint32_t n, uint32_t &E, uint32_t &O)
+{
+	const uint64_t m0 = n >= 8 ? ~0ull : (1ull << (8 * (n & 7))) - 1;
+	const uint64_t m1 = n <= 8 ? 0ull : (1ull << (8 * (n & 7))) - 1;
+	drop_masked(v, m0, m1, E, O);
+}
+
+static __device__ __forceinline__ void drop_suffix(u32x4 v, uint32_t n, uint32_t &E, uint32_t &O)
+{
+	const uint64_t m1 = n == 0 ? 0ull : (n >= 8 ? ~0ull : ~0ull << (8 * (8 - n)));
+	const uint64_t m0 = n <= 8 ? 0ull : ~0ull << (8 * ((16 - n) & 7));
+	drop_masked(v, m0, m1, E, O);
+}
+
+/* v_cndmask_b32 through inline asm: a per-lane pick the compiler cannot turn
+ * back into a runtime-indexed read of v[] (which it spills to scratch) */
+static __device__ __forceinline__ u32x4 pick_if(u32x4 a, u32x4 b, uint64_t lanes)
+{
+	u32x4 r;
+	asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r.x) : "v"(a.x), "v"(b.x), "s"(lanes));
+	asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r.y) : "v"(a.y), "v"(b.y), "s"(lanes));
+	asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r.z) : "v"(a.z), "v"(b.z), "s"(lanes));
+	asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r.w) : "v"(a.w), "v"(b.w), "s"(lanes));
+	return r;
+}
+
+/* After all K chunks were summed: lane 0 takes the head bytes of its first
+ * chunk back out (branch-free, n = 0 elsewhere); the tail comes out of the
+ * lane holding the last chunk, in one constant-index block per k -- or, with
+ * U > 1 (where the compiler merges those blocks into a runtime-indexed,
+ * scratch-spilled read of v[]), from a chunk every lane picks. */
+template <int G, int K, int U>
+static __device__ __forceinline__ void edge_drop(const Frame &f, const u32x4 (&v)[K],
+						 uint32_t lane, uint32_t &E, uint32_t &O)
+{
+	const uint32_t last = f.nchunks - 1;
+	drop_prefix(v[0], lane == 0 && f.nchunks ? f.head : 0u, E, O);
+	if (U > 1) {
+		u32x4 vl = v[0];
+#pragma unroll
+		for (int k = 1; k < K; k++)
+			vl = pick_if(vl, v[k], __builtin_amdgcn_ballot_w64((last / G) == (uint32_t)k));
+		drop_suffix(vl, f.nchunks && lane == (last & (G - 1)) ? f.tail : 0u, E, O);
+	} else if (f.tail && f.nchunks && lane == (last & (G - 1))) {
+#pragma unroll
+		for (int k = 0; k < K; k++)
+			if ((last / G) == (uint32_t)k)
+				drop_suffix(v[k], f.tail, E, O);
+	}
+}
+
+static __device__ __forceinline__ void edge_drop_one(const Frame &f, uint32_t c, u32x4 v,
+						     uint32_t &E, uint32_t &O)
+{
+	if (c == 0)
+		drop_prefix(v, f.head, E, O);
+	if (c + 1 == f.nchunks)
+		drop_suffix(v, f.tail, E, O);
+}
+
+/* all K chunks of a frame into E/O, edges handled per grid */
+template <int G, int K, int U, bool DW>
+static __device__ __forceinline__ void sum_frame(const Frame &f, const u32x4 (&vc)[K],
+						 uint32_t lane, uint32_t &E, uint32_t &O)
+{
+	if (DW) {
+		u32x4 v[K];
+#pragma unroll
+		for (int k = 0; k < K; k++)
+			v[k] = vc[k];
+		edge_mask<G, K>(f, v, lane);
+#pragma unroll
+		for (int k = 0; k < K; k++)
+			accum(v[k], E, O);
+	} else {
+#pragma unroll
+		for (int k = 0; k < K; k++)
+			accum(vc[k], E, O);
+		edge_drop<G, K, U>(f, vc, lane, E, O);
+	}
+}
+
+/* walking (jumbo) path: every chunk of f strided over G lanes */
+template <int G, bool DW>
+static __device__ __forceinline__ void sum_walk(const Frame &f, uint32_t lane, uint32_t &E,
+						uint32_t &O)
+{
+	for (uint32_t c = lane; c < f.nchunks; c += G) {
+		u32x4 v = load_chunk(f.base + 16u * c);
+		if (DW) {
+			accum(edge_mask_one(f, c, v), E, O);
+		} else {
+			accum(v, E, O);
+			edge_drop_one(f, c, v, E, O);
+		}
+	}
+}
+
+/* the chunk grid a geometry uses (measured, see the Frame comment) */
+template <int G, int K>
+struct Grid {
+	static constexpr bool DW = !(G == 16 && K >= 6) && !(G == 8 && K >= 12);
+};
 
 /* Sum over each aligned group of G lanes, result in every lane of the group.
  * DPP adds within a 16-lane row (quad_perm xor 1, xor 2, row_half_mirror,
@@ -364,20 +496,10 @@ static __device__ __forceinline__ void consume(const CsumArgs &a, const Frame (&
 	for (int u = 0; u < U; u++) {
 		const Frame &f = fc[u];
 		uint32_t E = 0, O = 0;
-		if (!TAIL || f.nchunks <= K * G) {
-			u32x4 v[K];
-#pragma unroll
-			for (int k = 0; k < K; k++)
-				v[k] = vc[u][k];
-			edge_mask<G, K>(f, v, lane);
-#pragma unroll
-			for (int k = 0; k < K; k++)
-				accum(v[k], E, O);
-		} else {
-			/* jumbo frame: plain strided walk over all its chunks */
-			for (uint32_t c = lane; c < f.nchunks; c += G)
-				accum(edge_mask_one(f, c, load_chunk(f.base + 16u * c)), E, O);
-		}
+		if (!TAIL || f.nchunks <= K * G)
+			sum_frame<G, K, U, Grid<G, K>::DW>(f, vc[u], lane, E, O);
+		else
+			sum_walk<G, Grid<G, K>::DW>(f, lane, E, O);   /* jumbo frame */
 		uint32_t s = f.odd ? (O << 8) + E : (E << 8) + O;
 		s = seg_sum<G>(s);
 		if (lane == 0 && f.mode != -2)
@@ -411,7 +533,7 @@ static __device__ __forceinline__ void csum_loop(const CsumArgs &a)
 		d[u] = load_desc<G == 64>(a, fidx<ORD>(a, seg + u * nseg));
 #pragma unroll
 	for (int u = 0; u < U; u++)
-		fc[u] = resolve(a, d[u], fidx<ORD>(a, seg + u * nseg) < a.n);
+		fc[u] = resolve<Grid<G, K>::DW>(a, d[u], fidx<ORD>(a, seg + u * nseg) < a.n);
 #pragma unroll
 	for (int u = 0; u < U; u++)
 		d[u] = load_desc<G == 64>(a, fidx<ORD>(a, seg + step + u * nseg));
@@ -426,7 +548,7 @@ static __device__ __forceinline__ void csum_loop(const CsumArgs &a)
 		u32x4 vn[U][K];
 #pragma unroll
 		for (int u = 0; u < U; u++)
-			fn[u] = resolve(a, d[u], fidx<ORD>(a, p0 + step + u * nseg) < a.n);
+			fn[u] = resolve<Grid<G, K>::DW>(a, d[u], fidx<ORD>(a, p0 + step + u * nseg) < a.n);
 #pragma unroll
 		for (int u = 0; u < U; u++)
 			d[u] = load_desc<G == 64>(a, fidx<ORD>(a, p0 + 2 * step + u * nseg));
@@ -515,7 +637,7 @@ __global__ void __launch_bounds__(256) csum_lds_kernel(CsumArgs a)
 		uint32_t f = frame0(j);
 		u32x4 d = pick(load_desc_scalar(a, f), load_desc_scalar(a, f + 1),
 			       load_desc_scalar(a, f + 2), load_desc_scalar(a, f + 3));
-		return resolve(a, d, f + sub < a.n);
+		return resolve<Grid<G, K>::DW>(a, d, f + sub < a.n);
 	};
 	auto issue_stage = [&](const Frame &f, int slot) {
 #pragma unroll
@@ -559,15 +681,10 @@ __global__ void __launch_bounds__(256) csum_lds_kernel(CsumArgs a)
 			__builtin_amdgcn_sched_barrier(0);
 			const Frame &f = fs[d];
 			uint32_t E = 0, O = 0;
-			if (__builtin_amdgcn_ballot_w64(f.nchunks > K * G)) {
-				for (uint32_t c = lane; c < f.nchunks; c += G)
-					accum(edge_mask_one(f, c, load_chunk(f.base + 16u * c)), E, O);
-			} else {
-				edge_mask<G, K>(f, v, lane);
-#pragma unroll
-				for (int k = 0; k < K; k++)
-					accum(v[k], E, O);
-			}
+			if (__builtin_amdgcn_ballot_w64(f.nchunks > K * G))
+				sum_walk<G, Grid<G, K>::DW>(f, lane, E, O);
+			else
+				sum_frame<G, K, 2, Grid<G, K>::DW>(f, v, lane, E, O);
 			uint32_t sum = f.odd ? (O << 8) + E : (E << 8) + O;
 			sum = seg_sum<G>(sum);
 			if (lane == 0 && f.mode != -2)
