@@ -170,6 +170,52 @@ int xcsum_build_device(xcsum_ctx *ctx, const struct xcsum_route *route,
 		       struct xcsum_desc *d_desc_out, uint16_t *d_out, uint32_t flags,
 		       uint32_t len_hint, void *stream);
 
+/* ---- receive path: xudp_nic_recv_channel's per-frame work on the GPU ------
+ * Replaces the loop of xudp_nic_recv_channel (group/channel.c:211-267) for a
+ * batch of received frames (the xdp_desc array dequeued from the RX ring):
+ * packet_parse() (include/packet_parse.h:101-165, with its quirks: h_proto
+ * first byte 0x08 OR second byte 0x00 parses as IPv4; IPv6 UDP is taken at
+ * iph6 + 1 even after extension headers), the stats-request test
+ * (channel.c:182-190) and the fields of xudp_fill_msg() (channel.c:69-128),
+ * one record per descriptor.  With XCSUM_F_VERIFY the UDP checksum is also
+ * verified under RFC 768/2460 with the length from the UDP header (received
+ * frames may carry Ethernet padding); with XCSUM_F_IPHDR also the IPv4 header
+ * checksum over 4*ihl bytes.  The reference verifies nothing. */
+enum xcsum_rx_status {
+	XCSUM_RX_OK = 0,        /* deliver (xudp_fill_msg) */
+	XCSUM_RX_PARSE = 1,     /* packet_parse() returned 0: not UDP over IPv4/IPv6,
+				   or truncated (the reference does not skip these,
+				   channel.c:241 tests ret < 0; it is never true) */
+	XCSUM_RX_STATS = 2,     /* iph->saddr == iph->daddr: a stats request the host
+				   answers (channel.c:189); recycle the frame */
+	XCSUM_RX_CSUM = 3,      /* XCSUM_F_VERIFY: checksum invalid, or the UDP length
+				   does not fit the frame */
+};
+
+struct xcsum_rx_msg {
+	uint64_t frame;         /* desc.addr (m->recycle1 / m->frame, channel.c:113-123) */
+	uint64_t body;          /* UMEM offset of the UDP payload, udp + 1 (m->p) */
+	uint32_t size;          /* ntohs(udp->len) - 8 (m->size; wraps below 8 as the
+				   reference's int does) */
+	uint8_t status;         /* enum xcsum_rx_status */
+	uint8_t family;         /* 4 or 6; 0 when the parse failed */
+	uint16_t l4_off;        /* UDP header offset in the frame */
+	uint16_t sport_be;      /* peer port, udp->source (network order) */
+	uint16_t dport_be;      /* local port, udp->dest */
+	uint32_t reserved;
+	uint8_t saddr[16];      /* peer address (IPv4: first 4 bytes) */
+	uint8_t daddr[16];      /* local address */
+};
+
+/* d_msgs[i] describes d_desc[i] (64 bytes each; fields past `status` are 0
+ * when the parse failed).  d_count (may be NULL) receives the number of
+ * XCSUM_RX_OK records (uint32, device memory).  flags: XCSUM_F_VERIFY,
+ * XCSUM_F_IPHDR.  len_hint = typical frame length (kernel geometry only).
+ * Asynchronous on `stream`. */
+int xcsum_rx_device(xcsum_ctx *ctx, const uint8_t *d_umem, const struct xcsum_desc *d_desc,
+		    uint32_t n, struct xcsum_rx_msg *d_msgs, uint32_t *d_count, uint32_t flags,
+		    uint32_t len_hint, void *stream);
+
 /* ---- host-resident batch (frames in the AF_XDP UMEM) ----------------------
  * Same semantics with host pointers.  Synchronous.  Frames are moved with
  * chunked, double-buffered hipMemcpyAsync (pinned when the UMEM range is

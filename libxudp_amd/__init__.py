@@ -59,6 +59,13 @@ DESC_DTYPE = np.dtype([("addr", "<u8"), ("len", "<u4"), ("options", "<u4")])
 # struct xcsum_msg (device frame build)
 MSG_DTYPE = np.dtype([("src", "<u8"), ("len", "<u4"), ("slot", "<u4")])
 
+# struct xcsum_rx_msg (64 bytes) and enum xcsum_rx_status
+RX_MSG_DTYPE = np.dtype([("frame", "<u8"), ("body", "<u8"), ("size", "<u4"), ("status", "u1"),
+                         ("family", "u1"), ("l4_off", "<u2"), ("sport_be", "<u2"),
+                         ("dport_be", "<u2"), ("reserved", "<u4"), ("saddr", "u1", 16),
+                         ("daddr", "u1", 16)])
+RX_OK, RX_PARSE, RX_STATS, RX_CSUM = 0, 1, 2, 3
+
 HDR4 = 42  # eth 14 + ip 20 + udp 8
 HDR6 = 62  # eth 14 + ip6 40 + udp 8
 
@@ -88,6 +95,9 @@ _SIGS = {
                                           ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p,
                                           ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32,
                                           ctypes.c_void_p]),
+    "xcsum_rx_device": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                       ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p,
+                                       ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p]),
     "xcsum_batch_host": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                         ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint32,
                                         ctypes.c_uint32]),
@@ -249,6 +259,13 @@ class Engine:
                                         _ptr(d_msgs), n, _ptr(d_umem), frame_size, data_off,
                                         _ptr(d_desc_out), _ptr(d_out), flags, len_hint,
                                         _ptr(stream)), "xcsum_build_device")
+
+    def rx_device(self, d_umem, d_desc, n, d_msgs, d_count=None, flags=0, len_hint=0,
+                  stream=None):
+        """Device-side receive batch: parse + fill_msg (+ verify) per frame."""
+        _check(lib().xcsum_rx_device(self._ctx, _ptr(d_umem), _ptr(d_desc), n, _ptr(d_msgs),
+                                     _ptr(d_count), flags, len_hint, _ptr(stream)),
+               "xcsum_rx_device")
 
     def batch_host(self, umem, desc, out, mode, flags=0):
         _check(lib().xcsum_batch_host(self._ctx, _ptr(umem), _ptr(desc), len(desc), _ptr(out),

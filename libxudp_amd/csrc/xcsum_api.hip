@@ -228,6 +228,30 @@ extern "C" int xcsum_batch_device(xcsum_ctx *c, uint8_t *d_umem, const struct xc
 	return 0;
 }
 
+extern "C" int xcsum_rx_device(xcsum_ctx *c, const uint8_t *d_umem, const struct xcsum_desc *d_desc,
+			       uint32_t n, struct xcsum_rx_msg *d_msgs, uint32_t *d_count,
+			       uint32_t flags, uint32_t len_hint, void *stream)
+{
+	if (!c)
+		return -XCSUM_ERR_INVAL;
+	if (n && (!d_umem || !d_desc || !d_msgs))
+		return -XCSUM_ERR_INVAL;
+	HIPCHK(hipSetDevice(c->device));
+	if (d_count)
+		HIPCHK(hipMemsetAsync(d_count, 0, sizeof(uint32_t), (hipStream_t)stream));
+	if (n == 0)
+		return 0;
+	RxArgs a;
+	a.umem = d_umem;
+	a.desc = d_desc;
+	a.n = n;
+	a.flags = flags & (XCSUM_F_VERIFY | XCSUM_F_IPHDR);
+	a.msgs = d_msgs;
+	a.count = d_count;
+	HIPCHK(launch_rx(a, len_hint, c->cus, (hipStream_t)stream));
+	return 0;
+}
+
 /* The 64-byte header template of a batch: every header byte that does not
  * depend on the frame (packet.c:141-150 eth_build, :68-84 iph_build,
  * :92-103 iph_build6, :119-126 udp_build), length and check fields 0.  Plain

@@ -77,6 +77,17 @@ struct BuildArgs {
 
 hipError_t launch_build(const BuildArgs &a, uint32_t len_hint, int cus, hipStream_t s);
 
+/* Receive-path kernel arguments (xcsum_rx.hip). */
+struct RxArgs {
+	const uint8_t *umem;
+	const struct xcsum_desc *desc;
+	uint32_t n, flags;
+	struct xcsum_rx_msg *msgs;
+	uint32_t *count;               /* may be null */
+};
+
+hipError_t launch_rx(const RxArgs &a, uint32_t len_hint, int cus, hipStream_t s);
+
 /* Kernel geometry: G lanes cooperate on one frame, each segment keeps U frames
  * in flight, and each lane preloads K 16-byte chunks per frame. */
 struct Geometry {

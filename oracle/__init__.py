@@ -51,6 +51,12 @@ def port():
         L.orc_batch_timed.restype = ctypes.c_double
         L.orc_batch_timed.argtypes = [u8p, u8p, ctypes.c_uint32, u8p, ctypes.c_int,
                                       ctypes.c_uint32, ctypes.c_int, ctypes.c_int]
+        L.orc_packet_parse.restype = ctypes.c_int
+        L.orc_packet_parse.argtypes = [u8p, ctypes.c_uint32, ctypes.POINTER(ctypes.c_int),
+                                       ctypes.POINTER(ctypes.c_uint32),
+                                       ctypes.POINTER(ctypes.c_uint32)]
+        L.orc_rx_batch.restype = None
+        L.orc_rx_batch.argtypes = [u8p, u8p, ctypes.c_uint32, ctypes.c_uint32, u8p]
         _port = L
     return _port
 
@@ -77,6 +83,10 @@ def ref():
         L.ref_packet_udp_payload.argtypes = [u8p, u8p, ctypes.c_int, ctypes.c_int, u8p, u8p,
                                              u8p, ctypes.c_uint16, u8p, ctypes.c_uint16,
                                              ctypes.POINTER(ctypes.c_int64)]
+        L.ref_packet_parse.restype = ctypes.c_int
+        L.ref_packet_parse.argtypes = [u8p, ctypes.c_uint32, ctypes.POINTER(ctypes.c_int),
+                                       ctypes.POINTER(ctypes.c_uint32),
+                                       ctypes.POINTER(ctypes.c_uint32)]
         L.ref_batch.restype = None
         L.ref_batch.argtypes = [u8p, u8p, ctypes.c_uint32, u8p, ctypes.c_int]
         L.ref_batch_timed.restype = ctypes.c_double
@@ -134,3 +144,33 @@ def build_frame(payload, family, smac, dmac, saddr, sport, daddr, dport, v4_rfc=
     n = port().orc_build_frame(_p(buf), _p(pl), len(payload), family, _p(dm), _p(sm), _p(sa),
                                be(sport), _p(da), be(dport), int(bool(v4_rfc)))
     return buf[:n].copy()
+
+
+def _parse(fn, frame):
+    buf = np.ascontiguousarray(np.frombuffer(bytes(frame), dtype=np.uint8))
+    fam, l3, l4 = ctypes.c_int(0), ctypes.c_uint32(0), ctypes.c_uint32(0)
+    r = fn(_p(buf), len(buf), ctypes.byref(fam), ctypes.byref(l3), ctypes.byref(l4))
+    return (int(r), fam.value, l3.value, l4.value) if r == 1 else (int(r), 0, 0, 0)
+
+
+def packet_parse(frame):
+    """The restatement of include/packet_parse.h:101-165: (ret, family, l3, l4)."""
+    return _parse(port().orc_packet_parse, frame)
+
+
+def ref_packet_parse(frame):
+    """The reference's own packet_parse(), compiled from include/packet_parse.h."""
+    return _parse(ref().ref_packet_parse, frame)
+
+
+RX_MSG_DTYPE = np.dtype([("frame", "<u8"), ("body", "<u8"), ("size", "<u4"), ("status", "u1"),
+                         ("family", "u1"), ("l4_off", "<u2"), ("sport_be", "<u2"),
+                         ("dport_be", "<u2"), ("reserved", "<u4"), ("saddr", "u1", 16),
+                         ("daddr", "u1", 16)])
+
+
+def rx_batch(umem, desc, flags=0):
+    """Receive records (struct xcsum_rx_msg) the oracle expects for a batch."""
+    out = np.zeros(len(desc), dtype=RX_MSG_DTYPE)
+    port().orc_rx_batch(_p(umem), _p(desc), len(desc), flags, _p(out))
+    return out

@@ -189,3 +189,23 @@ double ref_batch_timed(uint8_t *umem, const struct ref_desc *desc, uint32_t n, u
 	clock_gettime(CLOCK_MONOTONIC, &t1);
 	return (t1.tv_sec - t0.tv_sec) + 1e-9 * (t1.tv_nsec - t0.tv_nsec);
 }
+
+/* include/packet_parse.h:101-165 (packet_parse, parse_ipv6 :33-99), the
+ * reference's receive-side parser, compiled where it lies.  Returns its
+ * result and the L3/L4 offsets of the headers it found. */
+#include <linux/ipv6.h>
+#include "packet_parse.h"
+
+int ref_packet_parse(const uint8_t *pkt, uint32_t len, int *family, uint32_t *l3, uint32_t *l4)
+{
+	struct pkthdrs h;
+	int r;
+	memset(&h, 0, sizeof(h));
+	r = packet_parse(&h, (void *)pkt, (void *)(pkt + len));
+	if (r == 1) {
+		*family = h.family == AF_INET ? 4 : 6;
+		*l3 = (uint32_t)((const uint8_t *)(h.family == AF_INET ? (void *)h.iph : (void *)h.iph6) - pkt);
+		*l4 = (uint32_t)((const uint8_t *)h.udp - pkt);
+	}
+	return r;
+}

@@ -426,3 +426,171 @@ u32 orc_build_frame(u8 *eth, const u8 *payload, u32 psize, int family,
 	}
 	return psize + (family == 4 ? 42 : 62);
 }
+
+/* ---- receive path: xudp_nic_recv_channel's per-frame work ----------------
+ * (group/channel.c:211-267): packet_parse() (include/packet_parse.h:101-165,
+ * parse_ipv6 :33-99), the stats-request test (channel.c:182-190) and
+ * xudp_fill_msg() (channel.c:69-128), plus an RFC 768/2460 verify driven by
+ * the UDP header's own length (received frames may carry Ethernet padding),
+ * which the reference does not do.  Restated with the reference's quirks:
+ *   - IPv4 is taken when h_proto's first byte is 0x08 OR its second is 0x00
+ *     (packet_parse.h:117), so ARP (0x0806) and VLAN (0x8100) frames parse
+ *     as IPv4 when their bytes allow;
+ *   - ihl != 5 places the UDP header at iph + 4*ihl, ihl < 5 included (:127);
+ *   - parse_ipv6 walks up to 8 extension headers but returns iph6 + 1 for
+ *     UDP wherever it is found (:62);
+ *   - the stats test compares the iphdr saddr/daddr fields (offsets 12, 16
+ *     of the IP header) for IPv6 frames too (union, channel.c:241).
+ * The reference's own `ret < 0` test (channel.c:241) never fires, so its
+ * unparseable frames go on with stale headers; here they are reported
+ * (ORC_RX_PARSE) instead. */
+enum { ORC_RX_OK = 0, ORC_RX_PARSE = 1, ORC_RX_STATS = 2, ORC_RX_CSUM = 3 };
+
+struct orc_rx_msg {
+	u64 frame, body;
+	u32 size;
+	u8 status, family;
+	u16 l4_off, sport_be, dport_be;
+	u32 reserved;
+	u8 saddr[16], daddr[16];
+};
+
+/* packet_parse(): 1 and the L3/L4 offsets, or 0 */
+int orc_packet_parse(const u8 *pkt, u32 len, int *family, u32 *l3, u32 *l4)
+{
+	const u8 *p = pkt + 12;
+	if (len < 14)
+		return 0;                                   /* access_obj_ok(eth) */
+	if (p[0] == 0x08 || p[1] == 0x00) {
+		u32 ihl, udp;
+		if (len < 14 + 20)
+			return 0;
+		if (pkt[14 + 9] != 17)
+			return 0;
+		ihl = pkt[14] & 0xf;
+		udp = 14 + (ihl == 5 ? 20 : (ihl << 2));
+		if (udp + 8 > len)
+			return 0;
+		*family = 4;
+		*l3 = 14;
+		*l4 = udp;
+		return 1;
+	}
+	if (p[0] == 0x86 && p[1] == 0xDD) {
+		u32 pos = 14 + 40, i, ol;
+		u8 nexthdr;
+		if (len < 14 + 40)
+			return 0;
+		nexthdr = pkt[14 + 6];
+		for (i = 0; i < 8; i++) {
+			if (pos + 2 > len)
+				return 0;
+			switch (nexthdr) {
+			case 132: case 58: case 59: case 6: case 41:
+				return 0;
+			case 17:
+				if (14 + 40 + 8 > len)
+					return 0;
+				*family = 6;
+				*l3 = 14;
+				*l4 = 14 + 40;          /* iph6 + 1, packet_parse.h:62 */
+				return 1;
+			case 51:
+				ol = ((u32)pkt[pos + 1] + 2) << 2;
+				break;
+			case 44:
+				ol = 8;
+				break;
+			case 0: case 43: case 47: case 50: case 60: case 135:
+				ol = ((u32)pkt[pos + 1] + 1) << 3;
+				break;
+			default:
+				return 0;
+			}
+			nexthdr = pkt[pos];
+			pos += ol;
+		}
+		return 0;
+	}
+	return 0;
+}
+
+/* one's-complement sum check of a received UDP datagram at pkt + l4 with the
+ * pseudo header of the parsed family: 1 = valid */
+static int orc_rx_udp_ok(const u8 *pkt, u32 len, int family, u32 l3, u32 l4)
+{
+	u32 ulen = ((u32)pkt[l4 + 4] << 8) | pkt[l4 + 5], sum;
+	if (ulen < 8 || l4 + ulen > len)
+		return 0;
+	if (orc_load16(pkt + l4 + 6) == 0)
+		return family == 4;                 /* IPv4: no checksum; IPv6: invalid */
+	sum = orc_do_csum(pkt + l4, ulen);
+	if (family == 6) {
+		sum = orc_udp6_hdr_csum(sum, pkt + l3 + 8, pkt + l3 + 24, ulen);
+	} else {
+		sum = orc_sum32(sum, orc_load32(pkt + l3 + 12));
+		sum = orc_sum32(sum, orc_load32(pkt + l3 + 16));
+		sum = orc_sum32(sum, orc_bswap32(ulen));
+		sum = orc_sum32(sum, orc_bswap32(ORC_IPPROTO_UDP));
+	}
+	return orc_csum_fold(sum) == 0;
+}
+
+/* RFC 1071 over the 4*ihl-byte IPv4 header, check included: 1 = valid */
+static int orc_rx_iphdr_ok(const u8 *iph)
+{
+	u32 n = (u32)(iph[0] & 0xf) << 2, i, sum = 0;
+	if (n < 20)
+		return 0;
+	for (i = 0; i < n; i += 2)
+		sum += ((u32)iph[i] << 8) | iph[i + 1];
+	while (sum >> 16)
+		sum = (sum & 0xffff) + (sum >> 16);
+	return sum == 0xffff;
+}
+
+void orc_rx_one(const u8 *pkt, u32 len, u64 addr, u32 flags, struct orc_rx_msg *m)
+{
+	int family = 0;
+	u32 l3 = 0, l4 = 0;
+	memset(m, 0, sizeof(*m));
+	m->frame = addr;
+	if (!orc_packet_parse(pkt, len, &family, &l3, &l4)) {
+		m->status = ORC_RX_PARSE;
+		return;
+	}
+	m->family = (u8)family;
+	m->l4_off = (u16)l4;
+	/* xudp_fill_msg(): body = udp + 1, size = ntohs(udp->len) - 8 */
+	m->body = addr + l4 + 8;
+	m->size = (u32)((((u32)pkt[l4 + 4] << 8) | pkt[l4 + 5]) - 8);
+	memcpy(&m->sport_be, pkt + l4, 2);
+	memcpy(&m->dport_be, pkt + l4 + 2, 2);
+	if (family == 4) {
+		memcpy(m->saddr, pkt + l3 + 12, 4);
+		memcpy(m->daddr, pkt + l3 + 16, 4);
+	} else {
+		memcpy(m->saddr, pkt + l3 + 8, 16);
+		memcpy(m->daddr, pkt + l3 + 24, 16);
+	}
+	/* xudp_stats_req_check(): iph->saddr == iph->daddr (channel.c:189) */
+	if (memcmp(pkt + l3 + 12, pkt + l3 + 16, 4) == 0) {
+		m->status = ORC_RX_STATS;
+		return;
+	}
+	if (flags & ORC_FLAG_VERIFY) {
+		/* an IPv4 header shorter than 20 bytes is invalid (RFC 791) */
+		if ((family == 4 && (pkt[l3] & 0xf) < 5) ||
+		    !orc_rx_udp_ok(pkt, len, family, l3, l4) ||
+		    ((flags & ORC_FLAG_IPHDR) && family == 4 && !orc_rx_iphdr_ok(pkt + l3)))
+			m->status = ORC_RX_CSUM;
+	}
+}
+
+void orc_rx_batch(const u8 *umem, const struct orc_desc *desc, u32 n, u32 flags,
+		  struct orc_rx_msg *out)
+{
+	u32 i;
+	for (i = 0; i < n; i++)
+		orc_rx_one(umem + desc[i].addr, desc[i].len, desc[i].addr, flags, out + i);
+}

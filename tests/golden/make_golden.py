@@ -16,6 +16,8 @@ Outputs:
                    expected legacy / rfc / v6 / iphdr values
   build_fixtures.npz -- frames built by xudp_packet_udp_payload() for two
                    fixed routes and many payload sizes (device frame build)
+  rx_fixtures.npz -- received frames with the reference's packet_parse()
+                   results and the expected receive records
   digests.json  -- SHA-256 of the reference's output array for BASELINE.json
                    configs 1-5 over the synthetic generator's frames
                    (libxudp_amd gen_* == reference-built frames, see
@@ -269,10 +271,33 @@ def config_digest(cid, chunk=1 << 18, threads=8):
     return rec
 
 
+def rx_fixtures():
+    """rx_fixtures.npz: received frames (tests/golden/rx_frames.py corpus) at
+    irregular offsets, the reference's own packet_parse() result for each
+    (include/packet_parse.h compiled in place), and the records the oracle
+    restatement expects from xcsum_rx_device for flags 0 / VERIFY /
+    VERIFY|IPHDR."""
+    sys.path.insert(0, OUT)
+    import rx_frames
+    frames, expect = zip(*rx_frames.corpus())
+    umem, offs, lens = rx_frames.layout(frames, np.random.default_rng(3))
+    desc = np.zeros(len(frames), dtype=X.DESC_DTYPE)
+    desc["addr"], desc["len"] = offs, lens
+    refparse = np.array([oracle.ref_packet_parse(f) for f in frames], dtype=np.int64)
+    recs = {f"rec_{name}": oracle.rx_batch(umem, desc, fl).view(np.uint8)
+            for name, fl in (("plain", 0), ("verify", X.F_VERIFY),
+                             ("iphdr", X.F_VERIFY | X.F_IPHDR))}
+    np.savez_compressed(os.path.join(OUT, "rx_fixtures.npz"), umem=umem,
+                        desc=desc.view(np.uint8), expect=np.array(expect),
+                        refparse=refparse, **recs)
+    print(f"rx_fixtures.npz: {len(frames)} frames, {umem.nbytes} bytes")
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--no-digests", action="store_true")
     ap.add_argument("--only-build", action="store_true", help="only build_fixtures.npz")
+    ap.add_argument("--only-rx", action="store_true", help="only rx_fixtures.npz")
     ap.add_argument("--configs", default="1,2,3,4,5")
     args = ap.parse_args()
     if not oracle.have_ref():
@@ -280,8 +305,12 @@ def main():
     if args.only_build:
         build_frame_fixtures()
         return
+    if args.only_rx:
+        rx_fixtures()
+        return
     build_fixtures()
     build_frame_fixtures()
+    rx_fixtures()
     if not args.no_digests:
         path = os.path.join(OUT, "digests.json")
         digests = json.load(open(path)) if os.path.exists(path) else {}

@@ -147,3 +147,22 @@ def test_geometry_list_matches_kernel_source():
         r"g\.G == (\d+) && g\.U == (\d+) && g\.K == (\d+)\) return launch_lds_t", src)]
     assert reg == X.REG_GEOMETRIES
     assert sorted(lds) == sorted(X.LDS_GEOMETRIES)
+
+
+def test_rx_msg_layout_matches_c():
+    """struct xcsum_rx_msg (64 B) == libxudp_amd.RX_MSG_DTYPE, field by field."""
+    names = [n for n in X.RX_MSG_DTYPE.names]
+    src = "#include <stdio.h>\n#include <stddef.h>\n#include \"xcsum.h\"\nint main(void){\n" + \
+        'printf("%zu\\n", sizeof(struct xcsum_rx_msg));\n' + "".join(
+            f'printf("%zu\\n", offsetof(struct xcsum_rx_msg, {n}));\n' for n in names) + \
+        "return 0; }\n"
+    import tempfile
+    with tempfile.TemporaryDirectory() as d:
+        c = os.path.join(d, "r.c")
+        open(c, "w").write(src)
+        subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), c, "-o",
+                        os.path.join(d, "r")], check=True)
+        vals = [int(v) for v in subprocess.run([os.path.join(d, "r")], capture_output=True,
+                                               text=True, check=True).stdout.split()]
+    assert vals[0] == X.RX_MSG_DTYPE.itemsize == 64
+    assert vals[1:] == [X.RX_MSG_DTYPE.fields[n][1] for n in names]

@@ -1,0 +1,128 @@
+"""GPU: xcsum_rx_device (the receive path, csrc/xcsum_rx.hip) through the C ABI
+against the fixture records (tests/golden/rx_fixtures.npz: the reference's
+packet_parse() + the oracle's fill/verify), against the oracle on generated
+batches, and as a size-independent round trip at BASELINE sizes: frames the
+TX kernel checksummed in place all verify; one flipped bit in each fails."""
+import os
+import sys
+
+import numpy as np
+import pytest
+
+import bench
+import libxudp_amd as X
+import oracle
+
+pytestmark = pytest.mark.gpu
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+sys.path.insert(0, GOLDEN)
+import rx_frames  # noqa: E402
+
+FLAGS = {"plain": 0, "verify": X.F_VERIFY, "iphdr": X.F_VERIFY | X.F_IPHDR}
+
+
+@pytest.fixture(scope="module")
+def rx():
+    z = np.load(os.path.join(GOLDEN, "rx_fixtures.npz"))
+    d = {k: z[k] for k in z.files}
+    d["desc"] = d["desc"].view(X.DESC_DTYPE)
+    return d
+
+
+def run_rx(torch, eng, umem, desc, flags, len_hint=0, geometry=None):
+    dev = torch.device("cuda:0")
+    d_umem = torch.from_numpy(umem).to(dev)
+    d_desc = torch.from_numpy(desc.view(np.uint8)).to(dev)
+    d_msgs = torch.full((max(len(desc), 1) * 64,), 0xA5, dtype=torch.uint8, device=dev)
+    d_count = torch.full((1,), 77, dtype=torch.int32, device=dev)
+    old = os.environ.get("XCSUM_RX_GEOMETRY")
+    if geometry:
+        os.environ["XCSUM_RX_GEOMETRY"] = str(geometry)
+    try:
+        eng.rx_device(d_umem, d_desc, len(desc), d_msgs, d_count, flags, len_hint)
+        torch.cuda.synchronize()
+    finally:
+        if geometry:
+            if old is None:
+                del os.environ["XCSUM_RX_GEOMETRY"]
+            else:
+                os.environ["XCSUM_RX_GEOMETRY"] = old
+    recs = d_msgs.cpu().numpy()[:len(desc) * 64].view(X.RX_MSG_DTYPE)
+    return recs, int(d_count.cpu().item())
+
+
+@pytest.mark.parametrize("geometry", [4, 16, 64])
+@pytest.mark.parametrize("name", sorted(FLAGS))
+def test_rx_matches_fixtures(torch_cuda, engine, rx, name, geometry):
+    recs, count = run_rx(torch_cuda, engine, rx["umem"], rx["desc"], FLAGS[name],
+                         geometry=geometry)
+    exp = rx[f"rec_{name}"].view(X.RX_MSG_DTYPE)
+    bad = np.nonzero(recs.view(np.uint8).reshape(-1, 64) != exp.view(np.uint8).reshape(-1, 64))
+    assert len(bad[0]) == 0, f"records differ: {sorted(set(bad[0].tolist()))[:10]}"
+    assert count == int((exp["status"] == X.RX_OK).sum())
+
+
+def test_rx_generated_vs_oracle(torch_cuda, engine):
+    """6k frames: the corpus under three seeds, at irregular offsets."""
+    frames = []
+    for seed in (1, 2, 3):
+        frames += [f for f, _ in rx_frames.corpus(seed=seed)]
+    rng = np.random.default_rng(5)
+    frames = [frames[i] for i in rng.permutation(len(frames))] * 10
+    umem, offs, lens = rx_frames.layout(frames, rng)
+    desc = np.zeros(len(frames), dtype=X.DESC_DTYPE)
+    desc["addr"], desc["len"] = offs, lens
+    for flags in FLAGS.values():
+        for hint in (0, 100, 1500, 9000):
+            recs, count = run_rx(torch_cuda, engine, umem, desc, flags, hint)
+            exp = oracle.rx_batch(umem, desc, flags)
+            assert np.array_equal(recs.view(np.uint8), exp.view(np.uint8)), (flags, hint)
+            assert count == int((exp["status"] == X.RX_OK).sum())
+
+
+def test_rx_empty_batch(torch_cuda, engine):
+    dev = torch_cuda.device("cuda:0")
+    d = torch_cuda.zeros(64, dtype=torch_cuda.uint8, device=dev)
+    c = torch_cuda.full((1,), 5, dtype=torch_cuda.int32, device=dev)
+    engine.rx_device(d, d, 0, d, c, X.F_VERIFY)
+    torch_cuda.cuda.synchronize()
+    assert int(c.item()) == 0
+    with pytest.raises(X.XcsumError):
+        engine.rx_device(None, None, 3, None)
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("cid", [2, 3, 4])
+def test_rx_round_trip_full_size(torch_cuda, engine, cid):
+    """TX checksums written in place (RFC; IPv4 header too) verify on RX, at
+    the BASELINE config's size; a flipped payload bit fails every frame."""
+    cfg = dict(bench.CONFIGS[cid], id=cid)
+    n = cfg["n"]
+    desc, nbytes = X.gen_layout(n, cfg["family"], cfg["pmin"], cfg["pmax"],
+                                seed=bench.SEED_BASE ^ cid)
+    dev = torch_cuda.device("cuda:0")
+    d_desc = torch_cuda.from_numpy(desc.view(np.uint8)).to(dev)
+    d_umem = torch_cuda.empty(nbytes + 64, dtype=torch_cuda.uint8, device=dev)
+    engine.gen_fill_device(d_umem, d_desc, n, cfg["family"], bench.SEED_BASE ^ cid, 0)
+    mode = X.MODE_V6 if cfg["family"] == 6 else X.MODE_V4_RFC
+    engine.batch_device(d_umem, d_desc, n, None, mode, X.F_INPLACE | X.F_IPHDR)
+    d_msgs = torch_cuda.empty(n * 64, dtype=torch_cuda.uint8, device=dev)
+    d_count = torch_cuda.zeros(1, dtype=torch_cuda.int32, device=dev)
+    engine.rx_device(d_umem, d_desc, n, d_msgs, d_count, X.F_VERIFY | X.F_IPHDR,
+                     int(desc["len"][0]))
+    torch_cuda.cuda.synchronize()
+    recs = d_msgs.cpu().numpy().view(X.RX_MSG_DTYPE)
+    assert int(d_count.item()) == n
+    assert (recs["status"] == X.RX_OK).all()
+    hdr = 42 if cfg["family"] == 4 else 62
+    assert np.array_equal(recs["body"], desc["addr"] + hdr)
+    assert np.array_equal(recs["size"], desc["len"] - hdr)
+    # flip one bit of the last payload byte of every frame
+    last = torch_cuda.from_numpy((desc["addr"] + desc["len"] - 1).astype(np.int64)).to(dev)
+    d_umem[last] ^= 0x10
+    engine.rx_device(d_umem, d_desc, n, d_msgs, d_count, X.F_VERIFY, int(desc["len"][0]))
+    torch_cuda.cuda.synchronize()
+    recs = d_msgs.cpu().numpy().view(X.RX_MSG_DTYPE)
+    assert int(d_count.item()) == 0
+    assert (recs["status"] == X.RX_CSUM).all()
