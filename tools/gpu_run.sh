@@ -8,6 +8,7 @@ mkdir -p gpurun_out
 name="$1"; shift
 tmo="$1"; shift
 log="gpurun_out/${name}.log"
+mkdir -p "$(dirname "$log")"
 echo "=== $name: $*" > "$log"
 start=$(date +%s)
 timeout -k 10 "$tmo" "$@" >> "$log" 2>&1
