@@ -211,7 +211,8 @@ struct xcsum_rx_msg {
  * when the parse failed).  d_count (may be NULL) receives the number of
  * XCSUM_RX_OK records (uint32, device memory).  flags: XCSUM_F_VERIFY,
  * XCSUM_F_IPHDR.  len_hint = typical frame length (kernel geometry only).
- * Asynchronous on `stream`. */
+ * d_umem must be 4-byte aligned (-XCSUM_ERR_INVAL otherwise); frames may sit
+ * at any byte offset in it.  Asynchronous on `stream`. */
 int xcsum_rx_device(xcsum_ctx *ctx, const uint8_t *d_umem, const struct xcsum_desc *d_desc,
 		    uint32_t n, struct xcsum_rx_msg *d_msgs, uint32_t *d_count, uint32_t flags,
 		    uint32_t len_hint, void *stream);

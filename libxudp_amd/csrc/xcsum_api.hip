@@ -236,6 +236,8 @@ extern "C" int xcsum_rx_device(xcsum_ctx *c, const uint8_t *d_umem, const struct
 		return -XCSUM_ERR_INVAL;
 	if (n && (!d_umem || !d_desc || !d_msgs))
 		return -XCSUM_ERR_INVAL;
+	if ((uintptr_t)d_umem & 3u)   /* chunk grid: see xcsum_rx.hip */
+		return -XCSUM_ERR_INVAL;
 	HIPCHK(hipSetDevice(c->device));
 	if (d_count)
 		HIPCHK(hipMemsetAsync(d_count, 0, sizeof(uint32_t), (hipStream_t)stream));

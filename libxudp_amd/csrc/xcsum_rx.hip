@@ -9,16 +9,38 @@
  *   + UDP verify         RFC 768/2460 over the UDP header's own length
  *                        (the reference verifies nothing)
  *
- * G lanes own a frame.  The header parse is a handful of byte loads every
- * lane of the group makes itself (same addresses: one cache line, no
- * cross-lane traffic), so each lane knows every field; lanes 0..3 then store
- * the 64-byte record as four coalesced 16-byte pieces.  The UDP segment is
- * summed in 16-byte chunks on the dword grid of the checksum kernel (chunks
- * laid back from the segment end rounded up to 4 bytes, edge bytes masked
- * before summing), K chunks per lane in flight, G-lane DPP reduction.
- * HBM-bound: the frame bytes once, 16 B descriptor in, 64 B record out.
+ * Design (HBM-bound: frame bytes once, 16-B descriptor in, 64-B record out).
+ * The header decides where the checksum span ends (the UDP length, not the
+ * frame length: received frames may carry Ethernet padding), so loading the
+ * span after parsing would put a dependent HBM round trip on every frame.
+ * Instead the kernel loads the WHOLE frame speculatively from the descriptor
+ * alone -- 16-byte chunks on a dword grid laid back from the frame end
+ * rounded up to 4 bytes, reaching down to the EtherType at eth+12 -- with the
+ * checksum kernel's two-stage software pipeline (frame i+1's chunks and frame
+ * i+2's descriptor in flight while frame i is processed).  When frame i's
+ * chunks land:
+ *   1. its first 6 chunks (96 bytes: every header byte packet_parse reads
+ *      unless IPv6 extension headers follow) are written to a per-frame LDS
+ *      stage; the parse reads every field it may need (frame bytes
+ *      12..61) in one batch of 14 dword reads and cuts the fields out with
+ *      v_alignbyte, so no stage read waits on another;
+ *   2. the span [pseudo-header addresses, udp + ulen) is summed from the
+ *      chunk registers with v_dot4_u32_u8 (exact even/odd byte sums, as in
+ *      xcsum_kernels.hip); only chunks that straddle a span edge are masked,
+ *      and a chunk row is masked only if some lane of the wave needs it;
+ *   3. G-lane DPP reduction, RFC verify, the record (lanes 0..3 store one
+ *      16-byte piece each).
+ * Frames the stage cannot describe (IPv6 extension headers; IPv4 options
+ * under VERIFY, whose pseudo header is not contiguous with the UDP header)
+ * take a wave-uniform slow path that parses from global memory byte by byte
+ * exactly as before; jumbo frames (more than K*G chunks) re-walk their
+ * chunks from global memory.  Results never depend on the path.
+ *
+ * d_umem must be 4-byte aligned: the first chunk may start up to 3 bytes
+ * before a frame whose address is not (it never leaves the frame's dword).
  */
 #include "xcsum_internal.h"
+#include <stdio.h>
 #include <stdlib.h>
 
 namespace xcsum {
@@ -84,6 +106,14 @@ static __device__ __forceinline__ uint32_t be_words(const uint8_t *p, uint32_t n
 		s += be16(p + i);
 	return s;
 }
+
+/* big-endian 16-bit word sum of the 4 bytes of a little-endian dword */
+static __device__ __forceinline__ uint32_t be_words4(uint32_t w)
+{
+	return (dot_even(w, 0u) << 8) + dot_odd(w, 0u);
+}
+
+/* ---- slow path: packet_parse() from global memory ------------------------ */
 
 struct Parsed {
 	uint32_t ok, family, l3, l4;
@@ -166,154 +196,477 @@ static __device__ __forceinline__ u32x4 grid_chunk(const uint8_t *base, uint32_t
 	return v;
 }
 
+/* One frame's record fields, whichever path produced them. */
+struct Rec {
+	uint32_t status, family, l4, ulen, ports;
+};
+
+/* The whole per-frame work from global memory (the general case: IPv6
+ * extension headers, IPv4 options).  Every lane of the wave runs it (the
+ * reductions need them all); only frames flagged slow use the result. */
+template <int G>
+static __device__ Rec rx_slow(const uint8_t *pkt, uint32_t len, uint32_t lane, bool present,
+			      bool verify, bool iphdr)
+{
+	const Parsed ps = present ? packet_parse(pkt, len) : Parsed{0u, 0u, 14u, 0u};
+	Rec r = {XCSUM_RX_PARSE, ps.family, ps.ok ? ps.l4 : 0u, 0u, 0u};
+	if (ps.ok) {
+		const uint8_t *udp = pkt + ps.l4;
+		r.ulen = be16(udp + 4);
+		r.ports = (uint32_t)udp[0] | ((uint32_t)udp[1] << 8) | ((uint32_t)udp[2] << 16) |
+			  ((uint32_t)udp[3] << 24);
+		/* xudp_stats_req_check(): iphdr saddr/daddr fields, both
+		 * families (the union, channel.c:241) */
+		const uint8_t *ip = pkt + ps.l3;
+		const bool stats = ip[12] == ip[16] && ip[13] == ip[17] && ip[14] == ip[18] &&
+				   ip[15] == ip[19];
+		r.status = stats ? XCSUM_RX_STATS : XCSUM_RX_OK;
+	}
+	if (verify && r.status == XCSUM_RX_OK) {
+		const uint8_t *ip = pkt + ps.l3;
+		const uint32_t ihl = ip[0] & 0xfu;
+		const uint32_t ulen = r.ulen;
+		bool good = ulen >= 8 && ps.l4 + ulen <= len && !(ps.family == 4 && ihl < 5);
+		if (good) {
+			const uintptr_t lo = (uintptr_t)(pkt + ps.l4);
+			const uintptr_t hi = lo + ulen;
+			const uintptr_t e4 = (hi + 3) & ~(uintptr_t)3;
+			const uint32_t n = (uint32_t)(e4 - lo + 15) >> 4;
+			const uint8_t *base = (const uint8_t *)(e4 - 16u * n);
+			const uint32_t head = (uint32_t)(lo - (uintptr_t)base);
+			const uint32_t tail = (uint32_t)(e4 - hi);
+			uint32_t E = 0, O = 0;
+			for (uint32_t c = lane; c < n; c += G)   /* one chunk per lane in flight:
+								    rare path, few registers */
+				accum(grid_chunk(base, n, head, tail, c), E, O);
+			uint32_t s = (lo & 1u) ? (O << 8) + E : (E << 8) + O;
+			s = seg_sum<G>(s);
+			/* pseudo header (RFC 768 / RFC 2460 8.1) */
+			if (ps.family == 4)
+				s += be_words(ip + 12, 8);
+			else
+				s += be_words(ip + 8, 32);
+			s += 17u + (ulen >> 16) + (ulen & 0xffffu);
+			const bool nocheck = (pkt[ps.l4 + 6] | pkt[ps.l4 + 7]) == 0;
+			good = nocheck ? ps.family == 4 : fold16(s) == 0xffffu;
+		}
+		if (good && iphdr && ps.family == 4) {
+			/* RFC 1071 over the 4*ihl-byte header, check included */
+			uint32_t h = 0;
+			for (uint32_t j = 2 * lane; j < 4 * ihl; j += 2 * G)
+				h += be16(ip + j);
+			h = seg_sum<G>(h);
+			good = fold16(h) == 0xffffu;
+		}
+		if (!good)
+			r.status = XCSUM_RX_CSUM;
+	}
+	return r;
+}
+
+/* ---- fast path ----------------------------------------------------------- */
+
+constexpr uint32_t STAGE_CHUNKS = 6;   /* 96 bytes from the chunk holding eth+12 */
+
+/* A frame's chunk grid: dword grid laid back from E4 = (eth + len) rounded up
+ * to 4, down to the chunk holding eth + 12.  Chunk c covers frame bytes
+ * [g0 + 16c, g0 + 16c + 16) with g0 = 12 - h, h = offset of eth + 12 in chunk 0
+ * (0..15), so frame byte x sits at stage byte x - 12 + h.  Everything but the
+ * frame pointer is a 32-bit frame-relative offset (registers: two frames are
+ * live in the pipeline). */
+struct RFrame {
+	const uint8_t *eth;
+	uint32_t meta;          /* frame length (clamped to 2^31 - 1) | present << 31 */
+};
+
+typedef uint32_t u32x3 __attribute__((ext_vector_type(3)));
+typedef __attribute__((address_space(1))) const u32x3 gu32x3;
+
+/* xdp_desc {addr, len}: the unused options word is not loaded */
+static __device__ __forceinline__ u32x3 rx_desc(const RxArgs &a, uint32_t q)
+{
+	return *((gu32x3 *)(a.desc + (q < a.n ? q : a.n - 1)));
+}
+
+static __device__ __forceinline__ RFrame rx_resolve(const RxArgs &a, u32x3 d, bool present)
+{
+	RFrame f;
+	f.eth = a.umem + (((uint64_t)d.y << 32) | d.x);
+	f.meta = (d.z > 0x7fffffffu ? 0x7fffffffu : d.z) | (present ? 0x80000000u : 0u);
+	return f;
+}
+
+static __device__ __forceinline__ bool rx_present(const RFrame &f)
+{
+	return (f.meta >> 31) != 0;
+}
+
+static __device__ __forceinline__ uint32_t rx_len(const RFrame &f)
+{
+	return f.meta & 0x7fffffffu;
+}
+
+/* chunk count and h (registers are scarce: recomputed where needed) */
+static __device__ __forceinline__ uint32_t rx_nchunks(const RFrame &f)
+{
+	const uint32_t len = rx_len(f);
+	/* E4 - (eth + 12), with E4 = (eth + len + 3) & ~3 */
+	const uint32_t span = (((uint32_t)(uintptr_t)f.eth + len + 3u) & ~3u) -
+			      ((uint32_t)(uintptr_t)f.eth + 12u);
+	return (rx_present(f) && len >= 14) ? (span + 15u) >> 4 : 0u;
+}
+
+static __device__ __forceinline__ uint32_t rx_h(const RFrame &f, uint32_t nchunks)
+{
+	const uint32_t len = rx_len(f);
+	const uint32_t span = (((uint32_t)(uintptr_t)f.eth + len + 3u) & ~3u) -
+			      ((uint32_t)(uintptr_t)f.eth + 12u);
+	return nchunks ? 16u * nchunks - span : 0u;
+}
+
+/* frame-relative offset of chunk c's first byte */
+static __device__ __forceinline__ int rx_chunk_off(uint32_t h, uint32_t c)
+{
+	return 12 - (int)h + 16 * (int)c;
+}
+
+__device__ u32x4 g_rx_zero[4];
+
 template <int G, int K>
+static __device__ __forceinline__ void rx_issue(const RxArgs &a, const RFrame &f, uint32_t lane,
+						u32x4 (&v)[K])
+{
+	const uint8_t *zero = (const uint8_t *)g_rx_zero;
+	const uint32_t nc = rx_nchunks(f);
+	const uint32_t h = rx_h(f, nc);
+	/* all chunks under VERIFY, else only the header stage */
+	const uint32_t nl = (a.flags & XCSUM_F_VERIFY) || nc < STAGE_CHUNKS ? nc : STAGE_CHUNKS;
+#pragma unroll
+	for (int k = 0; k < K; k++) {
+		const uint32_t c = lane + k * G;
+		v[k] = __builtin_nontemporal_load(
+			(gu32x4 *)(c < nl ? f.eth + rx_chunk_off(h, c) : zero));
+	}
+}
+
+/* keep the bytes of chunk cb..cb+15 whose address is in [lo, hi) */
+static __device__ __forceinline__ uint64_t low_bytes(int n)
+{
+	/* bytes [0, n) of a qword set, n clamped to [0, 8] */
+	return n >= 8 ? ~0ull : (n <= 0 ? 0ull : ~0ull >> (64 - 8 * n));
+}
+
+static __device__ __forceinline__ u32x4 keep_span(u32x4 v, int a, int b)
+{
+	/* a = lo - cb, b = hi - cb */
+	const int ac = a < 0 ? 0 : (a > 16 ? 16 : (int)a);
+	const int bc = b < 0 ? 0 : (b > 16 ? 16 : (int)b);
+	const uint64_t m0 = low_bytes(bc) & ~low_bytes(ac);
+	const uint64_t m1 = low_bytes(bc - 8) & ~low_bytes(ac - 8);
+	v.x &= (uint32_t)m0;
+	v.y &= (uint32_t)(m0 >> 32);
+	v.z &= (uint32_t)m1;
+	v.w &= (uint32_t)(m1 >> 32);
+	return v;
+}
+
+/* Everything for frame p once its chunks v[] have landed: stage, parse,
+ * verify, record.  Group-uniform; every lane of the wave must call it. */
+template <int G, int K>
+static __device__ __forceinline__ void rx_frame(const RxArgs &a, uint32_t *st, const RFrame &fc,
+						const u32x4 (&vc)[K], uint32_t p, uint32_t lane,
+						bool verify, bool iphdr, uint32_t &delivered)
+{
+	/* 1. header stage */
+#pragma unroll
+	for (int k = 0; k < K; k++) {
+		const uint32_t c = lane + k * G;
+		if (k * G < (int)STAGE_CHUNKS && c < STAGE_CHUNKS)
+			*((u32x4 *)(st + 4 * c)) = vc[k];
+	}
+	__builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+	__builtin_amdgcn_wave_barrier();
+	__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+
+	/* 2. packet_parse() from the stage (frame byte x at x - 12 + h) */
+	const uint32_t len = rx_len(fc);
+	const uint32_t nchunks = rx_nchunks(fc);
+	const uint32_t fh = rx_h(fc, nchunks);
+	/* Every header field the fast path can use -- frame bytes 12..61 -- in
+	 * ONE batch of stage reads (14 dwords, no read waits on another): the
+	 * fields at x = 0 mod 4 come from dword pairs at a fixed shift, those
+	 * at x = 2 mod 4 at the shift + 2 (one select of the pair). */
+	const uint32_t s0 = fh & 3u;                    /* frame byte 12 = stage byte fh */
+	const uint32_t *dw = st + (fh >> 2);
+	uint32_t d[14];
+#pragma unroll
+	for (int i = 0; i < 14; i++)
+		d[i] = dw[i];
+	auto f0 = [&](int x) {                          /* x = 0 mod 4 */
+		const int i = (x - 12) >> 2;
+		return __builtin_amdgcn_alignbyte(d[i + 1], d[i], s0);
+	};
+	const bool wrap = s0 >= 2u;
+	auto f2 = [&](int x) {                          /* x = 2 mod 4 */
+		const int m = (x - 14) >> 2;
+		const uint32_t lo_ = wrap ? d[m + 1] : d[m];
+		const uint32_t hi_ = wrap ? d[m + 2] : d[m + 1];
+		return __builtin_amdgcn_alignbyte(hi_, lo_, (s0 + 2u) & 3u);
+	};
+	const uint32_t w12 = f0(12);                    /* h_proto, ver/ihl, tos */
+	const uint32_t w20 = f0(20);                    /* v4: proto at 23; v6: nexthdr at 20 */
+	const uint32_t w26 = f2(26), w30 = f2(30);      /* iph saddr / daddr fields */
+
+	/* packet_parse(), branch-free for the common cases */
+	const uint32_t p0 = w12 & 0xffu, p1 = (w12 >> 8) & 0xffu;
+	const uint32_t ihl = (w12 >> 16) & 0xfu;
+	const bool present = rx_present(fc);
+	const bool eth_ok = present && len >= 14;
+	const bool is4 = eth_ok && (p0 == 0x08 || p1 == 0x00);
+	const uint32_t l4v4 = 14u + (ihl == 5 ? 20u : (ihl << 2));
+	const bool ok4 = is4 && len >= 34 && (w20 >> 24) == 17 && l4v4 + 8 <= len;
+	const bool is6 = eth_ok && !is4 && p0 == 0x86 && p1 == 0xDD && len >= 54;
+	const bool ok6 = is6 && (w20 & 0xffu) == 17 && len >= 62;  /* pos+2, 14+40+8 <= len */
+	/* IPv4 options (UDP header outside the batch) and IPv6 extension
+	 * headers (walk them) go the general way */
+	const bool slow = (ok4 && ihl != 5) || (is6 && (w20 & 0xffu) != 17);
+	const bool ok = (ok4 && ihl == 5) || ok6;
+	const uint32_t family = ok ? (ok4 ? 4u : 6u) : 0u;
+	const uint32_t l4 = ok ? (ok4 ? 34u : 54u) : 0u;
+	/* selects only: every branch here would cost an exec-mask round trip */
+	const uint32_t wck = ok ? (ok4 ? f2(38) : f2(58)) : 0u;   /* len, check */
+	Rec r;
+	r.family = family;
+	r.l4 = l4;
+	r.ports = ok ? (ok4 ? f2(34) : f2(54)) : 0u;
+	r.ulen = ((wck & 0xffu) << 8) | ((wck >> 8) & 0xffu);
+	r.status = !ok ? XCSUM_RX_PARSE : (w26 == w30 ? XCSUM_RX_STATS : XCSUM_RX_OK);
+	/* record addresses: IPv4 iph + 12 / + 16, IPv6 iph6 + 8 / + 24 */
+	u32x4 saddr = ok4 ? u32x4{w26, 0u, 0u, 0u} : u32x4{f2(22), w26, w30, f2(34)};
+	u32x4 daddr = ok4 ? u32x4{w30, 0u, 0u, 0u} : u32x4{f2(38), f2(42), f2(46), f2(50)};
+	/* IPv4 header words (iphdr verify): bytes 14..33 */
+	const uint32_t hsum = be_words4(f2(14)) + be_words4(f2(18)) + be_words4(f2(22)) +
+			      be_words4(w26) + be_words4(w30);
+
+	/* 3. verify: sum [addresses, udp + ulen) from the chunk registers */
+	const bool want = verify && r.status == XCSUM_RX_OK && !slow;
+	bool good = want && r.ulen >= 8 && l4 + r.ulen <= len && !(family == 4 && ihl < 5);
+	const int lo = family == 4 ? 26 : 22;            /* frame-relative span */
+	const int hi = (int)(l4 + r.ulen);
+	if (__builtin_amdgcn_ballot_w64(want)) {
+		uint32_t E = 0, O = 0;
+		if (__builtin_amdgcn_ballot_w64(good && nchunks > K * G)) {
+			for (uint32_t c = lane; c < nchunks; c += G) {
+				const int cb = rx_chunk_off(fh, c);
+				u32x4 v = __builtin_nontemporal_load((gu32x4 *)(fc.eth + cb));
+				if (cb < lo || cb + 16 > hi)
+					v = keep_span(v, lo - cb, hi - cb);
+				accum(v, E, O);
+			}
+		} else {
+#pragma unroll
+			for (int k = 0; k < K; k++) {
+				const int cb = rx_chunk_off(fh, lane + k * G);
+				const bool edge = good && (cb < lo || cb + 16 > hi);
+				u32x4 v = vc[k];
+				if (__builtin_amdgcn_ballot_w64(edge))
+					v = edge ? keep_span(v, lo - cb, hi - cb) : v;
+				accum(v, E, O);
+			}
+		}
+		uint32_t s = ((uintptr_t)fc.eth & 1u) ? (O << 8) + E : (E << 8) + O;
+		s = seg_sum<G>(s);
+		if (good) {
+			s += 17u + r.ulen;
+			good = (wck >> 16) == 0 ? family == 4 : fold16(s) == 0xffffu;
+		}
+		/* RFC 1071 over the 20-byte IPv4 header (ihl == 5 here) */
+		if (iphdr && family == 4)
+			good = good && fold16(hsum) == 0xffffu;
+		if (want && !good)
+			r.status = XCSUM_RX_CSUM;
+	}
+
+	/* 4. general case */
+	if (__builtin_amdgcn_ballot_w64(slow)) {
+		const Rec rs = rx_slow<G>(fc.eth, len, lane, slow, verify, iphdr);
+		if (slow) {
+			r = rs;
+			/* addresses from global memory, iph + 12 / iph6 + 8 */
+			u32x4 ad[2] = {{0u, 0u, 0u, 0u}, {0u, 0u, 0u, 0u}};
+			if (r.status != XCSUM_RX_PARSE) {
+				const uint32_t nb = r.family == 4 ? 4 : 16;
+				for (uint32_t t = 0; t < 2; t++)
+					for (uint32_t q = 0; q < nb; q++)
+						ad[t][q >> 2] |= (uint32_t)fc.eth[(r.family == 4 ? 26u : 22u) +
+										 t * nb + q]
+								 << (8 * (q & 3));
+			}
+			saddr = ad[0];
+			daddr = ad[1];
+		}
+	}
+
+	/* 5. the record: four 16-byte pieces, piece j stored by lane j % G;
+	 * every piece is built with selects (no per-lane branches) */
+	const bool pok = r.status != XCSUM_RX_PARSE;
+	const uint64_t addr = (uint64_t)(fc.eth - a.umem);
+	const uint64_t body = pok ? addr + r.l4 + 8 : 0;
+	const u32x4 w0 = {(uint32_t)addr, (uint32_t)(addr >> 32), (uint32_t)body,
+			  (uint32_t)(body >> 32)};
+	const u32x4 w1 = {pok ? r.ulen - 8u : 0u,
+			  r.status | (r.family << 8) | ((pok ? r.l4 : 0u) << 16), r.ports, 0u};
+	const u32x4 zero4 = {0u, 0u, 0u, 0u};
+	if (!pok) {
+		saddr = zero4;
+		daddr = zero4;
+	}
+#pragma unroll
+	for (int i = 0; i < (G < 4 ? 4 / G : 1); i++) {
+		const uint32_t j = lane + i * G;       /* piece */
+		const u32x4 w = j == 0 ? w0 : (j == 1 ? w1 : (j == 2 ? saddr : daddr));
+		if (present && j < 4)
+			*((u32x4 *)(a.msgs + p) + j) = w;
+	}
+	if (lane == 0 && present && r.status == XCSUM_RX_OK)
+		delivered++;
+
+	/* the stage is rewritten next iteration: reads first */
+	__builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+	__builtin_amdgcn_wave_barrier();
+	__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+/*
+ * Persistent grid, G lanes per frame.  Two-stage software pipeline written
+ * as a ping-pong over two register sets (A, B): while frame p's chunks are
+ * processed, frame p + nseg's chunks and the descriptor after it are in
+ * flight.  No copy from the "next" set into the "current" one: such a copy
+ * needs the in-flight loads to have landed and would drain the pipeline
+ * every iteration (vmcnt(0) at the loop latch, seen in the ISA).
+ */
+template <int G, int K, int U>
 __global__ void __launch_bounds__(256) rx_kernel(RxArgs a)
 {
+	/* per-frame header stage: STAGE_CHUNKS chunks + one dword of slack */
+	constexpr uint32_t SW = STAGE_CHUNKS * 4 + 4;   /* dwords per group */
+	__shared__ __attribute__((aligned(16))) uint32_t stage[(256 / G) * SW];
 	const uint32_t lane = threadIdx.x & (G - 1);
-	const uint32_t seg = (blockIdx.x * 256u + threadIdx.x) / G;
+	const uint32_t grp = threadIdx.x / G;
+	uint32_t *st = stage + grp * SW;
+	uint32_t seg = (blockIdx.x * 256u + threadIdx.x) / G;
 	const uint32_t nseg = gridDim.x * (256u / G);
+	if (G == 64)
+		seg = __builtin_amdgcn_readfirstlane(seg);
 	const bool verify = (a.flags & XCSUM_F_VERIFY) != 0;
 	const bool iphdr = (a.flags & XCSUM_F_IPHDR) != 0;
 	uint32_t delivered = 0;
+	if (lane == 0)
+		st[SW - 1] = 0u;
+	auto desc = [&](uint32_t q) { return rx_desc(a, q); };
 
-	for (uint32_t p = seg; p < a.n; p += nseg) {
-		const u32x4 d = *((gu32x4 *)(a.desc + p));
-		const uint64_t addr = ((uint64_t)d.y << 32) | d.x;
-		const uint32_t len = d.z;
-		const uint8_t *pkt = a.umem + addr;
-		const Parsed ps = packet_parse(pkt, len);
-
-		uint32_t status = XCSUM_RX_PARSE;
-		uint32_t ulen = 0, sport = 0, dport = 0;
-		if (ps.ok) {
-			const uint8_t *udp = pkt + ps.l4;
-			ulen = be16(udp + 4);
-			sport = (uint32_t)udp[0] | ((uint32_t)udp[1] << 8);
-			dport = (uint32_t)udp[2] | ((uint32_t)udp[3] << 8);
-			/* xudp_stats_req_check(): iphdr saddr/daddr fields, both
-			 * families (the union, channel.c:241) */
-			const uint8_t *ip = pkt + ps.l3;
-			const bool stats = ip[12] == ip[16] && ip[13] == ip[17] &&
-					   ip[14] == ip[18] && ip[15] == ip[19];
-			status = stats ? XCSUM_RX_STATS : XCSUM_RX_OK;
-		}
-
-		/* ---- verify (group-uniform control flow: the reductions
-		 * below need every lane of the group) ---- */
-		if (verify && status == XCSUM_RX_OK) {
-			const uint8_t *ip = pkt + ps.l3;
-			const uint32_t ihl = ip[0] & 0xfu;
-			bool good = ulen >= 8 && ps.l4 + ulen <= len && !(ps.family == 4 && ihl < 5);
-			if (good) {
-				const uintptr_t lo = (uintptr_t)(pkt + ps.l4);
-				const uintptr_t hi = lo + ulen;
-				const uintptr_t e4 = (hi + 3) & ~(uintptr_t)3;
-				const uint32_t n = (uint32_t)(e4 - lo + 15) >> 4;
-				const uint8_t *base = (const uint8_t *)(e4 - 16u * n);
-				const uint32_t head = (uint32_t)(lo - (uintptr_t)base);
-				const uint32_t tail = (uint32_t)(e4 - hi);
-				uint32_t E = 0, O = 0;
-				for (uint32_t c0 = lane; c0 < n; c0 += K * G) {
-					u32x4 v[K];
+	/* set A holds frames p + u*nseg, set B frames p + (U + u)*nseg */
+	u32x3 d[U];
+	RFrame fa[U], fb[U];
+	u32x4 va[U][K], vb[U][K];
 #pragma unroll
-					for (int k = 0; k < K; k++)
-						v[k] = grid_chunk(base, n, head, tail, c0 + k * G);
+	for (int u = 0; u < U; u++)
+		d[u] = desc(seg + u * nseg);
 #pragma unroll
-					for (int k = 0; k < K; k++)
-						accum(v[k], E, O);
-				}
-				uint32_t s = (lo & 1u) ? (O << 8) + E : (E << 8) + O;
-				s = seg_sum<G>(s);
-				/* pseudo header (RFC 768 / RFC 2460 8.1) */
-				if (ps.family == 4)
-					s += be_words(ip + 12, 8);
-				else
-					s += be_words(ip + 8, 32);
-				s += 17u + (ulen >> 16) + (ulen & 0xffffu);
-				const bool nocheck = (pkt[ps.l4 + 6] | pkt[ps.l4 + 7]) == 0;
-				good = nocheck ? ps.family == 4 : fold16(s) == 0xffffu;
-			}
-			if (good && iphdr && ps.family == 4) {
-				/* RFC 1071 over the 4*ihl-byte header, check included */
-				uint32_t h = 0;
-				for (uint32_t j = 2 * lane; j < 4 * ihl; j += 2 * G)
-					h += be16(ip + j);
-				h = seg_sum<G>(h);
-				good = fold16(h) == 0xffffu;
-			}
-			if (!good)
-				status = XCSUM_RX_CSUM;
-		}
+	for (int u = 0; u < U; u++) {
+		fa[u] = rx_resolve(a, d[u], seg + u * nseg < a.n);
+		d[u] = desc(seg + (U + u) * nseg);
+	}
+	__builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+	for (int u = 0; u < U; u++)
+		rx_issue<G, K>(a, fa[u], lane, va[u]);
 
-		/* ---- the record: lanes 0..3 store one 16-byte piece each ---- */
-		if (lane < 4) {
-			u32x4 w = {0u, 0u, 0u, 0u};
-			if (lane == 0) {
-				const uint64_t body = ps.ok ? addr + ps.l4 + 8 : 0;
-				w = u32x4{(uint32_t)addr, (uint32_t)(addr >> 32), (uint32_t)body,
-					  (uint32_t)(body >> 32)};
-			} else if (lane == 1) {
-				w.x = ps.ok ? ulen - 8u : 0u;
-				w.y = status | (ps.family << 8) | ((ps.ok ? ps.l4 : 0u) << 16);
-				w.z = sport | (dport << 16);
-				w.w = 0;
-			} else if (ps.ok) {
-				/* lane 2: saddr, lane 3: daddr (IPv4: 4 bytes) */
-				const uint8_t *src = pkt + ps.l3 + (ps.family == 4 ? 12 : 8) +
-						     (lane == 3 ? (ps.family == 4 ? 4 : 16) : 0);
-				const uint32_t nb = ps.family == 4 ? 4 : 16;
-				uint32_t b[4] = {0u, 0u, 0u, 0u};
-				for (uint32_t i = 0; i < nb; i++)
-					b[i >> 2] |= (uint32_t)src[i] << (8 * (i & 3));
-				w = u32x4{b[0], b[1], b[2], b[3]};
-			}
-			*((u32x4 *)(a.msgs + p) + lane) = w;
+	for (uint32_t p = seg; p < a.n; p += 2 * U * nseg) {
+#pragma unroll
+		for (int u = 0; u < U; u++) {
+			fb[u] = rx_resolve(a, d[u], p + (U + u) * nseg < a.n);
+			d[u] = desc(p + (2 * U + u) * nseg);
 		}
-		if (lane == 0 && status == XCSUM_RX_OK)
-			delivered++;
+		__builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+		for (int u = 0; u < U; u++)
+			rx_issue<G, K>(a, fb[u], lane, vb[u]);
+#pragma unroll
+		for (int u = 0; u < U; u++)
+			rx_frame<G, K>(a, st, fa[u], va[u], p + u * nseg, lane, verify, iphdr,
+				       delivered);
+
+#pragma unroll
+		for (int u = 0; u < U; u++) {
+			fa[u] = rx_resolve(a, d[u], p + (2 * U + u) * nseg < a.n);
+			d[u] = desc(p + (3 * U + u) * nseg);
+		}
+		__builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+		for (int u = 0; u < U; u++)
+			rx_issue<G, K>(a, fa[u], lane, va[u]);
+#pragma unroll
+		for (int u = 0; u < U; u++)
+			rx_frame<G, K>(a, st, fb[u], vb[u], p + (U + u) * nseg, lane, verify, iphdr,
+				       delivered);
 	}
 	if (a.count && lane == 0 && delivered)
 		atomicAdd(a.count, delivered);
 }
 
-template <int G, int K>
+template <int G, int K, int U>
 static hipError_t launch_rx_t(const RxArgs &a, int cus, hipStream_t s)
 {
 	static int occ = 0;
 	if (!occ) {
 		int nb = 0;
-		if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, rx_kernel<G, K>, 256, 0) !=
+		if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, rx_kernel<G, K, U>, 256, 0) !=
 			    hipSuccess || nb <= 0)
 			nb = 4;
 		occ = nb;
 	}
-	uint64_t blocks = ((uint64_t)a.n * G + 255) / 256;
+	uint64_t blocks = (((uint64_t)a.n + U - 1) / U * G + 255) / 256;
 	const uint64_t cap = (uint64_t)cus * occ;
 	if (blocks > cap)
 		blocks = cap;
 	if (blocks == 0)
 		blocks = 1;
-	hipLaunchKernelGGL((rx_kernel<G, K>), dim3((unsigned)blocks), dim3(256), 0, s, a);
+	hipLaunchKernelGGL((rx_kernel<G, K, U>), dim3((unsigned)blocks), dim3(256), 0, s, a);
 	return hipGetLastError();
 }
+
+#define XCSUM_RX_GEOMETRIES(X) \
+	X(2, 4, 1) X(2, 4, 2) X(4, 2, 1) X(4, 2, 2) X(8, 1, 2) X(8, 2, 1) \
+	X(16, 2, 1) X(16, 3, 1) X(16, 6, 1) X(64, 9, 1)
 
 hipError_t launch_rx(const RxArgs &a, uint32_t len_hint, int cus, hipStream_t s)
 {
 	if (a.n == 0)
 		return hipSuccess;
-	int G = 16;
-	const char *e = getenv("XCSUM_RX_GEOMETRY");   /* "G" for sweeps */
-	if (e)
-		G = atoi(e);
-	else if (len_hint && len_hint <= 160)
-		G = 4;
-	else if (len_hint > 3000)
-		G = 64;
-	switch (G) {
-	case 4:  return launch_rx_t<4, 2>(a, cus, s);
-	case 64: return launch_rx_t<64, 2>(a, cus, s);
-	default: return launch_rx_t<16, 4>(a, cus, s);
+	int G, K, U = 1;
+	const char *e = getenv("XCSUM_RX_GEOMETRY");   /* "G,K[,U]" for sweeps and tests */
+	if (!(e && sscanf(e, "%d,%d,%d", &G, &K, &U) >= 2)) {
+		U = 1;
+		/* chunks of a typical frame from eth+12 to its end: cover it in
+		 * one preload with as few lanes as that allows; without VERIFY
+		 * only the 6-chunk header stage is loaded.  Measured
+		 * (tools/bench_rx.py, profiles/r01/bench_rx_*.log): two frames per
+		 * group per stage pay for their registers only on small frames. */
+		const uint32_t chunks = (len_hint + 6) / 16;  /* ceil((len + 3 - 12) / 16) */
+		if (!(a.flags & XCSUM_F_VERIFY)) { G = 4; K = 2; U = 2; }
+		else if (chunks <= 8) { G = 2; K = 4; U = 2; }
+		else if (chunks <= 16) { G = 8; K = 2; }
+		else if (chunks <= 32) { G = 16; K = 2; }
+		else if (chunks <= 48) { G = 16; K = 3; }
+		else if (chunks <= 96) { G = 16; K = 6; }
+		else { G = 64; K = 9; }
 	}
+#define X(g_, k_, u_) \
+	if (G == g_ && K == k_ && U == u_) return launch_rx_t<g_, k_, u_>(a, cus, s);
+	XCSUM_RX_GEOMETRIES(X)
+#undef X
+	return hipErrorInvalidValue;
 }
 
 } /* namespace xcsum */

@@ -52,7 +52,20 @@ def run_rx(torch, eng, umem, desc, flags, len_hint=0, geometry=None):
     return recs, int(d_count.cpu().item())
 
 
-@pytest.mark.parametrize("geometry", [4, 16, 64])
+GEOMETRIES = ["2,4,1", "2,4,2", "4,2,1", "4,2,2", "8,1,2", "8,2,1", "16,2,1", "16,3,1", "16,6,1", "64,9,1"]
+
+
+def test_rx_geometry_list_matches_kernel():
+    src = open(os.path.join(os.path.dirname(GOLDEN), "..", "libxudp_amd", "csrc",
+                            "xcsum_rx.hip")).read()
+    i = src.index("#define XCSUM_RX_GEOMETRIES")
+    block = src[i:src.index("\n\n", i)]
+    import re
+    assert sorted(GEOMETRIES) == sorted(",".join(t) for t in
+                                        re.findall(r"X\((\d+), (\d+), (\d+)\)", block))
+
+
+@pytest.mark.parametrize("geometry", GEOMETRIES)
 @pytest.mark.parametrize("name", sorted(FLAGS))
 def test_rx_matches_fixtures(torch_cuda, engine, rx, name, geometry):
     recs, count = run_rx(torch_cuda, engine, rx["umem"], rx["desc"], FLAGS[name],
@@ -63,7 +76,8 @@ def test_rx_matches_fixtures(torch_cuda, engine, rx, name, geometry):
     assert count == int((exp["status"] == X.RX_OK).sum())
 
 
-def test_rx_generated_vs_oracle(torch_cuda, engine):
+@pytest.mark.parametrize("geometry", [None] + GEOMETRIES)
+def test_rx_generated_vs_oracle(torch_cuda, engine, geometry):
     """6k frames: the corpus under three seeds, at irregular offsets."""
     frames = []
     for seed in (1, 2, 3):
@@ -73,10 +87,11 @@ def test_rx_generated_vs_oracle(torch_cuda, engine):
     umem, offs, lens = rx_frames.layout(frames, rng)
     desc = np.zeros(len(frames), dtype=X.DESC_DTYPE)
     desc["addr"], desc["len"] = offs, lens
+    exps = {flags: oracle.rx_batch(umem, desc, flags) for flags in FLAGS.values()}
     for flags in FLAGS.values():
-        for hint in (0, 100, 1500, 9000):
-            recs, count = run_rx(torch_cuda, engine, umem, desc, flags, hint)
-            exp = oracle.rx_batch(umem, desc, flags)
+        for hint in ((0, 100, 1500, 9000) if geometry is None else (0,)):
+            recs, count = run_rx(torch_cuda, engine, umem, desc, flags, hint, geometry)
+            exp = exps[flags]
             assert np.array_equal(recs.view(np.uint8), exp.view(np.uint8)), (flags, hint)
             assert count == int((exp["status"] == X.RX_OK).sum())
 
@@ -90,6 +105,8 @@ def test_rx_empty_batch(torch_cuda, engine):
     assert int(c.item()) == 0
     with pytest.raises(X.XcsumError):
         engine.rx_device(None, None, 3, None)
+    with pytest.raises(X.XcsumError):   # d_umem must be 4-byte aligned
+        engine.rx_device(d.data_ptr() + 1, d, 1, d, c, X.F_VERIFY)
 
 
 @pytest.mark.slow

@@ -1,0 +1,113 @@
+#!/usr/bin/env python3
+"""Throughput of xcsum_rx_device (xudp_nic_recv_channel's per-frame work on
+the GPU, csrc/xcsum_rx.hip) on BASELINE-sized batches of received frames.
+
+Frames: the bench generator's packed layout (configs 2/3/4: 1M x 1472 B
+IPv4, 1M x 64 B IPv4, 1M x 1472 B IPv6), checksummed in place by the TX
+kernel (RFC rules, IPv4 header too) so every frame verifies.  Batches under
+1 GiB are replicated and rotated (no pass served by the Infinity Cache).
+
+Bytes moved per frame: descriptor 16 + record 64 + the frame bytes the
+kernel must read -- the whole frame with XCSUM_F_VERIFY, the 64-byte header
+line without.  For comparison the checksum kernel's VERIFY mode (2-byte
+result instead of the 64-byte record) runs on the same buffers.
+One JSON line per (config, flags, geometry).
+Usage: python tools/bench_rx.py [--configs 2,3,4] [--geoms "auto;4,2,1;16,6,1"]"""
+import argparse
+import json
+import math
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import bench  # noqa: E402
+import libxudp_amd as X  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--configs", default="2,3,4")
+    ap.add_argument("--geoms", default="auto")
+    ap.add_argument("--reps", type=int, default=20)
+    args = ap.parse_args()
+    import torch
+    dev = torch.device("cuda:0")
+    eng = X.Engine(0)
+    s = torch.cuda.current_stream(dev)
+    for cid in [int(c) for c in args.configs.split(",")]:
+        cfg = bench.CONFIGS[cid]
+        n, fam = cfg["n"], cfg["family"]
+        seed = bench.SEED_BASE ^ cid
+        desc, nbytes = X.gen_layout(n, fam, cfg["pmin"], cfg["pmax"], seed=seed)
+        d_desc = torch.from_numpy(desc.view(np.uint8)).to(dev)
+        nrot = max(1, math.ceil((1 << 30) / nbytes))
+        bufs = [torch.empty(nbytes + 64, dtype=torch.uint8, device=dev) for _ in range(nrot)]
+        eng.gen_fill_device(bufs[0], d_desc, n, fam, seed, 0)
+        mode = X.MODE_V6 if fam == 6 else X.MODE_V4_RFC
+        eng.batch_device(bufs[0], d_desc, n, None, mode, X.F_INPLACE | X.F_IPHDR)
+        for b in bufs[1:]:
+            b.copy_(bufs[0])
+        d_msgs = torch.empty(n * 64, dtype=torch.uint8, device=dev)
+        d_count = torch.zeros(1, dtype=torch.int32, device=dev)
+        d_out = torch.empty(n, dtype=torch.int16, device=dev)
+        frame_bytes = int(desc["len"].astype(np.int64).sum())
+        hint = int(desc["len"].mean())
+        torch.cuda.synchronize()
+
+        def timed(fn):
+            for k in range(3):
+                fn(k)
+            evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                   for _ in range(args.reps)]
+            for k, (e0, e1) in enumerate(evs):
+                e0.record(s)
+                fn(k)
+                e1.record(s)
+            torch.cuda.synchronize()
+            return float(np.median([a.elapsed_time(b) for a, b in evs])) * 1e-3
+
+        for gname in args.geoms.split(";"):
+            if gname == "auto":
+                os.environ.pop("XCSUM_RX_GEOMETRY", None)
+            else:
+                os.environ["XCSUM_RX_GEOMETRY"] = gname
+            for fname, flags in (("plain", 0), ("verify", X.F_VERIFY),
+                                 ("verify_iphdr", X.F_VERIFY | X.F_IPHDR)):
+                def rx(k):
+                    d_count.zero_()
+                    eng.rx_device(bufs[k % nrot], d_desc, n, d_msgs, d_count, flags, hint,
+                                  stream=s.cuda_stream)
+                t = timed(rx)
+                ok = int(d_count.item()) == n
+                read = frame_bytes if flags else 64 * n
+                moved = read + n * (16 + 64)
+                print(json.dumps({"kernel": "rx", "config": cid, "flags": fname,
+                                  "geometry": gname, "frames": n, "ms": round(t * 1e3, 4),
+                                  "mpps": round(n / t / 1e6, 1),
+                                  "GBps_moved": round(moved / t / 1e9, 1),
+                                  "pct_hbm_peak": round(100 * moved / t / 8e12, 1),
+                                  "all_delivered": ok}), flush=True)
+        os.environ.pop("XCSUM_RX_GEOMETRY", None)
+
+        def ver(k):
+            eng.batch_device(bufs[k % nrot], d_desc, n, d_out, mode, X.F_VERIFY, hint,
+                             stream=s.cuda_stream)
+        t = timed(ver)
+        ok = bool((d_out == 0).all().item())
+        moved = frame_bytes + n * (16 + 2)
+        print(json.dumps({"kernel": "csum_verify", "config": cid, "frames": n,
+                          "ms": round(t * 1e3, 4), "mpps": round(n / t / 1e6, 1),
+                          "GBps_moved": round(moved / t / 1e9, 1),
+                          "pct_hbm_peak": round(100 * moved / t / 8e12, 1),
+                          "all_valid": ok}), flush=True)
+        del bufs, d_msgs
+        torch.cuda.empty_cache()
+    eng.close()
+
+
+if __name__ == "__main__":
+    main()
