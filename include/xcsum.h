@@ -212,7 +212,9 @@ struct xcsum_rx_msg {
  * XCSUM_RX_OK records (uint32, device memory).  flags: XCSUM_F_VERIFY,
  * XCSUM_F_IPHDR.  len_hint = typical frame length (kernel geometry only).
  * d_umem must be 4-byte aligned (-XCSUM_ERR_INVAL otherwise); frames may sit
- * at any byte offset in it.  Asynchronous on `stream`. */
+ * at any byte offset in it.  Asynchronous on `stream`; with d_count the
+ * launches use per-context scratch, so keep one context's receive batches on
+ * one stream (one context per stream, as everywhere in this ABI). */
 int xcsum_rx_device(xcsum_ctx *ctx, const uint8_t *d_umem, const struct xcsum_desc *d_desc,
 		    uint32_t n, struct xcsum_rx_msg *d_msgs, uint32_t *d_count, uint32_t flags,
 		    uint32_t len_hint, void *stream);

@@ -71,7 +71,11 @@ extern "C" int xcsum_ctx_create(int device, xcsum_ctx **out)
 	c->cus = prop.multiProcessorCount;
 	c->max_blocks = c->cus * 8;
 	c->d_err = nullptr;
-	if (hipMalloc(&c->d_err, sizeof(unsigned long long)) != hipSuccess) {
+	c->d_rx_part = nullptr;
+	if (hipMalloc(&c->d_err, sizeof(unsigned long long)) != hipSuccess ||
+	    hipMalloc(&c->d_rx_part, RX_PART_MAX * sizeof(uint32_t)) != hipSuccess) {
+		if (c->d_err)
+			(void)hipFree(c->d_err);
 		delete c;
 		return -XCSUM_ERR_NOMEM;
 	}
@@ -124,6 +128,8 @@ extern "C" void xcsum_ctx_destroy(xcsum_ctx *c)
 		(void)hipHostUnregister(r.host);
 	if (c->d_err)
 		(void)hipFree(c->d_err);
+	if (c->d_rx_part)
+		(void)hipFree(c->d_rx_part);
 	delete c;
 }
 
@@ -239,10 +245,11 @@ extern "C" int xcsum_rx_device(xcsum_ctx *c, const uint8_t *d_umem, const struct
 	if ((uintptr_t)d_umem & 3u)   /* chunk grid: see xcsum_rx.hip */
 		return -XCSUM_ERR_INVAL;
 	HIPCHK(hipSetDevice(c->device));
-	if (d_count)
-		HIPCHK(hipMemsetAsync(d_count, 0, sizeof(uint32_t), (hipStream_t)stream));
-	if (n == 0)
+	if (n == 0) {
+		if (d_count)
+			HIPCHK(hipMemsetAsync(d_count, 0, sizeof(uint32_t), (hipStream_t)stream));
 		return 0;
+	}
 	RxArgs a;
 	a.umem = d_umem;
 	a.desc = d_desc;
@@ -250,6 +257,7 @@ extern "C" int xcsum_rx_device(xcsum_ctx *c, const uint8_t *d_umem, const struct
 	a.flags = flags & (XCSUM_F_VERIFY | XCSUM_F_IPHDR);
 	a.msgs = d_msgs;
 	a.count = d_count;
+	a.part = c->d_rx_part;
 	HIPCHK(launch_rx(a, len_hint, c->cus, (hipStream_t)stream));
 	return 0;
 }

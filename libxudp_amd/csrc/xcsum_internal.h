@@ -84,7 +84,11 @@ struct RxArgs {
 	uint32_t n, flags;
 	struct xcsum_rx_msg *msgs;
 	uint32_t *count;               /* may be null */
+	uint32_t *part;                /* per-block counts (ctx scratch, RX_PART_MAX) */
 };
+
+/* per-block delivered counts of one receive launch: >= CUs x blocks per CU */
+constexpr uint32_t RX_PART_MAX = 4096;
 
 hipError_t launch_rx(const RxArgs &a, uint32_t len_hint, int cus, hipStream_t s);
 
@@ -120,6 +124,7 @@ struct Ctx {
 	int blocks_per_cu;             /* forced grid cap, 0: automatic */
 	int order_rlog, order_tlog;    /* visiting order, rlog < 0: automatic */
 	unsigned long long *d_err;
+	uint32_t *d_rx_part;           /* RX_PART_MAX per-block receive counts */
 	std::vector<Region> regions;
 
 	/* host path staging: NSLOT slots of frames + descriptors + results */

@@ -370,6 +370,31 @@ static __device__ __forceinline__ u32x4 keep_span(u32x4 v, int a, int b)
 	return v;
 }
 
+/* a where the lane's bit of `lanes` is clear, b where it is set: v_cndmask
+ * through inline asm, so the compiler cannot fold a select chain back into a
+ * runtime-indexed (scratch) array read */
+static __device__ __forceinline__ uint32_t pick(uint32_t a, uint32_t b, uint64_t lanes)
+{
+	uint32_t r;
+	asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "s"(lanes));
+	return r;
+}
+
+/* Chunk C of a frame held by a group of G <= 4 lanes (lane C % G, slot
+ * C / G), copied into every lane of the group with DPP quad_perm. */
+template <int G, int K, int C>
+static __device__ __forceinline__ void dpp_chunk(const u32x4 (&vc)[K], uint32_t *raw)
+{
+	constexpr int k = C / G < K ? C / G : K - 1, src = C % G;
+	constexpr int ctrl = G == 4 ? (src | src << 2 | src << 4 | src << 6)
+			   : G == 2 ? (src | src << 2 | (2 + src) << 4 | (2 + src) << 6)
+				    : 0xE4;   /* G == 1: identity */
+	raw[4 * C + 0] = (uint32_t)__builtin_amdgcn_mov_dpp((int)vc[k].x, ctrl, 0xF, 0xF, false);
+	raw[4 * C + 1] = (uint32_t)__builtin_amdgcn_mov_dpp((int)vc[k].y, ctrl, 0xF, 0xF, false);
+	raw[4 * C + 2] = (uint32_t)__builtin_amdgcn_mov_dpp((int)vc[k].z, ctrl, 0xF, 0xF, false);
+	raw[4 * C + 3] = (uint32_t)__builtin_amdgcn_mov_dpp((int)vc[k].w, ctrl, 0xF, 0xF, false);
+}
+
 /* Everything for frame p once its chunks v[] have landed: stage, parse,
  * verify, record.  Group-uniform; every lane of the wave must call it. */
 template <int G, int K>
@@ -377,42 +402,63 @@ static __device__ __forceinline__ void rx_frame(const RxArgs &a, uint32_t *st, c
 						const u32x4 (&vc)[K], uint32_t p, uint32_t lane,
 						bool verify, bool iphdr, uint32_t &delivered)
 {
-	/* 1. header stage */
-#pragma unroll
-	for (int k = 0; k < K; k++) {
-		const uint32_t c = lane + k * G;
-		if (k * G < (int)STAGE_CHUNKS && c < STAGE_CHUNKS)
-			*((u32x4 *)(st + 4 * c)) = vc[k];
-	}
-	__builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-	__builtin_amdgcn_wave_barrier();
-	__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-
-	/* 2. packet_parse() from the stage (frame byte x at x - 12 + h) */
 	const uint32_t len = rx_len(fc);
 	const uint32_t nchunks = rx_nchunks(fc);
-	const uint32_t fh = rx_h(fc, nchunks);
-	/* Every header field the fast path can use -- frame bytes 12..61 -- in
-	 * ONE batch of stage reads (14 dwords, no read waits on another): the
-	 * fields at x = 0 mod 4 come from dword pairs at a fixed shift, those
-	 * at x = 2 mod 4 at the shift + 2 (one select of the pair). */
-	const uint32_t s0 = fh & 3u;                    /* frame byte 12 = stage byte fh */
-	const uint32_t *dw = st + (fh >> 2);
-	uint32_t d[14];
+	const uint32_t fh = rx_h(fc, nchunks);          /* frame byte 12 = header byte fh */
+
+	/* 1. the header: hdr[i] = frame bytes [12 + 4i, 16 + 4i), i < 13 (every
+	 * field the fast path can use lies in bytes 12..61).  Chunks 0..5 of
+	 * the grid hold it, spread over the group's lanes. */
+	uint32_t hdr[13];
+	if (G <= 4) {
+		/* Small groups: broadcast the 6 chunks inside the quad with DPP
+		 * quad_perm (pure VALU, no LDS round trip), then realign by fh. */
+		uint32_t raw[24];
+		dpp_chunk<G, K, 0>(vc, raw);
+		dpp_chunk<G, K, 1>(vc, raw);
+		dpp_chunk<G, K, 2>(vc, raw);
+		dpp_chunk<G, K, 3>(vc, raw);
+		dpp_chunk<G, K, 4>(vc, raw);
+		dpp_chunk<G, K, 5>(vc, raw);
+		const uint32_t q = fh >> 2, r = fh & 3u;
+		const uint64_t m1 = __builtin_amdgcn_ballot_w64(q == 1);
+		const uint64_t m2 = __builtin_amdgcn_ballot_w64(q == 2);
+		const uint64_t m3 = __builtin_amdgcn_ballot_w64(q == 3);
+		uint32_t sh[14];
 #pragma unroll
-	for (int i = 0; i < 14; i++)
-		d[i] = dw[i];
-	auto f0 = [&](int x) {                          /* x = 0 mod 4 */
+		for (int j = 0; j < 14; j++)
+			sh[j] = pick(pick(pick(raw[j], raw[j + 1], m1), raw[j + 2], m2), raw[j + 3], m3);
+#pragma unroll
+		for (int i = 0; i < 13; i++)
+			hdr[i] = __builtin_amdgcn_alignbyte(sh[i + 1], sh[i], r);
+	} else {
+		/* Wide groups: through a per-frame LDS stage, read back in one
+		 * batch of 14 dwords (no read waits on another). */
+#pragma unroll
+		for (int k = 0; k < K; k++) {
+			const uint32_t c = lane + k * G;
+			if (k * G < (int)STAGE_CHUNKS && c < STAGE_CHUNKS)
+				*((u32x4 *)(st + 4 * c)) = vc[k];
+		}
+		__builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+		__builtin_amdgcn_wave_barrier();
+		__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+		const uint32_t *dw = st + (fh >> 2);
+		uint32_t d[14];
+#pragma unroll
+		for (int i = 0; i < 14; i++)
+			d[i] = dw[i];
+#pragma unroll
+		for (int i = 0; i < 13; i++)
+			hdr[i] = __builtin_amdgcn_alignbyte(d[i + 1], d[i], fh & 3u);
+	}
+	auto f0 = [&](int x) { return hdr[(x - 12) >> 2]; };          /* x = 0 mod 4 */
+	auto f2 = [&](int x) {                                         /* x = 2 mod 4 */
 		const int i = (x - 12) >> 2;
-		return __builtin_amdgcn_alignbyte(d[i + 1], d[i], s0);
+		return __builtin_amdgcn_alignbyte(hdr[i + 1], hdr[i], 2u);
 	};
-	const bool wrap = s0 >= 2u;
-	auto f2 = [&](int x) {                          /* x = 2 mod 4 */
-		const int m = (x - 14) >> 2;
-		const uint32_t lo_ = wrap ? d[m + 1] : d[m];
-		const uint32_t hi_ = wrap ? d[m + 2] : d[m + 1];
-		return __builtin_amdgcn_alignbyte(hi_, lo_, (s0 + 2u) & 3u);
-	};
+
+	/* 2. packet_parse() */
 	const uint32_t w12 = f0(12);                    /* h_proto, ver/ihl, tos */
 	const uint32_t w20 = f0(20);                    /* v4: proto at 23; v6: nexthdr at 20 */
 	const uint32_t w26 = f2(26), w30 = f2(30);      /* iph saddr / daddr fields */
@@ -531,10 +577,12 @@ static __device__ __forceinline__ void rx_frame(const RxArgs &a, uint32_t *st, c
 	if (lane == 0 && present && r.status == XCSUM_RX_OK)
 		delivered++;
 
-	/* the stage is rewritten next iteration: reads first */
-	__builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-	__builtin_amdgcn_wave_barrier();
-	__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+	if (G > 4) {
+		/* the stage is rewritten next iteration: reads first */
+		__builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+		__builtin_amdgcn_wave_barrier();
+		__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+	}
 }
 
 /*
@@ -550,7 +598,7 @@ __global__ void __launch_bounds__(256) rx_kernel(RxArgs a)
 {
 	/* per-frame header stage: STAGE_CHUNKS chunks + one dword of slack */
 	constexpr uint32_t SW = STAGE_CHUNKS * 4 + 4;   /* dwords per group */
-	__shared__ __attribute__((aligned(16))) uint32_t stage[(256 / G) * SW];
+	__shared__ __attribute__((aligned(16))) uint32_t stage[G > 4 ? (256 / G) * SW : 4];
 	const uint32_t lane = threadIdx.x & (G - 1);
 	const uint32_t grp = threadIdx.x / G;
 	uint32_t *st = stage + grp * SW;
@@ -611,8 +659,33 @@ __global__ void __launch_bounds__(256) rx_kernel(RxArgs a)
 			rx_frame<G, K>(a, st, fb[u], vb[u], p + (U + u) * nseg, lane, verify, iphdr,
 				       delivered);
 	}
-	if (a.count && lane == 0 && delivered)
-		atomicAdd(a.count, delivered);
+	/* The delivered count: one plain store per block, summed by a second
+	 * one-block kernel.  Device-scope atomics to one address serialise
+	 * (~8 ns each): even one per wave cost ~20 us on a config-3 batch. */
+	if (a.count) {
+		__shared__ uint32_t wsum[4];
+		const uint32_t tot = seg_sum<64>(delivered);   /* all lanes live again */
+		if ((threadIdx.x & 63) == 0)
+			wsum[threadIdx.x >> 6] = tot;
+		__syncthreads();
+		if (threadIdx.x == 0)
+			a.part[blockIdx.x] = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+	}
+}
+
+__global__ void __launch_bounds__(256) rx_count_kernel(const uint32_t *part, uint32_t nblocks,
+						      uint32_t *count)
+{
+	__shared__ uint32_t wsum[4];
+	uint32_t v = 0;
+	for (uint32_t i = threadIdx.x; i < nblocks; i += 256)
+		v += part[i];
+	v = seg_sum<64>(v);
+	if ((threadIdx.x & 63) == 0)
+		wsum[threadIdx.x >> 6] = v;
+	__syncthreads();
+	if (threadIdx.x == 0)
+		*count = wsum[0] + wsum[1] + wsum[2] + wsum[3];
 }
 
 template <int G, int K, int U>
@@ -630,9 +703,14 @@ static hipError_t launch_rx_t(const RxArgs &a, int cus, hipStream_t s)
 	const uint64_t cap = (uint64_t)cus * occ;
 	if (blocks > cap)
 		blocks = cap;
+	if (blocks > RX_PART_MAX)
+		blocks = RX_PART_MAX;
 	if (blocks == 0)
 		blocks = 1;
 	hipLaunchKernelGGL((rx_kernel<G, K, U>), dim3((unsigned)blocks), dim3(256), 0, s, a);
+	if (a.count)
+		hipLaunchKernelGGL(rx_count_kernel, dim3(1), dim3(256), 0, s, a.part,
+				   (uint32_t)blocks, a.count);
 	return hipGetLastError();
 }
 

@@ -33,6 +33,7 @@ def main():
     ap.add_argument("--configs", default="2,3,4")
     ap.add_argument("--geoms", default="auto")
     ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--no-count", action="store_true", help="pass d_count = NULL")
     args = ap.parse_args()
     import torch
     dev = torch.device("cuda:0")
@@ -78,11 +79,15 @@ def main():
             for fname, flags in (("plain", 0), ("verify", X.F_VERIFY),
                                  ("verify_iphdr", X.F_VERIFY | X.F_IPHDR)):
                 def rx(k):
-                    d_count.zero_()
-                    eng.rx_device(bufs[k % nrot], d_desc, n, d_msgs, d_count, flags, hint,
+                    eng.rx_device(bufs[k % nrot], d_desc, n, d_msgs,
+                                  None if args.no_count else d_count, flags, hint,
                                   stream=s.cuda_stream)
                 t = timed(rx)
-                ok = int(d_count.item()) == n
+                if args.no_count:
+                    st = d_msgs.view(-1, 64)[:, 20].cpu()
+                    ok = bool((st == 0).all().item())
+                else:
+                    ok = int(d_count.item()) == n
                 read = frame_bytes if flags else 64 * n
                 moved = read + n * (16 + 64)
                 print(json.dumps({"kernel": "rx", "config": cid, "flags": fname,
