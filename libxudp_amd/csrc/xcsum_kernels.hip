@@ -507,13 +507,39 @@ static __device__ __forceinline__ void consume(const CsumArgs &a, const Frame (&
 	}
 }
 
+/* XCSUM_PINGPONG=0 builds the previous loop shape (A/B only): "next" copied
+ * into "current" at the loop latch */
+#ifndef XCSUM_PINGPONG
+#define XCSUM_PINGPONG 1
+#endif
+
+/* wave-uniform split: the jumbo path lives in its own copy of the body, so
+ * its drains never merge into the common path's vmcnt bookkeeping */
+template <int G, int U, int K, bool ORD>
+static __device__ __forceinline__ void consume_any(const CsumArgs &a, const Frame (&fc)[U],
+						   const u32x4 (&vc)[U][K], uint32_t lane,
+						   uint32_t p0, uint32_t nseg)
+{
+	bool big = false;
+#pragma unroll
+	for (int u = 0; u < U; u++)
+		big |= fc[u].nchunks > K * G;
+	if (__builtin_amdgcn_ballot_w64(big))
+		consume<G, U, K, true, ORD>(a, fc, vc, lane, p0, nseg);
+	else
+		consume<G, U, K, false, ORD>(a, fc, vc, lane, p0, nseg);
+}
+
 /*
  * Persistent grid; segment s (G lanes) owns frames s, s + nseg, ... and
- * handles U of them per iteration.  Two-stage software pipeline: while
- * iteration i's chunks are reduced, iteration i+1's chunks are in flight and
- * iteration i+2's descriptors are loading.  Descriptor loads are issued
- * BEFORE the chunk loads of the same step, so the in-order vmcnt wait for
- * them never waits on chunk data.
+ * handles U of them per step.  Two-stage software pipeline written as a
+ * ping-pong over two register sets (A, B): while step i's chunks are
+ * reduced, step i+1's chunks are in flight and step i+2's descriptors are
+ * loading.  Descriptor loads are issued BEFORE the chunk loads of the same
+ * step, so the in-order vmcnt wait for them never waits on chunk data.
+ * The ping-pong matters: with one "current" set refilled from a "next" set
+ * at the loop latch, that copy needs the next step's loads to have landed,
+ * and the ISA showed a vmcnt(0) there -- one step in flight, not two.
  */
 template <int G, int U, int K, bool ORD>
 static __device__ __forceinline__ void csum_loop(const CsumArgs &a)
@@ -524,16 +550,20 @@ static __device__ __forceinline__ void csum_loop(const CsumArgs &a)
 	if (G == 64)
 		seg = __builtin_amdgcn_readfirstlane(seg);
 	const uint32_t step = nseg * U;
+	const uint32_t limit = ORD ? a.ord.nlog : a.n;
+	/* logical index q names a frame only below the logical range end (past
+	 * it, frame_of() would alias real frames) */
+	auto has = [&](uint32_t q) { return q < limit && fidx<ORD>(a, q) < a.n; };
 
 	u32x4 d[U];
-	Frame fc[U];
-	u32x4 vc[U][K];
+	Frame fa[U];
+	u32x4 va[U][K];
 #pragma unroll
 	for (int u = 0; u < U; u++)
 		d[u] = load_desc<G == 64>(a, fidx<ORD>(a, seg + u * nseg));
 #pragma unroll
 	for (int u = 0; u < U; u++)
-		fc[u] = resolve<Grid<G, K>::DW>(a, d[u], fidx<ORD>(a, seg + u * nseg) < a.n);
+		fa[u] = resolve<Grid<G, K>::DW>(a, d[u], has(seg + u * nseg));
 #pragma unroll
 	for (int u = 0; u < U; u++)
 		d[u] = load_desc<G == 64>(a, fidx<ORD>(a, seg + step + u * nseg));
@@ -541,39 +571,55 @@ static __device__ __forceinline__ void csum_loop(const CsumArgs &a)
 	 * vmcnt queue with: the next wait for the descriptors then leaves all
 	 * chunk loads in flight */
 	__builtin_amdgcn_sched_barrier(0);
-	issue<G, U, K>(fc, lane, vc);
+	issue<G, U, K>(fa, lane, va);
 
-	for (uint32_t p0 = seg; p0 < (ORD ? a.ord.nlog : a.n); p0 += step) {
+#if XCSUM_PINGPONG
+	Frame fb[U];
+	u32x4 vb[U][K];
+	for (uint32_t p0 = seg; p0 < limit; p0 += 2 * step) {
+#pragma unroll
+		for (int u = 0; u < U; u++)
+			fb[u] = resolve<Grid<G, K>::DW>(a, d[u], has(p0 + step + u * nseg));
+#pragma unroll
+		for (int u = 0; u < U; u++)
+			d[u] = load_desc<G == 64>(a, fidx<ORD>(a, p0 + 2 * step + u * nseg));
+		__builtin_amdgcn_sched_barrier(0);
+		issue<G, U, K>(fb, lane, vb);
+		consume_any<G, U, K, ORD>(a, fa, va, lane, p0, nseg);
+
+#pragma unroll
+		for (int u = 0; u < U; u++)
+			fa[u] = resolve<Grid<G, K>::DW>(a, d[u],
+							has(p0 + 2 * step + u * nseg));
+#pragma unroll
+		for (int u = 0; u < U; u++)
+			d[u] = load_desc<G == 64>(a, fidx<ORD>(a, p0 + 3 * step + u * nseg));
+		__builtin_amdgcn_sched_barrier(0);
+		issue<G, U, K>(fa, lane, va);
+		consume_any<G, U, K, ORD>(a, fb, vb, lane, p0 + step, nseg);
+	}
+#else
+	for (uint32_t p0 = seg; p0 < limit; p0 += step) {
 		Frame fn[U];
 		u32x4 vn[U][K];
 #pragma unroll
 		for (int u = 0; u < U; u++)
-			fn[u] = resolve<Grid<G, K>::DW>(a, d[u], fidx<ORD>(a, p0 + step + u * nseg) < a.n);
+			fn[u] = resolve<Grid<G, K>::DW>(a, d[u], has(p0 + step + u * nseg));
 #pragma unroll
 		for (int u = 0; u < U; u++)
 			d[u] = load_desc<G == 64>(a, fidx<ORD>(a, p0 + 2 * step + u * nseg));
 		__builtin_amdgcn_sched_barrier(0);
 		issue<G, U, K>(fn, lane, vn);
-
-		/* wave-uniform split: the jumbo path lives in its own copy of the
-		 * body, so its drains never merge into the common path's vmcnt
-		 * bookkeeping (which keeps the next iteration in flight) */
-		bool big = false;
-#pragma unroll
-		for (int u = 0; u < U; u++)
-			big |= fc[u].nchunks > K * G;
-		if (__builtin_amdgcn_ballot_w64(big))
-			consume<G, U, K, true, ORD>(a, fc, vc, lane, p0, nseg);
-		else
-			consume<G, U, K, false, ORD>(a, fc, vc, lane, p0, nseg);
+		consume_any<G, U, K, ORD>(a, fa, va, lane, p0, nseg);
 #pragma unroll
 		for (int u = 0; u < U; u++) {
-			fc[u] = fn[u];
+			fa[u] = fn[u];
 #pragma unroll
 			for (int k = 0; k < K; k++)
-				vc[u][k] = vn[u][k];
+				va[u][k] = vn[u][k];
 		}
 	}
+#endif
 }
 
 /* The identity order gets its own copy of the loop, so descriptor-order
@@ -729,12 +775,12 @@ static hipError_t launch_lds_t(const CsumArgs &a, int cus, int bpc, hipStream_t 
 Geometry pick_geometry(uint32_t len_hint)
 {
 	if (len_hint == 0)
-		return Geometry{16, 1, 6, 3};
+		return Geometry{16, 2, 6, 1};
 	/* worst-case chunks of a frame of len_hint bytes: span <= len - 22,
 	 * plus up to 15 bytes of 16-byte misalignment */
 	uint32_t chunks = (len_hint + 8) / 16;
 	if (chunks <= 8)
-		return Geometry{4, 1, 2, 0};   /* 64-byte payloads: 2.6 TB/s algorithmic */
+		return Geometry{4, 1, 2, 4};   /* 64-byte payloads: 3.1 TB/s algorithmic */
 	if (chunks <= 16)
 		return Geometry{8, 1, 2, 0};
 	if (chunks <= 32)
@@ -742,8 +788,8 @@ Geometry pick_geometry(uint32_t len_hint)
 	if (chunks <= 48)
 		return Geometry{16, 1, 3, 0};
 	if (chunks <= 96)
-		return Geometry{16, 1, 6, 3};  /* MTU frames: 6.2 TB/s at 3 blocks/CU */
-	return Geometry{64, 1, 9, 0};          /* jumbo / mixed up to 9 KB: 6.0 TB/s */
+		return Geometry{16, 2, 6, 1};  /* MTU frames: 6.4-6.5 TB/s at 1 block/CU */
+	return Geometry{64, 1, 9, 2};          /* jumbo / mixed up to 9 KB: 6.2 TB/s */
 }
 
 template <int G, int U, int K>
