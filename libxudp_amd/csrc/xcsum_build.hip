@@ -101,6 +101,16 @@ static __device__ __forceinline__ void issue_blocks(const Msg &g, uint32_t lane,
 	}
 }
 
+/* a where the lane's bit of `lanes` is clear, b where it is set: v_cndmask
+ * through inline asm, so the compiler cannot fold a select chain back into a
+ * runtime-indexed (scratch) array read */
+static __device__ __forceinline__ uint32_t pick(uint32_t a, uint32_t b, uint64_t lanes)
+{
+	uint32_t r;
+	asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "s"(lanes));
+	return r;
+}
+
 /* the chunk's 16 payload bytes from its two blocks (byte shift by sh), bytes
  * past the payload cleared */
 static __device__ __forceinline__ u32x4 shift_chunk(u32x4 v0, u32x4 v1, uint32_t sh, uint32_t rem)
@@ -109,17 +119,15 @@ static __device__ __forceinline__ u32x4 shift_chunk(u32x4 v0, u32x4 v1, uint32_t
 	if (sh == 0) {
 		r = v0;
 	} else {
-		uint32_t w[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
-		uint32_t q = sh >> 2, s8 = sh & 3u;
+		const uint32_t w[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+		const uint32_t q = sh >> 2, s8 = sh & 3u;
+		const uint64_t m1 = __builtin_amdgcn_ballot_w64(q == 1);
+		const uint64_t m2 = __builtin_amdgcn_ballot_w64(q == 2);
+		const uint64_t m3 = __builtin_amdgcn_ballot_w64(q == 3);
 		uint32_t o[5];
 #pragma unroll
-		for (int j = 0; j < 5; j++) {
-			uint32_t x = w[j];
-			x = q == 1 ? w[j + 1] : x;
-			x = q == 2 ? w[j + 2] : x;
-			x = q == 3 ? w[j + 3] : x;
-			o[j] = x;
-		}
+		for (int j = 0; j < 5; j++)
+			o[j] = pick(pick(pick(w[j], w[j + 1], m1), w[j + 2], m2), w[j + 3], m3);
 		r.x = __builtin_amdgcn_alignbyte(o[1], o[0], s8);
 		r.y = __builtin_amdgcn_alignbyte(o[2], o[1], s8);
 		r.z = __builtin_amdgcn_alignbyte(o[3], o[2], s8);
@@ -143,21 +151,30 @@ static __device__ __forceinline__ u32x4 load_payload(const uint8_t *blk, uint32_
 	return shift_chunk(v0, v1, sh, rem);
 }
 
+/* the chunk's first min(rem, 16) bytes to d (16-byte aligned): a full chunk
+ * is one non-temporal 16-byte store; a payload's last, partial chunk is up
+ * to three dword stores, a short and a byte -- all at static offsets (the
+ * byte-by-byte loop this replaces held ~100 VGPRs of addresses) */
 static __device__ __forceinline__ void store_payload(uint8_t *d, u32x4 v, uint32_t rem)
 {
 	if (rem >= 16) {
 		__builtin_nontemporal_store(v, (__attribute__((address_space(1))) u32x4 *)d);
 		return;
 	}
-	uint32_t w[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-	for (int j = 0; j < 4; j++) {
-		int n = (int)rem - 4 * j;
-		if (n >= 4)
-			*reinterpret_cast<uint32_t *>(d + 4 * j) = w[j];
-		else
-			for (int k = 0; k < n; k++)
-				d[4 * j + k] = (uint8_t)(w[j] >> (8 * k));
+	const uint32_t nd = rem >> 2, t = rem & 3u;
+	if (nd >= 1)
+		*reinterpret_cast<uint32_t *>(d) = v.x;
+	if (nd >= 2)
+		*reinterpret_cast<uint32_t *>(d + 4) = v.y;
+	if (nd >= 3)
+		*reinterpret_cast<uint32_t *>(d + 8) = v.z;
+	if (t) {
+		const uint32_t w = nd == 0 ? v.x : (nd == 1 ? v.y : (nd == 2 ? v.z : v.w));
+		uint8_t *q = d + 4 * nd;
+		if (t & 2u)
+			*reinterpret_cast<uint16_t *>(q) = (uint16_t)w;
+		if (t & 1u)
+			q[t & 2u] = (uint8_t)(w >> (8 * (t & 2u)));
 	}
 }
 
@@ -259,10 +276,50 @@ static __device__ __forceinline__ void finish_frame(const BuildArgs &a, const Ms
 	}
 }
 
+/* Copy (unless in place), sum, header and descriptor of one message whose
+ * payload blocks v[] have landed.  Group-uniform; every lane calls it. */
+template <int G, int K, bool TWO>
+static __device__ __forceinline__ void build_msg(const BuildArgs &a, const Msg &gc,
+						 const u32x4 (&vc)[K][TWO ? 2 : 1], uint32_t ic,
+						 uint32_t lane, bool inplace, const uint16_t *tmpl,
+						 bool v6, uint32_t hdr, uint32_t sconst,
+						 uint32_t ipconst)
+{
+	uint32_t E = 0, O = 0;
+	if (__builtin_amdgcn_ballot_w64(gc.len > 16u * K * G)) {
+		/* jumbo payloads: plain walk (own copy of the body) */
+		for (uint32_t off = 16u * lane; off < gc.len; off += 16u * G) {
+			u32x4 v = load_payload(gc.blk, gc.sh, off, gc.len - off);
+			if (!inplace)
+				store_payload(gc.data + off, v, gc.len - off);
+			accum(v, E, O);
+		}
+	} else {
+#pragma unroll
+		for (int k = 0; k < K; k++) {
+			uint32_t off = 16u * (lane + k * G);
+			if (off < gc.len) {
+				u32x4 v = TWO ? shift_chunk(vc[k][0], vc[k][TWO ? 1 : 0], gc.sh,
+							    gc.len - off)
+					      : shift_chunk(vc[k][0], vc[k][0], 0u, gc.len - off);
+				if (!inplace)
+					store_payload(gc.data + off, v, gc.len - off);
+				accum(v, E, O);
+			}
+		}
+	}
+	/* payload starts 16-aligned (even address): E holds high bytes */
+	uint32_t s = seg_sum<G>((E << 8) + O);
+	if (gc.present)
+		finish_frame<G>(a, gc, ic, s, lane, tmpl, v6, hdr, sconst, ipconst);
+}
+
 /*
- * Persistent grid, G lanes per message, same two-stage pipeline as the
- * checksum kernel: message i+2's descriptor and message i+1's payload blocks
- * are in flight while message i is shifted, stored, summed and headed.
+ * Persistent grid, G lanes per message, the checksum kernel's two-stage
+ * pipeline written as a ping-pong over two register sets (A, B): message
+ * i+1's payload blocks and message i+2's descriptor are in flight while
+ * message i is shifted, stored, summed and headed.  (A "next" set copied into
+ * "current" at the loop latch would wait for the in-flight loads there.)
  */
 template <int G, int K, bool TWO>
 __global__ void __launch_bounds__(256) build_kernel(BuildArgs a)
@@ -293,62 +350,36 @@ __global__ void __launch_bounds__(256) build_kernel(BuildArgs a)
 	const uint32_t nseg = gridDim.x * (256u / G);
 	const bool inplace = (a.flags & XCSUM_F_BUILD_INPLACE) != 0;
 	const uint32_t last = a.n - 1;
+	/* message index of logical position q in the batch's visiting order
+	 * (a.ord); >= n: none (past the logical range frame_of would alias) */
+	auto idx = [&](uint32_t q) { return q < a.ord.nlog ? frame_of(a.ord, q) : a.n; };
+	auto msg = [&](uint32_t i) { return *((gu32x4 *)(a.msgs + (i < a.n ? i : last))); };
 
-	/* message indices in the batch's visiting order (a.ord); >= n: none */
-	uint32_t ic = frame_of(a.ord, seg), in = frame_of(a.ord, seg + nseg);
-	u32x4 d = *((gu32x4 *)(a.msgs + (ic < a.n ? ic : last)));
-	Msg gc = resolve_msg(a, d, ic < a.n, inplace);
-	d = *((gu32x4 *)(a.msgs + (in < a.n ? in : last)));
+	uint32_t ia = idx(seg);
+	u32x4 d = msg(ia);
+	Msg ga = resolve_msg(a, d, ia < a.n, inplace);
+	uint32_t ib = idx(seg + nseg);
+	d = msg(ib);
 	__builtin_amdgcn_sched_barrier(0);
-	u32x4 vc[K][TWO ? 2 : 1];
-	issue_blocks<G, K, TWO>(gc, lane, vc);
+	u32x4 va[K][TWO ? 2 : 1], vb[K][TWO ? 2 : 1];
+	issue_blocks<G, K, TWO>(ga, lane, va);
 
-	for (uint32_t p = seg; p < a.ord.nlog; p += nseg) {
-		Msg gn = resolve_msg(a, d, in < a.n, inplace);
-		const uint32_t iq = frame_of(a.ord, p + 2 * nseg);
-		d = *((gu32x4 *)(a.msgs + (iq < a.n ? iq : last)));
+	for (uint32_t p = seg; p < a.ord.nlog; p += 2 * nseg) {
+		Msg gb = resolve_msg(a, d, ib < a.n, inplace);
+		const uint32_t ia2 = idx(p + 2 * nseg);
+		d = msg(ia2);
 		__builtin_amdgcn_sched_barrier(0);
-		u32x4 vn[K][TWO ? 2 : 1];
-		issue_blocks<G, K, TWO>(gn, lane, vn);
+		issue_blocks<G, K, TWO>(gb, lane, vb);
+		build_msg<G, K, TWO>(a, ga, va, ia, lane, inplace, tmpl, v6, hdr, sconst, ipconst);
 
-		uint32_t E = 0, O = 0;
-		if (__builtin_amdgcn_ballot_w64(gc.len > 16u * K * G)) {
-			/* jumbo payloads: plain walk (own copy of the body) */
-			for (uint32_t off = 16u * lane; off < gc.len; off += 16u * G) {
-				u32x4 v = load_payload(gc.blk, gc.sh, off, gc.len - off);
-				if (!inplace)
-					store_payload(gc.data + off, v, gc.len - off);
-				accum(v, E, O);
-			}
-		} else {
-#pragma unroll
-			for (int k = 0; k < K; k++) {
-				uint32_t off = 16u * (lane + k * G);
-				if (off < gc.len) {
-					u32x4 v = TWO ? shift_chunk(vc[k][0], vc[k][TWO ? 1 : 0],
-								    gc.sh, gc.len - off)
-						      : shift_chunk(vc[k][0], vc[k][0], 0u,
-								    gc.len - off);
-					if (!inplace)
-						store_payload(gc.data + off, v, gc.len - off);
-					accum(v, E, O);
-				}
-			}
-		}
-		/* payload starts 16-aligned (even address): E holds high bytes */
-		uint32_t s = seg_sum<G>((E << 8) + O);
-		if (gc.present)
-			finish_frame<G>(a, gc, ic, s, lane, tmpl, v6, hdr, sconst, ipconst);
-
-		gc = gn;
-		ic = in;
-		in = iq;
-#pragma unroll
-		for (int k = 0; k < K; k++) {
-			vc[k][0] = vn[k][0];
-			if (TWO)
-				vc[k][TWO ? 1 : 0] = vn[k][TWO ? 1 : 0];
-		}
+		ga = resolve_msg(a, d, ia2 < a.n, inplace);
+		ia = ia2;
+		const uint32_t ib2 = idx(p + 3 * nseg);
+		d = msg(ib2);
+		__builtin_amdgcn_sched_barrier(0);
+		issue_blocks<G, K, TWO>(ga, lane, va);
+		build_msg<G, K, TWO>(a, gb, vb, ib, lane, inplace, tmpl, v6, hdr, sconst, ipconst);
+		ib = ib2;
 	}
 }
 
@@ -391,11 +422,10 @@ hipError_t launch_build(const BuildArgs &a, uint32_t len_hint, int cus, hipStrea
 		if (chunks <= 4) { G = 4; K = 1; }
 		else if (chunks <= 16) { G = 8; K = 2; }
 		else if (chunks <= 96) {
-			/* MTU payloads, measured (tools/bench_build.py): copies
-			 * 4.1-4.6 TB/s moved at (32,3), in place 4.0 at (16,6) */
-			const bool copy = !(a.flags & XCSUM_F_BUILD_INPLACE);
-			G = copy ? 32 : 16;
-			K = copy ? 3 : 6;
+			/* MTU payloads, measured (tools/bench_build.py,
+			 * profiles/r01/build_*.log): 5.1-5.3 TB/s moved at (16,6) */
+			G = 16;
+			K = 6;
 		}
 		else { G = 64; K = 9; }
 	}
