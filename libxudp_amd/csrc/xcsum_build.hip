@@ -423,7 +423,7 @@ hipError_t launch_build(const BuildArgs &a, uint32_t len_hint, int cus, hipStrea
 		else if (chunks <= 16) { G = 8; K = 2; }
 		else if (chunks <= 96) {
 			/* MTU payloads, measured (tools/bench_build.py,
-			 * profiles/r01/build_*.log): 5.1-5.3 TB/s moved at (16,6) */
+			 * profiles/r01/build/pingpong_*.log): 5.1-5.3 TB/s moved at (16,6) */
 			G = 16;
 			K = 6;
 		}
