@@ -69,6 +69,8 @@ struct Frame {
 	uint32_t udp_len;
 	uint32_t odd;           /* span starts at an odd address */
 	int mode;               /* 0 legacy, 1 rfc, 2 v6, -1 malformed, -2 absent */
+	uint32_t ck;            /* VERIFY: the frame's udp->check (raw 16 bits),
+				   loaded a pipeline step ahead */
 };
 
 typedef __attribute__((address_space(1))) const u32x4 gu32x4;
@@ -172,6 +174,15 @@ static __device__ __forceinline__ Frame resolve(const CsumArgs &a, u32x4 d, bool
 	if (mode < 0 || !present)
 		f.nchunks = 0;
 	f.mode = present ? mode : -2;
+	/* VERIFY needs the check field: load it with this frame's chunks, one
+	 * pipeline step before finalize() reads it (loaded there, it was a
+	 * dependent round trip on every frame).  Unconditional and unused
+	 * until then: any branch or arithmetic on it here makes the compiler
+	 * wait for the load on the spot. */
+	f.ck = 0;
+	if (a.flags & XCSUM_F_VERIFY)   /* wave-uniform: no load otherwise */
+		f.ck = *(const uint16_t *)(f.nchunks ? f.eth + (mode == 2 ? 60 : 40)
+						     : (const uint8_t *)g_zero_chunk);
 	return f;
 }
 
@@ -420,8 +431,11 @@ static __device__ __forceinline__ void finalize(const CsumArgs &a, const Frame &
 			uint32_t t = (S & 0xffffu) + (S >> 16);
 			t = (t & 0xffffu) + (t >> 16);
 			r = ~t & 0xffffu;
-			const uint8_t *ck = f.eth + (f.mode == 2 ? 60 : 40);
-			if ((ck[0] | ck[1]) == 0)  /* no checksum: IPv4 ok, IPv6 invalid */
+			/* opaque until here, or the compiler hoists the test into
+			 * resolve() and waits for the load there */
+			uint32_t ck = f.ck;
+			asm volatile("" : "+v"(ck));
+			if ((ck & 0xffffu) == 0)  /* no checksum: IPv4 ok, IPv6 invalid */
 				r = f.mode == 2 ? 0xffffu : 0u;
 			wire = bswap16(r);
 			if ((a.flags & XCSUM_F_IPHDR) && f.mode != 2) {

@@ -380,19 +380,41 @@ static __device__ __forceinline__ uint32_t pick(uint32_t a, uint32_t b, uint64_t
 	return r;
 }
 
-/* Chunk C of a frame held by a group of G <= 4 lanes (lane C % G, slot
- * C / G), copied into every lane of the group with DPP quad_perm. */
+/* dword x of chunk C of the frame, in every lane of the group: the chunk is
+ * held by lane C % G, slot C / G.  Cross-lane moves only, no LDS:
+ *   G <= 4:  DPP quad_perm inside the quad;
+ *   G == 8:  DPP row_newbcast (gfx90a+) from lanes C and 8 + C of the row,
+ *            each half of the row picks its own group's;
+ *   G == 16: DPP row_newbcast: the row is the group;
+ *   G == 64: v_readlane (the frame is wave-uniform). */
 template <int G, int K, int C>
-static __device__ __forceinline__ void dpp_chunk(const u32x4 (&vc)[K], uint32_t *raw)
+static __device__ __forceinline__ uint32_t bcast_dword(const u32x4 (&vc)[K], int x)
 {
 	constexpr int k = C / G < K ? C / G : K - 1, src = C % G;
-	constexpr int ctrl = G == 4 ? (src | src << 2 | src << 4 | src << 6)
-			   : G == 2 ? (src | src << 2 | (2 + src) << 4 | (2 + src) << 6)
-				    : 0xE4;   /* G == 1: identity */
-	raw[4 * C + 0] = (uint32_t)__builtin_amdgcn_mov_dpp((int)vc[k].x, ctrl, 0xF, 0xF, false);
-	raw[4 * C + 1] = (uint32_t)__builtin_amdgcn_mov_dpp((int)vc[k].y, ctrl, 0xF, 0xF, false);
-	raw[4 * C + 2] = (uint32_t)__builtin_amdgcn_mov_dpp((int)vc[k].z, ctrl, 0xF, 0xF, false);
-	raw[4 * C + 3] = (uint32_t)__builtin_amdgcn_mov_dpp((int)vc[k].w, ctrl, 0xF, 0xF, false);
+	const uint32_t v = x == 0 ? vc[k].x : (x == 1 ? vc[k].y : (x == 2 ? vc[k].z : vc[k].w));
+	if (G <= 4) {
+		constexpr int ctrl = G == 4 ? (src | src << 2 | src << 4 | src << 6)
+				   : G == 2 ? (src | src << 2 | (2 + src) << 4 | (2 + src) << 6)
+					    : 0xE4;   /* G == 1: identity */
+		return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, ctrl, 0xF, 0xF, false);
+	} else if (G == 8) {
+		const uint32_t lo = (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x150 + src, 0xF, 0xF, false);
+		const uint32_t hi = (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x158 + src, 0xF, 0xF, false);
+		return (threadIdx.x & 8) ? hi : lo;
+	} else if (G == 16) {
+		return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x150 + src, 0xF, 0xF, false);
+	} else {
+		return (uint32_t)__builtin_amdgcn_readlane((int)v, src);
+	}
+}
+
+template <int G, int K, int C>
+static __device__ __forceinline__ void bcast_chunk(const u32x4 (&vc)[K], uint32_t *raw)
+{
+	raw[4 * C + 0] = bcast_dword<G, K, C>(vc, 0);
+	raw[4 * C + 1] = bcast_dword<G, K, C>(vc, 1);
+	raw[4 * C + 2] = bcast_dword<G, K, C>(vc, 2);
+	raw[4 * C + 3] = bcast_dword<G, K, C>(vc, 3);
 }
 
 /* Everything for frame p once its chunks v[] have landed: stage, parse,
@@ -410,16 +432,17 @@ static __device__ __forceinline__ void rx_frame(const RxArgs &a, uint32_t *st, c
 	 * field the fast path can use lies in bytes 12..61).  Chunks 0..5 of
 	 * the grid hold it, spread over the group's lanes. */
 	uint32_t hdr[13];
-	if (G <= 4) {
-		/* Small groups: broadcast the 6 chunks inside the quad with DPP
-		 * quad_perm (pure VALU, no LDS round trip), then realign by fh. */
+	constexpr bool XL = G != 32;     /* cross-lane header (bcast_dword) */
+	if (XL) {
+		/* broadcast the 6 chunks to every lane of the group (no LDS round
+		 * trip), then realign by fh */
 		uint32_t raw[24];
-		dpp_chunk<G, K, 0>(vc, raw);
-		dpp_chunk<G, K, 1>(vc, raw);
-		dpp_chunk<G, K, 2>(vc, raw);
-		dpp_chunk<G, K, 3>(vc, raw);
-		dpp_chunk<G, K, 4>(vc, raw);
-		dpp_chunk<G, K, 5>(vc, raw);
+		bcast_chunk<G, K, 0>(vc, raw);
+		bcast_chunk<G, K, 1>(vc, raw);
+		bcast_chunk<G, K, 2>(vc, raw);
+		bcast_chunk<G, K, 3>(vc, raw);
+		bcast_chunk<G, K, 4>(vc, raw);
+		bcast_chunk<G, K, 5>(vc, raw);
 		const uint32_t q = fh >> 2, r = fh & 3u;
 		const uint64_t m1 = __builtin_amdgcn_ballot_w64(q == 1);
 		const uint64_t m2 = __builtin_amdgcn_ballot_w64(q == 2);
@@ -432,8 +455,8 @@ static __device__ __forceinline__ void rx_frame(const RxArgs &a, uint32_t *st, c
 		for (int i = 0; i < 13; i++)
 			hdr[i] = __builtin_amdgcn_alignbyte(sh[i + 1], sh[i], r);
 	} else {
-		/* Wide groups: through a per-frame LDS stage, read back in one
-		 * batch of 14 dwords (no read waits on another). */
+		/* G == 32 (two rows): through a per-frame LDS stage, read back in
+		 * one batch of 14 dwords (no read waits on another). */
 #pragma unroll
 		for (int k = 0; k < K; k++) {
 			const uint32_t c = lane + k * G;
@@ -577,7 +600,7 @@ static __device__ __forceinline__ void rx_frame(const RxArgs &a, uint32_t *st, c
 	if (lane == 0 && present && r.status == XCSUM_RX_OK)
 		delivered++;
 
-	if (G > 4) {
+	if (!XL) {
 		/* the stage is rewritten next iteration: reads first */
 		__builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
 		__builtin_amdgcn_wave_barrier();
@@ -598,7 +621,7 @@ __global__ void __launch_bounds__(256) rx_kernel(RxArgs a)
 {
 	/* per-frame header stage: STAGE_CHUNKS chunks + one dword of slack */
 	constexpr uint32_t SW = STAGE_CHUNKS * 4 + 4;   /* dwords per group */
-	__shared__ __attribute__((aligned(16))) uint32_t stage[G > 4 ? (256 / G) * SW : 4];
+	__shared__ __attribute__((aligned(16))) uint32_t stage[G == 32 ? (256 / G) * SW : 4];
 	const uint32_t lane = threadIdx.x & (G - 1);
 	const uint32_t grp = threadIdx.x / G;
 	uint32_t *st = stage + grp * SW;
