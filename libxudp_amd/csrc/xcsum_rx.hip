@@ -739,7 +739,7 @@ static hipError_t launch_rx_t(const RxArgs &a, int cus, hipStream_t s)
 
 #define XCSUM_RX_GEOMETRIES(X) \
 	X(2, 4, 1) X(2, 4, 2) X(4, 2, 1) X(4, 2, 2) X(8, 1, 2) X(8, 2, 1) \
-	X(16, 2, 1) X(16, 3, 1) X(16, 6, 1) X(64, 9, 1)
+	X(16, 2, 1) X(16, 3, 1) X(16, 6, 1) X(16, 6, 2) X(64, 9, 1)
 
 hipError_t launch_rx(const RxArgs &a, uint32_t len_hint, int cus, hipStream_t s)
 {
@@ -760,7 +760,7 @@ hipError_t launch_rx(const RxArgs &a, uint32_t len_hint, int cus, hipStream_t s)
 		else if (chunks <= 16) { G = 8; K = 2; }
 		else if (chunks <= 32) { G = 16; K = 2; }
 		else if (chunks <= 48) { G = 16; K = 3; }
-		else if (chunks <= 96) { G = 16; K = 6; }
+		else if (chunks <= 96) { G = 16; K = 6; U = 2; }
 		else { G = 64; K = 9; }
 	}
 #define X(g_, k_, u_) \
