@@ -214,10 +214,17 @@ static __device__ __forceinline__ uint32_t bswap16(uint32_t x)
 }
 
 /* header bytes + descriptor + result for one built frame (s = payload sum,
- * in every lane of the segment) */
+ * in every lane of the segment).  The header is written as the four 16-byte
+ * pieces of [data - 64, data) (data is 16-byte aligned): piece i comes from
+ * the batch's header image in LDS (template right-aligned at byte 64 - hdr),
+ * the per-frame length and check halfwords are patched in at their static
+ * positions, and lanes 0..3 store one piece each -- full pieces with one
+ * 16-byte store, the piece holding the header's first bytes with a short,
+ * (a dword,) and a dwordx2.  (A halfword-per-store loop cost ~10 store
+ * instructions per frame.) */
 template <int G>
 static __device__ __forceinline__ void finish_frame(const BuildArgs &a, const Msg &g, uint32_t p,
-						    uint32_t s, uint32_t lane, const uint16_t *tmpl,
+						    uint32_t s, uint32_t lane, const u32x4 *img,
 						    bool v6, uint32_t hdr, uint32_t sconst,
 						    uint32_t ipconst)
 {
@@ -248,25 +255,34 @@ static __device__ __forceinline__ void finish_frame(const BuildArgs &a, const Ms
 		ip = (ip & 0xffffu) + (ip >> 16);
 		ipcheck = bswap16(~ip & 0xffffu);
 	}
-	uint8_t *eth = g.data - hdr;
-	for (uint32_t j = lane; j < hdr / 2; j += G) {
-		uint32_t h = tmpl[j];
+	if (lane < 4) {
+		u32x4 w = img[lane];
+		/* image byte of header byte b: 64 - hdr + b.  IPv4 (at 22):
+		 * tot_len 38, check 46, udp len 60, udp check 62.  IPv6 (at 2):
+		 * payload_len 20, udp len 60, udp check 62. */
 		if (v6) {
-			if (j == 9 || j == 29)
-				h = bswap16(ulen);                 /* payload_len, udp len */
-			else if (j == 30)
-				h = ucheck;
-		} else {
-			if (j == 8)
-				h = bswap16(20u + ulen);           /* tot_len */
-			else if (j == 12)
-				h = ipcheck;
-			else if (j == 19)
-				h = bswap16(ulen);
-			else if (j == 20)
-				h = ucheck;
+			if (lane == 1)
+				w.y = (w.y & 0xffff0000u) | bswap16(ulen);
+		} else if (lane == 2) {
+			w.y = (w.y & 0x0000ffffu) | (bswap16(20u + ulen) << 16);
+			w.w = (w.w & 0x0000ffffu) | (ipcheck << 16);
 		}
-		*reinterpret_cast<uint16_t *>(eth + 2 * j) = (uint16_t)h;
+		if (lane == 3)
+			w.w = bswap16(ulen) | (ucheck << 16);
+		uint8_t *pb = g.data - 64 + 16 * lane;
+		const uint32_t first = v6 ? 0u : 1u;      /* piece holding header byte 0 */
+		if (lane > first) {
+			*reinterpret_cast<u32x4 *>(pb) = w;
+		} else if (lane == first) {
+			if (v6) {                          /* bytes 2..15 */
+				*reinterpret_cast<uint16_t *>(pb + 2) = (uint16_t)(w.x >> 16);
+				*reinterpret_cast<uint32_t *>(pb + 4) = w.y;
+			} else {                           /* bytes 6..15 */
+				*reinterpret_cast<uint16_t *>(pb + 6) = (uint16_t)(w.y >> 16);
+			}
+			typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+			*reinterpret_cast<u32x2 *>(pb + 8) = u32x2{w.z, w.w};
+		}
 	}
 	if (lane == 0) {
 		struct xcsum_desc d0 = {g.data_off - hdr, hdr + g.len, 0u};
@@ -281,7 +297,7 @@ static __device__ __forceinline__ void finish_frame(const BuildArgs &a, const Ms
 template <int G, int K, bool TWO>
 static __device__ __forceinline__ void build_msg(const BuildArgs &a, const Msg &gc,
 						 const u32x4 (&vc)[K][TWO ? 2 : 1], uint32_t ic,
-						 uint32_t lane, bool inplace, const uint16_t *tmpl,
+						 uint32_t lane, bool inplace, const u32x4 *img,
 						 bool v6, uint32_t hdr, uint32_t sconst,
 						 uint32_t ipconst)
 {
@@ -311,7 +327,7 @@ static __device__ __forceinline__ void build_msg(const BuildArgs &a, const Msg &
 	/* payload starts 16-aligned (even address): E holds high bytes */
 	uint32_t s = seg_sum<G>((E << 8) + O);
 	if (gc.present)
-		finish_frame<G>(a, gc, ic, s, lane, tmpl, v6, hdr, sconst, ipconst);
+		finish_frame<G>(a, gc, ic, s, lane, img, v6, hdr, sconst, ipconst);
 }
 
 /*
@@ -327,12 +343,19 @@ __global__ void __launch_bounds__(256) build_kernel(BuildArgs a)
 	/* header template as memory-order halfwords; big-endian word j of the
 	 * header is bswap16(tmpl[j]) */
 	__shared__ uint16_t tmpl[32];
-	if (threadIdx.x < 32)
-		tmpl[threadIdx.x] = (uint16_t)(a.tmpl[threadIdx.x / 2] >> (16 * (threadIdx.x & 1)));
-	__syncthreads();
-
+	/* the header image: the template right-aligned in 64 bytes */
+	__shared__ __attribute__((aligned(16))) u32x4 img[4];
 	const bool v6 = a.family == 6;
 	const uint32_t hdr = v6 ? 62u : 42u;
+	if (threadIdx.x < 32)
+		tmpl[threadIdx.x] = (uint16_t)(a.tmpl[threadIdx.x / 2] >> (16 * (threadIdx.x & 1)));
+	if (threadIdx.x < 64) {
+		const uint32_t b = threadIdx.x, pad = 64u - hdr;
+		const uint8_t v = b < pad ? 0u : (uint8_t)(a.tmpl[(b - pad) >> 2] >> (8 * ((b - pad) & 3)));
+		reinterpret_cast<uint8_t *>(img)[b] = v;
+	}
+	__syncthreads();
+
 	/* constant part of the UDP checksum: pseudo-header addresses and the
 	 * ports (header halfwords 13..18 / 11..28), protocol 17 */
 	uint32_t sconst = 17u;
@@ -370,7 +393,7 @@ __global__ void __launch_bounds__(256) build_kernel(BuildArgs a)
 		d = msg(ia2);
 		__builtin_amdgcn_sched_barrier(0);
 		issue_blocks<G, K, TWO>(gb, lane, vb);
-		build_msg<G, K, TWO>(a, ga, va, ia, lane, inplace, tmpl, v6, hdr, sconst, ipconst);
+		build_msg<G, K, TWO>(a, ga, va, ia, lane, inplace, img, v6, hdr, sconst, ipconst);
 
 		ga = resolve_msg(a, d, ia2 < a.n, inplace);
 		ia = ia2;
@@ -378,7 +401,7 @@ __global__ void __launch_bounds__(256) build_kernel(BuildArgs a)
 		d = msg(ib2);
 		__builtin_amdgcn_sched_barrier(0);
 		issue_blocks<G, K, TWO>(ga, lane, va);
-		build_msg<G, K, TWO>(a, gb, vb, ib, lane, inplace, tmpl, v6, hdr, sconst, ipconst);
+		build_msg<G, K, TWO>(a, gb, vb, ib, lane, inplace, img, v6, hdr, sconst, ipconst);
 		ib = ib2;
 	}
 }
