@@ -436,13 +436,13 @@ static __device__ __forceinline__ void rx_frame(const RxArgs &a, uint32_t *st, c
 	if (XL) {
 		/* broadcast the 6 chunks to every lane of the group (no LDS round
 		 * trip), then realign by fh */
-		uint32_t raw[24];
+		/* frame bytes 12..63 start at raw byte fh <= 15: chunks 0..4 */
+		uint32_t raw[20];
 		bcast_chunk<G, K, 0>(vc, raw);
 		bcast_chunk<G, K, 1>(vc, raw);
 		bcast_chunk<G, K, 2>(vc, raw);
 		bcast_chunk<G, K, 3>(vc, raw);
 		bcast_chunk<G, K, 4>(vc, raw);
-		bcast_chunk<G, K, 5>(vc, raw);
 		const uint32_t q = fh >> 2, r = fh & 3u;
 		const uint64_t m1 = __builtin_amdgcn_ballot_w64(q == 1);
 		const uint64_t m2 = __builtin_amdgcn_ballot_w64(q == 2);
