@@ -219,6 +219,15 @@ int xcsum_rx_device(xcsum_ctx *ctx, const uint8_t *d_umem, const struct xcsum_de
 		    uint32_t n, struct xcsum_rx_msg *d_msgs, uint32_t *d_count, uint32_t flags,
 		    uint32_t len_hint, void *stream);
 
+/* Same for received frames in the host UMEM (the AF_XDP RX ring's frames):
+ * frames are staged to the device with chunked, double-buffered
+ * hipMemcpyAsync, or with XCSUM_F_ZEROCOPY read in place over PCIe from a
+ * registered UMEM; the 64-byte records come back into h_msgs.  *h_count (may
+ * be NULL) = number of XCSUM_RX_OK records.  flags: XCSUM_F_VERIFY,
+ * XCSUM_F_IPHDR, XCSUM_F_ZEROCOPY.  Synchronous. */
+int xcsum_rx_host(xcsum_ctx *ctx, const uint8_t *h_umem, const struct xcsum_desc *h_desc,
+		  uint32_t n, struct xcsum_rx_msg *h_msgs, uint32_t *h_count, uint32_t flags);
+
 /* ---- host-resident batch (frames in the AF_XDP UMEM) ----------------------
  * Same semantics with host pointers.  Synchronous.  Frames are moved with
  * chunked, double-buffered hipMemcpyAsync (pinned when the UMEM range is

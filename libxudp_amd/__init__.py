@@ -101,6 +101,9 @@ _SIGS = {
     "xcsum_batch_host": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                         ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint32,
                                         ctypes.c_uint32]),
+    "xcsum_rx_host": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                     ctypes.c_uint32, ctypes.c_void_p,
+                                     ctypes.POINTER(ctypes.c_uint32), ctypes.c_uint32]),
     "xcsum_register_umem": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t]),
     "xcsum_unregister_umem": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
     "xcsum_sync": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
@@ -270,6 +273,14 @@ class Engine:
     def batch_host(self, umem, desc, out, mode, flags=0):
         _check(lib().xcsum_batch_host(self._ctx, _ptr(umem), _ptr(desc), len(desc), _ptr(out),
                                       mode, flags), "xcsum_batch_host")
+
+    def rx_host(self, umem, desc, msgs, flags=0):
+        """Receive batch on host frames; fills msgs (RX_MSG_DTYPE), returns
+        the number of XCSUM_RX_OK records."""
+        count = ctypes.c_uint32(0)
+        _check(lib().xcsum_rx_host(self._ctx, _ptr(umem), _ptr(desc), len(desc), _ptr(msgs),
+                                   ctypes.byref(count), flags), "xcsum_rx_host")
+        return count.value
 
     def register_umem(self, buf):
         _check(lib().xcsum_register_umem(self._ctx, _ptr(buf), buf.nbytes),

@@ -87,6 +87,8 @@ extern "C" int xcsum_ctx_create(int device, xcsum_ctx **out)
 		c->d_desc[s] = nullptr;
 		c->d_out[s] = nullptr;
 		c->h_out[s] = nullptr;
+		c->d_rx_msgs[s] = nullptr;
+		c->h_rx_msgs[s] = nullptr;
 	}
 	c->frame_cap = 0;
 	c->desc_cap = 0;
@@ -106,6 +108,10 @@ static void free_staging(xcsum_ctx *c)
 		if (c->d_desc[s]) (void)hipFree(c->d_desc[s]);
 		if (c->d_out[s]) (void)hipFree(c->d_out[s]);
 		if (c->h_out[s]) (void)hipHostFree(c->h_out[s]);
+		if (c->d_rx_msgs[s]) (void)hipFree(c->d_rx_msgs[s]);
+		if (c->h_rx_msgs[s]) (void)hipHostFree(c->h_rx_msgs[s]);
+		c->d_rx_msgs[s] = nullptr;
+		c->h_rx_msgs[s] = nullptr;
 		c->streams[s] = nullptr;
 		c->done[s] = nullptr;
 		c->d_frames[s] = nullptr;
@@ -574,6 +580,120 @@ extern "C" int xcsum_batch_host(xcsum_ctx *c, uint8_t *h_umem, const struct xcsu
 				uint32_t n, uint16_t *h_out, uint32_t mode, uint32_t flags)
 {
 	return batch_host_impl(c, h_umem, h_desc, n, h_out, nullptr, mode, flags);
+}
+
+/* Receive batch on host-resident frames: the chunking of batch_host_impl
+ * (<= desc_cap frames, <= frame_cap bytes of UMEM per chunk, two slots in
+ * flight), the receive kernel per chunk, records back through pinned
+ * staging.  Record addresses are UMEM offsets, as from xcsum_rx_device: the
+ * staged copy's base is handed to the kernel biased by the chunk's offset. */
+extern "C" int xcsum_rx_host(xcsum_ctx *c, const uint8_t *h_umem, const struct xcsum_desc *h_desc,
+			     uint32_t n, struct xcsum_rx_msg *h_msgs, uint32_t *h_count,
+			     uint32_t flags)
+{
+	if (!c)
+		return -XCSUM_ERR_INVAL;
+	if (h_count)
+		*h_count = 0;
+	if (n == 0)
+		return 0;
+	if (!h_umem || !h_desc || !h_msgs || ((uintptr_t)h_umem & 3u))
+		return -XCSUM_ERR_INVAL;
+	HIPCHK(hipSetDevice(c->device));
+	int rc = ensure_staging(c);
+	if (rc)
+		return rc;
+	for (int s = 0; s < Ctx::NSLOT; s++) {
+		if (!c->d_rx_msgs[s] &&
+		    hipMalloc(&c->d_rx_msgs[s], c->desc_cap * sizeof(struct xcsum_rx_msg)) != hipSuccess)
+			return -XCSUM_ERR_NOMEM;
+		if (!c->h_rx_msgs[s] &&
+		    hipHostMalloc(&c->h_rx_msgs[s], c->desc_cap * sizeof(struct xcsum_rx_msg), 0) !=
+			    hipSuccess)
+			return -XCSUM_ERR_NOMEM;
+	}
+	const Region *zc = nullptr;
+	if (flags & XCSUM_F_ZEROCOPY) {
+		uint64_t lo = UINT64_MAX, hi = 0;
+		for (uint32_t i = 0; i < n; i++) {
+			if (h_desc[i].addr < lo) lo = h_desc[i].addr;
+			if (h_desc[i].addr + h_desc[i].len > hi) hi = h_desc[i].addr + h_desc[i].len;
+		}
+		zc = find_region(c, h_umem + lo, h_umem + hi);
+		if (!zc || ((uintptr_t)zc->dev & 3u) != ((uintptr_t)zc->host & 3u))
+			return -XCSUM_ERR_NOT_REGISTERED;
+	}
+	Pending pend[Ctx::NSLOT];
+	for (int s = 0; s < Ctx::NSLOT; s++)
+		pend[s].busy = false;
+	uint32_t delivered = 0;
+	auto finish = [&](int s) -> int {
+		HIPCHK(hipEventSynchronize(c->done[s]));
+		memcpy(h_msgs + pend[s].first, c->h_rx_msgs[s],
+		       (size_t)pend[s].count * sizeof(struct xcsum_rx_msg));
+		for (uint32_t k = 0; k < pend[s].count; k++)
+			delivered += c->h_rx_msgs[s][k].status == XCSUM_RX_OK;
+		pend[s].busy = false;
+		return 0;
+	};
+	uint32_t i = 0;
+	int slot = 0;
+	while (i < n) {
+		uint64_t lo = h_desc[i].addr, hi = h_desc[i].addr + h_desc[i].len;
+		if (!zc && hi - lo > c->frame_cap)
+			return -XCSUM_ERR_INVAL;
+		uint32_t cnt = 1;
+		while (i + cnt < n && cnt < c->desc_cap) {
+			const struct xcsum_desc &d = h_desc[i + cnt];
+			uint64_t nlo = d.addr < lo ? d.addr : lo;
+			uint64_t nhi = d.addr + d.len > hi ? d.addr + d.len : hi;
+			if (!zc && nhi - nlo > c->frame_cap)
+				break;
+			lo = nlo;
+			hi = nhi;
+			cnt++;
+		}
+		if (pend[slot].busy && (rc = finish(slot)))
+			return rc;
+		hipStream_t st = c->streams[slot];
+		RxArgs a;
+		if (zc) {
+			a.umem = zc->dev + (h_umem - zc->host);
+		} else {
+			/* 16-byte aligned copy of [lo, hi): every frame keeps its
+			 * address phase; the kernel sees umem + addr inside it */
+			const uint64_t alo = lo & ~(uint64_t)15;
+			HIPCHK(hipMemcpyAsync(c->d_frames[slot], h_umem + alo, hi - alo,
+					      hipMemcpyHostToDevice, st));
+			a.umem = (const uint8_t *)((uintptr_t)c->d_frames[slot] - (uintptr_t)alo);
+		}
+		HIPCHK(hipMemcpyAsync(c->d_desc[slot], h_desc + i, cnt * sizeof(struct xcsum_desc),
+				      hipMemcpyHostToDevice, st));
+		a.desc = c->d_desc[slot];
+		a.n = cnt;
+		a.flags = flags & (XCSUM_F_VERIFY | XCSUM_F_IPHDR);
+		a.msgs = c->d_rx_msgs[slot];
+		a.count = nullptr;
+		a.part = c->d_rx_part;
+		HIPCHK(launch_rx(a, (uint32_t)((hi - lo) / cnt), c->cus, st));
+		HIPCHK(hipMemcpyAsync(c->h_rx_msgs[slot], c->d_rx_msgs[slot],
+				      (size_t)cnt * sizeof(struct xcsum_rx_msg), hipMemcpyDeviceToHost,
+				      st));
+		HIPCHK(hipEventRecord(c->done[slot], st));
+		pend[slot].first = i;
+		pend[slot].count = cnt;
+		pend[slot].busy = true;
+		i += cnt;
+		slot = (slot + 1) % Ctx::NSLOT;
+	}
+	for (int k = 0; k < Ctx::NSLOT; k++) {
+		const int s = (slot + k) % Ctx::NSLOT;
+		if (pend[s].busy && (rc = finish(s)))
+			return rc;
+	}
+	if (h_count)
+		*h_count = delivered;
+	return 0;
 }
 
 /* ---- synthetic frames ---------------------------------------------------- */

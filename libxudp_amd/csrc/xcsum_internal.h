@@ -135,6 +135,8 @@ struct Ctx {
 	struct xcsum_desc *d_desc[NSLOT];
 	uint16_t *d_out[NSLOT];
 	uint16_t *h_out[NSLOT];        /* pinned */
+	struct xcsum_rx_msg *d_rx_msgs[NSLOT];  /* receive records (lazy) */
+	struct xcsum_rx_msg *h_rx_msgs[NSLOT];  /* pinned */
 	size_t frame_cap;              /* bytes per slot */
 	uint32_t desc_cap;             /* frames per slot */
 };

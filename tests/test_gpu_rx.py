@@ -143,3 +143,43 @@ def test_rx_round_trip_full_size(torch_cuda, engine, cid):
     recs = d_msgs.cpu().numpy().view(X.RX_MSG_DTYPE)
     assert int(d_count.item()) == 0
     assert (recs["status"] == X.RX_CSUM).all()
+
+
+@pytest.mark.parametrize("zerocopy", [False, True])
+def test_rx_host_vs_oracle(torch_cuda, engine, zerocopy):
+    """xcsum_rx_host on host-resident frames (staged copies, or zero-copy from
+    a registered UMEM): the same records as the oracle, > 65,536 frames so the
+    batch is cut into several chunks over both staging slots."""
+    frames = []
+    for seed in (4, 5):
+        frames += [f for f, _ in rx_frames.corpus(seed=seed)]
+    rng = np.random.default_rng(9)
+    frames = [frames[i] for i in rng.integers(0, len(frames), 70000)]
+    umem, offs, lens = rx_frames.layout(frames, rng)
+    desc = np.zeros(len(frames), dtype=X.DESC_DTYPE)
+    desc["addr"], desc["len"] = offs, lens
+    flags_zc = X.F_ZEROCOPY if zerocopy else 0
+    if zerocopy:
+        engine.register_umem(umem)
+    try:
+        for flags in FLAGS.values():
+            msgs = np.full(len(desc) * 64, 0xA5, dtype=np.uint8).view(X.RX_MSG_DTYPE)
+            count = engine.rx_host(umem, desc, msgs, flags | flags_zc)
+            exp = oracle.rx_batch(umem, desc, flags)
+            assert np.array_equal(msgs.view(np.uint8), exp.view(np.uint8)), flags
+            assert count == int((exp["status"] == X.RX_OK).sum())
+    finally:
+        if zerocopy:
+            engine.unregister_umem(umem)
+
+
+def test_rx_host_errors(engine):
+    umem = np.zeros(4096, dtype=np.uint8)
+    desc = np.zeros(1, dtype=X.DESC_DTYPE)
+    desc["len"] = 64
+    msgs = np.zeros(1, dtype=X.RX_MSG_DTYPE)
+    assert engine.rx_host(umem, desc[:0], msgs[:0], X.F_VERIFY) == 0
+    with pytest.raises(X.XcsumError):   # zero-copy needs a registered UMEM
+        engine.rx_host(umem, desc, msgs, X.F_VERIFY | X.F_ZEROCOPY)
+    assert engine.rx_host(umem, desc, msgs, X.F_VERIFY) == 0
+    assert msgs["status"][0] == X.RX_PARSE

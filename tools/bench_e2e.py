@@ -6,8 +6,9 @@ hipMemcpyAsync H2D -> kernel -> 2-byte results D2H, for
   registered -- UMEM page-locked with xcsum_register_umem (direct DMA),
   zerocopy   -- registered UMEM read in place by the kernel over PCIe,
 and each of them with XCSUM_F_INPLACE (udp->check written into the host
-frames).  Also the raw pinned H2D copy rate for context.  One JSON line per
-variant.  Usage: python tools/bench_e2e.py [--config 2] [--reps 5]"""
+frames); then the receive side, xcsum_rx_host with VERIFY on the same frames
+(checksums written in first), in the same three variants.  Also the raw
+pinned H2D copy rate for context.  One JSON line per variant.  Usage: python tools/bench_e2e.py [--config 2] [--reps 5]"""
 import argparse
 import json
 import os
@@ -70,9 +71,6 @@ def main():
             if variant != "pageable":
                 eng.unregister_umem(umem)
             if inplace:  # restore check fields for the next variant
-                off = 60 if cfg["family"] == 6 else 40
-                for d in desc[:0]:
-                    pass
                 umem2, _ = X.gen_frames_host(n, cfg["family"], cfg["pmin"], cfg["pmax"],
                                              seed=bench.SEED_BASE ^ args.config)
                 umem[:] = umem2
@@ -81,6 +79,30 @@ def main():
                               "GiBps_alg": round(alg / dt / 2**30, 1),
                               "GBps_frames": round(umem.nbytes / dt / 1e9, 1),
                               "mpps": round(n / dt / 1e6, 1), "parity": ok}), flush=True)
+
+    # receive side: the same frames with valid checksums written in
+    # (RFC rules, IPv4 header too), verified by xcsum_rx_host
+    rfc = X.MODE_V6 if cfg["family"] == 6 else X.MODE_V4_RFC
+    eng.batch_host(umem, desc, out, rfc, X.F_INPLACE | X.F_IPHDR)
+    msgs = np.zeros(n, dtype=X.RX_MSG_DTYPE)
+    flags_rx = X.F_VERIFY | X.F_IPHDR
+    exp_rx = oracle.rx_batch(umem, desc, flags_rx)
+    for variant in ("pageable", "registered", "zerocopy"):
+        flags = flags_rx | (X.F_ZEROCOPY if variant == "zerocopy" else 0)
+        if variant != "pageable":
+            eng.register_umem(umem)
+        cnt = eng.rx_host(umem, desc, msgs, flags)  # warm-up
+        ok = bool(np.array_equal(msgs.view(np.uint8), exp_rx.view(np.uint8))) and cnt == n
+        t0 = time.perf_counter()
+        for _ in range(args.reps):
+            eng.rx_host(umem, desc, msgs, flags)
+        dt = (time.perf_counter() - t0) / args.reps
+        if variant != "pageable":
+            eng.unregister_umem(umem)
+        print(json.dumps({"variant": "rx_" + variant, "verify": True, "frames": n,
+                          "ms": round(dt * 1e3, 3),
+                          "GBps_frames": round(umem.nbytes / dt / 1e9, 1),
+                          "mpps": round(n / dt / 1e6, 1), "parity": ok}), flush=True)
     eng.close()
 
 
