@@ -93,6 +93,32 @@ static void check_batches(xcsum_ctx *c, uint32_t family, uint32_t stride, uint32
 	CHECK(bad == 0, "in-place udp->check v%u: %u wrong", family, bad);
 	CHECK(xcsum_unregister_umem(c, umem) == 0, "unregister_umem");
 
+	/* receive side on the host frames: write RFC checksums (and the IPv4
+	 * header's), then every frame must parse and verify; one flipped
+	 * payload byte fails exactly that frame */
+	const uint32_t rfc = family == 6 ? XCSUM_MODE_V6 : XCSUM_MODE_V4_RFC;
+	for (uint32_t i = 0; i < n; i++)   /* the pass above wrote udp->check */
+		memset(umem + desc[i].addr + (family == 6 ? 60 : 40), 0, 2);
+	CHECK(xcsum_batch_host(c, umem, desc, n, got, rfc, XCSUM_F_INPLACE | XCSUM_F_IPHDR) == 0,
+	      "batch_host rfc in place");
+	struct xcsum_rx_msg *msgs = calloc(n, sizeof(*msgs));
+	uint32_t count = 0;
+	const uint32_t hdr = family == 6 ? 62 : 42;
+	CHECK(xcsum_rx_host(c, umem, desc, n, msgs, &count, XCSUM_F_VERIFY | XCSUM_F_IPHDR) == 0,
+	      "rx_host");
+	CHECK(count == n, "rx_host v%u: %u of %u delivered", family, count, n);
+	bad = 0;
+	for (uint32_t i = 0; i < n; i++)
+		bad += msgs[i].status != XCSUM_RX_OK || msgs[i].family != family ||
+		       msgs[i].frame != desc[i].addr || msgs[i].body != desc[i].addr + hdr ||
+		       msgs[i].size != desc[i].len - hdr;
+	CHECK(bad == 0, "rx_host v%u: %u wrong records", family, bad);
+	umem[desc[n / 2].addr + desc[n / 2].len - 1] ^= 0x40;
+	CHECK(xcsum_rx_host(c, umem, desc, n, msgs, &count, XCSUM_F_VERIFY) == 0, "rx_host 2");
+	CHECK(count == n - 1 && msgs[n / 2].status == XCSUM_RX_CSUM, "rx_host v%u: corrupted frame",
+	      family);
+	free(msgs);
+
 	/* device-resident: the frames as xudp would have them in HBM */
 	uint8_t *d_umem = NULL;
 	struct xcsum_desc *d_desc = NULL;
