@@ -71,6 +71,9 @@ struct Frame {
 	int mode;               /* 0 legacy, 1 rfc, 2 v6, -1 malformed, -2 absent */
 	uint32_t ck;            /* VERIFY: the frame's udp->check (raw 16 bits),
 				   loaded a pipeline step ahead */
+	uint32_t ih[6];         /* IPHDR: the dwords holding the IPv4 header
+				   [eth+14, eth+34), loaded a step ahead */
+	uint32_t ihs;           /* byte phase of eth+14 in ih[0] */
 };
 
 typedef __attribute__((address_space(1))) const u32x4 gu32x4;
@@ -131,7 +134,7 @@ static __device__ __forceinline__ u32x4 load_desc(const CsumArgs &a, uint32_t p)
 	return *((gu32x4 *)(a.desc + q));
 }
 
-template <bool DW>
+template <bool DW, bool IPH>
 static __device__ __forceinline__ Frame resolve(const CsumArgs &a, u32x4 d, bool present)
 {
 	Frame f;
@@ -183,6 +186,16 @@ static __device__ __forceinline__ Frame resolve(const CsumArgs &a, u32x4 d, bool
 	if (a.flags & XCSUM_F_VERIFY)   /* wave-uniform: no load otherwise */
 		f.ck = *(const uint16_t *)(f.nchunks ? f.eth + (mode == 2 ? 60 : 40)
 						     : (const uint8_t *)g_zero_chunk);
+	/* IPHDR: the IPv4 header too (six dwords, same reasoning) */
+	if (IPH && (a.flags & XCSUM_F_IPHDR)) {
+		const uint8_t *ih = f.nchunks && mode != 2 ? f.eth + 14
+							   : (const uint8_t *)g_zero_chunk;
+		f.ihs = (uint32_t)(uintptr_t)ih & 3u;
+		const uint32_t *w = (const uint32_t *)((uintptr_t)ih & ~(uintptr_t)3);
+#pragma unroll
+		for (int j = 0; j < 6; j++)
+			f.ih[j] = w[j];
+	}
 	return f;
 }
 
@@ -406,7 +419,7 @@ static __device__ __forceinline__ void store_u16(uint8_t *p, uint16_t v)
  * iph_build() writes (ihl is always 5 there, packet.c:21, and the
  * frame-layout contract of xcsum.h) -- or, to VERIFY a received header, with
  * the check field included (0 = valid).  Returns the memory-order value. */
-static __device__ uint16_t ip_header_csum(const uint8_t *iph, bool verify)
+static __device__ uint16_t ip_header_csum_mem(const uint8_t *iph, bool verify)
 {
 	uint32_t sum = 0;
 #pragma unroll
@@ -418,6 +431,37 @@ static __device__ uint16_t ip_header_csum(const uint8_t *iph, bool verify)
 	return bswap16(~sum & 0xffffu);
 }
 
+/* IPH: from the dwords resolve() prefetched; else from memory (a dependent
+ * round trip -- the kernels are instantiated with IPH whenever IPHDR is set,
+ * the fallback only keeps results independent of the instantiation) */
+template <bool IPH>
+static __device__ uint16_t ip_header_csum(const Frame &f, bool verify)
+{
+	if (!IPH)
+		return ip_header_csum_mem(f.eth + 14, verify);
+	/* the header from the dwords resolve() prefetched, opaque until here
+	 * (or the compiler computes on them early and waits for the loads) */
+	uint32_t w[6];
+#pragma unroll
+	for (int j = 0; j < 6; j++) {
+		w[j] = f.ih[j];
+		asm volatile("" : "+v"(w[j]));
+	}
+	uint32_t sum = 0;
+#pragma unroll
+	for (int j = 0; j < 5; j++) {
+		/* header bytes 4j..4j+3, little-endian; BE words = 256*even + odd */
+		const uint32_t d = __builtin_amdgcn_alignbyte(w[j + 1], w[j], f.ihs);
+		sum += (dot_even(d, 0u) << 8) + dot_odd(d, 0u);
+		if (j == 2 && !verify)   /* bytes 10-11: the check field itself */
+			sum -= ((d >> 8) & 0xff00u) | (d >> 24);
+	}
+	sum = (sum & 0xffffu) + (sum >> 16);
+	sum = (sum & 0xffffu) + (sum >> 16);
+	return bswap16(~sum & 0xffffu);
+}
+
+template <bool IPH>
 static __device__ __forceinline__ void finalize(const CsumArgs &a, const Frame &f, uint32_t p,
 						uint32_t s)
 {
@@ -439,7 +483,7 @@ static __device__ __forceinline__ void finalize(const CsumArgs &a, const Frame &
 				r = f.mode == 2 ? 0xffffu : 0u;
 			wire = bswap16(r);
 			if ((a.flags & XCSUM_F_IPHDR) && f.mode != 2) {
-				uint16_t ipr = ip_header_csum(f.eth + 14, true);
+				uint16_t ipr = ip_header_csum<IPH>(f, true);
 				if (a.out_ip)
 					a.out_ip[p] = ipr;
 				if (wire == 0)
@@ -463,7 +507,7 @@ static __device__ __forceinline__ void finalize(const CsumArgs &a, const Frame &
 		if (a.flags & XCSUM_F_INPLACE)
 			store_u16(f.eth + (f.mode == 2 ? 60 : 40), wire);
 		if ((a.flags & XCSUM_F_IPHDR) && f.mode != 2) {
-			uint16_t ipc = ip_header_csum(f.eth + 14, false);
+			uint16_t ipc = ip_header_csum<IPH>(f, false);
 			if (a.flags & XCSUM_F_INPLACE)
 				store_u16(f.eth + 24, ipc);
 			if (a.out_ip)
@@ -501,7 +545,7 @@ static __device__ __forceinline__ uint32_t fidx(const CsumArgs &a, uint32_t p)
 	return ORD ? frame_of(a.ord, p) : p;
 }
 
-template <int G, int U, int K, bool TAIL, bool ORD>
+template <int G, int U, int K, bool TAIL, bool ORD, bool IPH>
 static __device__ __forceinline__ void consume(const CsumArgs &a, const Frame (&fc)[U],
 					       const u32x4 (&vc)[U][K], uint32_t lane,
 					       uint32_t p0, uint32_t nseg)
@@ -517,7 +561,7 @@ static __device__ __forceinline__ void consume(const CsumArgs &a, const Frame (&
 		uint32_t s = f.odd ? (O << 8) + E : (E << 8) + O;
 		s = seg_sum<G>(s);
 		if (lane == 0 && f.mode != -2)
-			finalize(a, f, fidx<ORD>(a, p0 + u * nseg), s);
+			finalize<IPH>(a, f, fidx<ORD>(a, p0 + u * nseg), s);
 	}
 }
 
@@ -529,7 +573,7 @@ static __device__ __forceinline__ void consume(const CsumArgs &a, const Frame (&
 
 /* wave-uniform split: the jumbo path lives in its own copy of the body, so
  * its drains never merge into the common path's vmcnt bookkeeping */
-template <int G, int U, int K, bool ORD>
+template <int G, int U, int K, bool ORD, bool IPH>
 static __device__ __forceinline__ void consume_any(const CsumArgs &a, const Frame (&fc)[U],
 						   const u32x4 (&vc)[U][K], uint32_t lane,
 						   uint32_t p0, uint32_t nseg)
@@ -539,9 +583,9 @@ static __device__ __forceinline__ void consume_any(const CsumArgs &a, const Fram
 	for (int u = 0; u < U; u++)
 		big |= fc[u].nchunks > K * G;
 	if (__builtin_amdgcn_ballot_w64(big))
-		consume<G, U, K, true, ORD>(a, fc, vc, lane, p0, nseg);
+		consume<G, U, K, true, ORD, IPH>(a, fc, vc, lane, p0, nseg);
 	else
-		consume<G, U, K, false, ORD>(a, fc, vc, lane, p0, nseg);
+		consume<G, U, K, false, ORD, IPH>(a, fc, vc, lane, p0, nseg);
 }
 
 /*
@@ -555,7 +599,7 @@ static __device__ __forceinline__ void consume_any(const CsumArgs &a, const Fram
  * at the loop latch, that copy needs the next step's loads to have landed,
  * and the ISA showed a vmcnt(0) there -- one step in flight, not two.
  */
-template <int G, int U, int K, bool ORD>
+template <int G, int U, int K, bool ORD, bool IPH>
 static __device__ __forceinline__ void csum_loop(const CsumArgs &a)
 {
 	const uint32_t lane = threadIdx.x & (G - 1);
@@ -577,7 +621,7 @@ static __device__ __forceinline__ void csum_loop(const CsumArgs &a)
 		d[u] = load_desc<G == 64>(a, fidx<ORD>(a, seg + u * nseg));
 #pragma unroll
 	for (int u = 0; u < U; u++)
-		fa[u] = resolve<Grid<G, K>::DW>(a, d[u], has(seg + u * nseg));
+		fa[u] = resolve<Grid<G, K>::DW, IPH>(a, d[u], has(seg + u * nseg));
 #pragma unroll
 	for (int u = 0; u < U; u++)
 		d[u] = load_desc<G == 64>(a, fidx<ORD>(a, seg + step + u * nseg));
@@ -593,24 +637,24 @@ static __device__ __forceinline__ void csum_loop(const CsumArgs &a)
 	for (uint32_t p0 = seg; p0 < limit; p0 += 2 * step) {
 #pragma unroll
 		for (int u = 0; u < U; u++)
-			fb[u] = resolve<Grid<G, K>::DW>(a, d[u], has(p0 + step + u * nseg));
+			fb[u] = resolve<Grid<G, K>::DW, IPH>(a, d[u], has(p0 + step + u * nseg));
 #pragma unroll
 		for (int u = 0; u < U; u++)
 			d[u] = load_desc<G == 64>(a, fidx<ORD>(a, p0 + 2 * step + u * nseg));
 		__builtin_amdgcn_sched_barrier(0);
 		issue<G, U, K>(fb, lane, vb);
-		consume_any<G, U, K, ORD>(a, fa, va, lane, p0, nseg);
+		consume_any<G, U, K, ORD, IPH>(a, fa, va, lane, p0, nseg);
 
 #pragma unroll
 		for (int u = 0; u < U; u++)
-			fa[u] = resolve<Grid<G, K>::DW>(a, d[u],
+			fa[u] = resolve<Grid<G, K>::DW, IPH>(a, d[u],
 							has(p0 + 2 * step + u * nseg));
 #pragma unroll
 		for (int u = 0; u < U; u++)
 			d[u] = load_desc<G == 64>(a, fidx<ORD>(a, p0 + 3 * step + u * nseg));
 		__builtin_amdgcn_sched_barrier(0);
 		issue<G, U, K>(fa, lane, va);
-		consume_any<G, U, K, ORD>(a, fb, vb, lane, p0 + step, nseg);
+		consume_any<G, U, K, ORD, IPH>(a, fb, vb, lane, p0 + step, nseg);
 	}
 #else
 	for (uint32_t p0 = seg; p0 < limit; p0 += step) {
@@ -618,13 +662,13 @@ static __device__ __forceinline__ void csum_loop(const CsumArgs &a)
 		u32x4 vn[U][K];
 #pragma unroll
 		for (int u = 0; u < U; u++)
-			fn[u] = resolve<Grid<G, K>::DW>(a, d[u], has(p0 + step + u * nseg));
+			fn[u] = resolve<Grid<G, K>::DW, IPH>(a, d[u], has(p0 + step + u * nseg));
 #pragma unroll
 		for (int u = 0; u < U; u++)
 			d[u] = load_desc<G == 64>(a, fidx<ORD>(a, p0 + 2 * step + u * nseg));
 		__builtin_amdgcn_sched_barrier(0);
 		issue<G, U, K>(fn, lane, vn);
-		consume_any<G, U, K, ORD>(a, fa, va, lane, p0, nseg);
+		consume_any<G, U, K, ORD, IPH>(a, fa, va, lane, p0, nseg);
 #pragma unroll
 		for (int u = 0; u < U; u++) {
 			fa[u] = fn[u];
@@ -639,14 +683,14 @@ static __device__ __forceinline__ void csum_loop(const CsumArgs &a)
 /* The identity order gets its own copy of the loop, so descriptor-order
  * batches pay nothing for the region order; which copy runs is decided once
  * per launch (uniform branch, after resolve_order). */
-template <int G, int U, int K>
+template <int G, int U, int K, bool IPH>
 __global__ void __launch_bounds__(256) csum_kernel(CsumArgs a)
 {
 	resolve_order(a);
 	if (a.ord.rshift == 0)
-		csum_loop<G, U, K, false>(a);
+		csum_loop<G, U, K, false, IPH>(a);
 	else
-		csum_loop<G, U, K, true>(a);
+		csum_loop<G, U, K, true, IPH>(a);
 }
 
 /* ---- LDS-staged variant ---------------------------------------------------
@@ -697,7 +741,7 @@ __global__ void __launch_bounds__(256) csum_lds_kernel(CsumArgs a)
 		uint32_t f = frame0(j);
 		u32x4 d = pick(load_desc_scalar(a, f), load_desc_scalar(a, f + 1),
 			       load_desc_scalar(a, f + 2), load_desc_scalar(a, f + 3));
-		return resolve<Grid<G, K>::DW>(a, d, f + sub < a.n);
+		return resolve<Grid<G, K>::DW, true>(a, d, f + sub < a.n);
 	};
 	auto issue_stage = [&](const Frame &f, int slot) {
 #pragma unroll
@@ -748,7 +792,7 @@ __global__ void __launch_bounds__(256) csum_lds_kernel(CsumArgs a)
 			uint32_t sum = f.odd ? (O << 8) + E : (E << 8) + O;
 			sum = seg_sum<G>(sum);
 			if (lane == 0 && f.mode != -2)
-				finalize(a, f, frame0(j) + sub, sum);
+				finalize<true>(a, f, frame0(j) + sub, sum);
 			fs[d] = fn;
 		}
 	}
@@ -806,7 +850,7 @@ Geometry pick_geometry(uint32_t len_hint)
 	return Geometry{64, 1, 9, 2};          /* jumbo / mixed up to 9 KB: 6.2 TB/s */
 }
 
-template <int G, int U, int K>
+template <int G, int U, int K, bool IPH>
 static hipError_t launch_t(const CsumArgs &a, int cus, int bpc, hipStream_t s)
 {
 	/* persistent grid: at most what the device keeps resident, so no second
@@ -814,7 +858,7 @@ static hipError_t launch_t(const CsumArgs &a, int cus, int bpc, hipStream_t s)
 	static int occ = 0;
 	if (!occ) {
 		int nb = 0;
-		if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, csum_kernel<G, U, K>, 256, 0) !=
+		if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, csum_kernel<G, U, K, IPH>, 256, 0) !=
 			    hipSuccess || nb <= 0)
 			nb = 4;
 		occ = nb;
@@ -827,7 +871,7 @@ static hipError_t launch_t(const CsumArgs &a, int cus, int bpc, hipStream_t s)
 		blocks = cap;
 	if (blocks == 0)
 		blocks = 1;
-	hipLaunchKernelGGL((csum_kernel<G, U, K>), dim3((unsigned)blocks), dim3(256), 0, s, a);
+	hipLaunchKernelGGL((csum_kernel<G, U, K, IPH>), dim3((unsigned)blocks), dim3(256), 0, s, a);
 	return hipGetLastError();
 }
 
@@ -860,8 +904,12 @@ hipError_t launch_csum(const CsumArgs &a, Geometry g, int cus, hipStream_t s)
 	if (g.G == 16 && g.U == 13 && g.K == 6) return launch_lds_t<6, 3>(b, cus, g.B, s);
 	if (g.G == 16 && g.U == 14 && g.K == 3) return launch_lds_t<3, 4>(b, cus, g.B, s);
 	if (g.G == 16 && g.U == 12 && g.K == 3) return launch_lds_t<3, 2>(b, cus, g.B, s);
-#define X(g_, u_, k_) \
-	if (g.G == g_ && g.U == u_ && g.K == k_) return launch_t<g_, u_, k_>(a, cus, g.B, s);
+	/* IPHDR kernels prefetch the IPv4 header a pipeline step ahead: a
+	 * separate instantiation, so the plain path keeps its registers */
+#define X(g_, u_, k_)                                                                  \
+	if (g.G == g_ && g.U == u_ && g.K == k_)                                        \
+		return (a.flags & XCSUM_F_IPHDR) ? launch_t<g_, u_, k_, true>(a, cus, g.B, s)  \
+						 : launch_t<g_, u_, k_, false>(a, cus, g.B, s);
 	XCSUM_GEOMETRIES(X)
 #undef X
 	return hipErrorInvalidValue;

@@ -32,7 +32,10 @@ def main():
                     help="visiting orders to try, 'R,T;R,T' (log2 regions, log2 tile frames; "
                          "-1,0 = automatic)")
     ap.add_argument("--layout", default="packed", choices=["packed", "umem"])
+    ap.add_argument("--flags", default="", help="comma list of inplace,iphdr,verify,rfc")
     args = ap.parse_args()
+    fl = {"inplace": X.F_INPLACE, "iphdr": X.F_IPHDR, "verify": X.F_VERIFY}
+    flags = sum(fl[f] for f in args.flags.split(",") if f in fl)
     import torch
     dev = torch.device("cuda:0")
     cfg = dict(bench.CONFIGS[args.config], id=args.config, layout=args.layout)
@@ -41,6 +44,9 @@ def main():
     desc, d_desc, bufs, out, first, count = bench.build_batch(cfg, 0, 1, torch, dev, eng,
                                                               s.cuda_stream)
     alg = X.alg_bytes(desc, cfg["family"])
+    mode = cfg["mode"]
+    if "rfc" in args.flags.split(",") and cfg["family"] == 4:
+        mode = X.MODE_V4_RFC
     geoms = GEOMS if not args.geoms else [tuple(int(v) for v in g.split(","))
                                           for g in args.geoms.split(";")]
     bpcs = [int(b) for b in args.bpc.split(",")]
@@ -53,20 +59,21 @@ def main():
             eng.set_launch(b)
             eng.set_order(*o)
             for k in range(3):
-                eng.batch_device(bufs[k % len(bufs)], d_desc, count, out, cfg["mode"],
+                eng.batch_device(bufs[k % len(bufs)], d_desc, count, out, mode, flags,
                                  stream=s.cuda_stream)
             evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
                    for _ in range(args.launches)]
             for k in range(args.launches):
                 evs[k][0].record(s)
-                eng.batch_device(bufs[k % len(bufs)], d_desc, count, out, cfg["mode"],
+                eng.batch_device(bufs[k % len(bufs)], d_desc, count, out, mode, flags,
                                  stream=s.cuda_stream)
                 evs[k][1].record(s)
             torch.cuda.synchronize()
             times[(g, b, o)] += [e0.elapsed_time(e1) for e0, e1 in evs]
     for g, b, o in geoms:
         t = np.array(times[(g, b, o)])
-        print(json.dumps({"config": args.config, "layout": args.layout, "geometry": g, "bpc": b,
+        print(json.dumps({"config": args.config, "layout": args.layout, "flags": args.flags,
+                          "geometry": g, "bpc": b,
                           "order": o, "median_ms": round(float(
             np.median(t)), 4), "min_ms": round(float(t.min()), 4), "GBps_median": round(
             alg / (np.median(t) * 1e-3) / 1e9, 1), "GBps_best": round(alg / (t.min() * 1e-3) / 1e9,
