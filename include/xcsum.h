@@ -243,6 +243,11 @@ int xcsum_batch_host(xcsum_ctx *ctx, uint8_t *h_umem, const struct xcsum_desc *h
 int xcsum_register_umem(xcsum_ctx *ctx, void *base, size_t size);
 int xcsum_unregister_umem(xcsum_ctx *ctx, void *base);
 
+/* Diagnostics (no reference counterpart): the hipError_t of the last HIP call
+ * that made an entry point of this thread return -XCSUM_ERR_HIP (0: none),
+ * with the library source line and the error's name. */
+int xcsum_last_hip_error(int *line, const char **name);
+
 /* Wait for all work the context issued on `stream`. */
 int xcsum_sync(xcsum_ctx *ctx, void *stream);
 

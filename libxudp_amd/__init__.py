@@ -107,6 +107,8 @@ _SIGS = {
     "xcsum_register_umem": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t]),
     "xcsum_unregister_umem": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
     "xcsum_sync": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
+    "xcsum_last_hip_error": (ctypes.c_int, [ctypes.POINTER(ctypes.c_int),
+                                            ctypes.POINTER(ctypes.c_char_p)]),
     "xcsum_gen_layout": (ctypes.c_int, [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
                                         ctypes.c_uint32, ctypes.c_uint64, ctypes.c_uint64,
                                         ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
@@ -146,6 +148,10 @@ def lib():
 
 def _check(rc, what):
     if rc != 0:
+        if ERR_NAMES.get(-rc) == "XCSUM_ERR_HIP":
+            line, name = ctypes.c_int(0), ctypes.c_char_p()
+            code = lib().xcsum_last_hip_error(ctypes.byref(line), ctypes.byref(name))
+            what = f"{what} ({(name.value or b'?').decode()} = {code} at xcsum_api.hip:{line.value})"
         raise XcsumError(rc, what)
     return rc
 

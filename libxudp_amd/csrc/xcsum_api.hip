@@ -15,11 +15,27 @@
 
 using namespace xcsum;
 
-#define HIPCHK(x)                                   \
-	do {                                        \
-		if ((x) != hipSuccess)              \
-			return -XCSUM_ERR_HIP;      \
+/* the last failing HIP call of this thread, for xcsum_last_hip_error() */
+static thread_local int t_hip_err = 0, t_hip_line = 0;
+
+#define HIPCHK(x)                                           \
+	do {                                                \
+		const hipError_t e_ = (x);                  \
+		if (e_ != hipSuccess) {                     \
+			t_hip_err = (int)e_;                \
+			t_hip_line = __LINE__;              \
+			return -XCSUM_ERR_HIP;              \
+		}                                           \
 	} while (0)
+
+extern "C" int xcsum_last_hip_error(int *line, const char **name)
+{
+	if (line)
+		*line = t_hip_line;
+	if (name)
+		*name = t_hip_err ? hipGetErrorName((hipError_t)t_hip_err) : "hipSuccess";
+	return t_hip_err;
+}
 
 /* $XCSUM_GEOMETRY="G,U,K" forces a geometry for every new context (sweeps) */
 static Geometry env_geometry()
