@@ -424,6 +424,8 @@ static hipError_t launch_build_t(const BuildArgs &a, int cus, hipStream_t s)
 		blocks = cap;
 	if (blocks == 0)
 		blocks = 1;
+	(void)hipGetLastError();  /* clear a stale error (e.g. hipErrorNotReady from
+	                           * someone's hipEventQuery) before checking ours */
 	hipLaunchKernelGGL((build_kernel<G, K, TWO>), dim3((unsigned)blocks), dim3(256), 0, s, a);
 	return hipGetLastError();
 }

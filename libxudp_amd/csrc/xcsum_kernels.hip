@@ -821,6 +821,8 @@ static hipError_t launch_lds_t(const CsumArgs &a, int cus, int bpc, hipStream_t 
 		blocks = cap;
 	if (blocks == 0)
 		blocks = 1;
+	(void)hipGetLastError();  /* clear a stale error (e.g. hipErrorNotReady from
+	                           * someone's hipEventQuery) before checking ours */
 	hipLaunchKernelGGL((csum_lds_kernel<K, D>), dim3((unsigned)blocks), dim3(256), lds, s, a);
 	return hipGetLastError();
 }
@@ -871,6 +873,8 @@ static hipError_t launch_t(const CsumArgs &a, int cus, int bpc, hipStream_t s)
 		blocks = cap;
 	if (blocks == 0)
 		blocks = 1;
+	(void)hipGetLastError();  /* clear a stale error (e.g. hipErrorNotReady from
+	                           * someone's hipEventQuery) before checking ours */
 	hipLaunchKernelGGL((csum_kernel<G, U, K, IPH>), dim3((unsigned)blocks), dim3(256), 0, s, a);
 	return hipGetLastError();
 }
@@ -975,6 +979,8 @@ hipError_t launch_gen(uint8_t *d_umem, const struct xcsum_desc *d_desc, uint32_t
 	uint64_t blocks = ((uint64_t)n + 3) / 4;
 	if (blocks > (uint64_t)max_blocks)
 		blocks = max_blocks;
+	(void)hipGetLastError();  /* clear a stale error (e.g. hipErrorNotReady from
+	                           * someone's hipEventQuery) before checking ours */
 	hipLaunchKernelGGL(gen_kernel, dim3((unsigned)blocks), dim3(256), 0, s, d_umem, d_desc, n,
 			   family, seed, first_index);
 	return hipGetLastError();

@@ -730,6 +730,8 @@ static hipError_t launch_rx_t(const RxArgs &a, int cus, hipStream_t s)
 		blocks = RX_PART_MAX;
 	if (blocks == 0)
 		blocks = 1;
+	(void)hipGetLastError();  /* clear a stale error (e.g. hipErrorNotReady from
+	                           * someone's hipEventQuery) before checking ours */
 	hipLaunchKernelGGL((rx_kernel<G, K, U>), dim3((unsigned)blocks), dim3(256), 0, s, a);
 	if (a.count)
 		hipLaunchKernelGGL(rx_count_kernel, dim3(1), dim3(256), 0, s, a.part,

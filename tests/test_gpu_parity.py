@@ -297,3 +297,20 @@ def test_visiting_order_bad_arguments(engine):
     for bad in ((-2, 0), (13, 0), (2, -1), (2, 17)):
         with pytest.raises(X.XcsumError):
             engine.set_order(*bad)
+
+
+def test_launch_ignores_stale_hip_error(torch_cuda, engine, golden):
+    """A pending event query elsewhere in the thread (hipEventQuery ->
+    hipErrorNotReady, which HIP keeps as the thread's last error) must not
+    make the next launch report failure."""
+    torch = torch_cuda
+    x = torch.ones(1 << 27, device="cuda:0")
+    for _ in range(4):
+        x = x * 1.0001
+    ev = torch.cuda.Event()
+    ev.record()
+    ev.query()   # usually not ready yet
+    desc = golden_desc(golden, np.nonzero(golden["family"] == 4)[0][:64])
+    got, _ = run_device(torch, engine, golden["umem"].copy(), desc, X.MODE_V4_LEGACY)
+    assert np.array_equal(got, golden["exp_legacy"][np.nonzero(golden["family"] == 4)[0][:64]])
+    torch.cuda.synchronize()
