@@ -367,9 +367,13 @@ static __device__ __forceinline__ void sum_walk(const Frame &f, uint32_t lane, u
 }
 
 /* the chunk grid a geometry uses (measured, see the Frame comment) */
+/* XCSUM_GRID_DW=1 builds a variant with the dword grid everywhere (A/B only) */
+#ifndef XCSUM_GRID_DW
+#define XCSUM_GRID_DW 0
+#endif
 template <int G, int K>
 struct Grid {
-	static constexpr bool DW = !(G == 16 && K >= 6) && !(G == 8 && K >= 12);
+	static constexpr bool DW = XCSUM_GRID_DW || (!(G == 16 && K >= 6) && !(G == 8 && K >= 12));
 };
 
 /* Sum over each aligned group of G lanes, result in every lane of the group.

@@ -349,25 +349,30 @@ static __device__ __forceinline__ void rx_issue(const RxArgs &a, const RFrame &f
 	}
 }
 
-/* keep the bytes of chunk cb..cb+15 whose address is in [lo, hi) */
-static __device__ __forceinline__ uint64_t low_bytes(int n)
+/* Byte masks of a chunk, from a 17-entry LDS table: SPAN[n] keeps bytes
+ * [0, n) of 16.  keep_span(v, a, b) keeps bytes [a, b) (both clamped to
+ * [0, 16]): two ds_read_b128 and one and-not per dword, where building the
+ * masks with 64-bit shifts took ~55 VALU per edge chunk (the ISA). */
+constexpr uint32_t SPAN_DWORDS = 17 * 4;
+
+static __device__ __forceinline__ void span_init(uint32_t *tab)
 {
-	/* bytes [0, n) of a qword set, n clamped to [0, 8] */
-	return n >= 8 ? ~0ull : (n <= 0 ? 0ull : ~0ull >> (64 - 8 * n));
+	/* called by every thread, then a block barrier */
+	for (uint32_t t = threadIdx.x; t < SPAN_DWORDS; t += blockDim.x) {
+		const int n = (int)(t >> 2) - 4 * (int)(t & 3u);   /* bytes kept of dword t & 3 */
+		tab[t] = n >= 4 ? 0xffffffffu : (n <= 0 ? 0u : 0xffffffffu >> (32 - 8 * n));
+	}
 }
 
-static __device__ __forceinline__ u32x4 keep_span(u32x4 v, int a, int b)
+static __device__ __forceinline__ u32x4 span_mask(const uint32_t *tab, int n)
 {
-	/* a = lo - cb, b = hi - cb */
-	const int ac = a < 0 ? 0 : (a > 16 ? 16 : (int)a);
-	const int bc = b < 0 ? 0 : (b > 16 ? 16 : (int)b);
-	const uint64_t m0 = low_bytes(bc) & ~low_bytes(ac);
-	const uint64_t m1 = low_bytes(bc - 8) & ~low_bytes(ac - 8);
-	v.x &= (uint32_t)m0;
-	v.y &= (uint32_t)(m0 >> 32);
-	v.z &= (uint32_t)m1;
-	v.w &= (uint32_t)(m1 >> 32);
-	return v;
+	n = n < 0 ? 0 : (n > 16 ? 16 : n);
+	return *(const u32x4 *)(tab + 4 * n);
+}
+
+static __device__ __forceinline__ u32x4 keep_span(const uint32_t *tab, u32x4 v, int a, int b)
+{
+	return v & span_mask(tab, b) & ~span_mask(tab, a);
 }
 
 /* a where the lane's bit of `lanes` is clear, b where it is set: v_cndmask
@@ -420,7 +425,8 @@ static __device__ __forceinline__ void bcast_chunk(const u32x4 (&vc)[K], uint32_
 /* Everything for frame p once its chunks v[] have landed: stage, parse,
  * verify, record.  Group-uniform; every lane of the wave must call it. */
 template <int G, int K>
-static __device__ __forceinline__ void rx_frame(const RxArgs &a, uint32_t *st, const RFrame &fc,
+static __device__ __forceinline__ void rx_frame(const RxArgs &a, uint32_t *st, const uint32_t *tab,
+						const RFrame &fc,
 						const u32x4 (&vc)[K], uint32_t p, uint32_t lane,
 						bool verify, bool iphdr, uint32_t &delivered)
 {
@@ -529,17 +535,20 @@ static __device__ __forceinline__ void rx_frame(const RxArgs &a, uint32_t *st, c
 				const int cb = rx_chunk_off(fh, c);
 				u32x4 v = __builtin_nontemporal_load((gu32x4 *)(fc.eth + cb));
 				if (cb < lo || cb + 16 > hi)
-					v = keep_span(v, lo - cb, hi - cb);
+					v = keep_span(tab, v, lo - cb, hi - cb);
 				accum(v, E, O);
 			}
 		} else {
 #pragma unroll
 			for (int k = 0; k < K; k++) {
 				const int cb = rx_chunk_off(fh, lane + k * G);
-				const bool edge = good && (cb < lo || cb + 16 > hi);
+				/* the span's start lies in chunks 0..1 (k == 0) */
+				const bool edge = good && ((k == 0 && cb < lo) || cb + 16 > hi);
 				u32x4 v = vc[k];
 				if (__builtin_amdgcn_ballot_w64(edge))
-					v = edge ? keep_span(v, lo - cb, hi - cb) : v;
+					v = edge ? (k == 0 ? keep_span(tab, v, lo - cb, hi - cb)
+						       : v & span_mask(tab, hi - cb))
+						 : v;
 				accum(v, E, O);
 			}
 		}
@@ -625,6 +634,9 @@ __global__ void __launch_bounds__(256) rx_kernel(RxArgs a)
 	const uint32_t lane = threadIdx.x & (G - 1);
 	const uint32_t grp = threadIdx.x / G;
 	uint32_t *st = stage + grp * SW;
+	__shared__ __attribute__((aligned(16))) uint32_t span[SPAN_DWORDS];
+	span_init(span);
+	__syncthreads();
 	uint32_t seg = (blockIdx.x * 256u + threadIdx.x) / G;
 	const uint32_t nseg = gridDim.x * (256u / G);
 	if (G == 64)
@@ -663,9 +675,13 @@ __global__ void __launch_bounds__(256) rx_kernel(RxArgs a)
 #pragma unroll
 		for (int u = 0; u < U; u++)
 			rx_issue<G, K>(a, fb[u], lane, vb[u]);
+		/* keep the other set's work below its loads: hoisted above them,
+		 * its first use waits for everything in flight (vmcnt(2) in the
+		 * ISA) and the loads go out only after it -- one set in flight */
+		__builtin_amdgcn_sched_barrier(0);
 #pragma unroll
 		for (int u = 0; u < U; u++)
-			rx_frame<G, K>(a, st, fa[u], va[u], p + u * nseg, lane, verify, iphdr,
+			rx_frame<G, K>(a, st, span, fa[u], va[u], p + u * nseg, lane, verify, iphdr,
 				       delivered);
 
 #pragma unroll
@@ -677,9 +693,10 @@ __global__ void __launch_bounds__(256) rx_kernel(RxArgs a)
 #pragma unroll
 		for (int u = 0; u < U; u++)
 			rx_issue<G, K>(a, fa[u], lane, va[u]);
+		__builtin_amdgcn_sched_barrier(0);
 #pragma unroll
 		for (int u = 0; u < U; u++)
-			rx_frame<G, K>(a, st, fb[u], vb[u], p + (U + u) * nseg, lane, verify, iphdr,
+			rx_frame<G, K>(a, st, span, fb[u], vb[u], p + (U + u) * nseg, lane, verify, iphdr,
 				       delivered);
 	}
 	/* The delivered count: one plain store per block, summed by a second
@@ -712,7 +729,7 @@ __global__ void __launch_bounds__(256) rx_count_kernel(const uint32_t *part, uin
 }
 
 template <int G, int K, int U>
-static hipError_t launch_rx_t(const RxArgs &a, int cus, hipStream_t s)
+static hipError_t launch_rx_t(const RxArgs &a, int cus, int bpc, hipStream_t s)
 {
 	static int occ = 0;
 	if (!occ) {
@@ -723,7 +740,7 @@ static hipError_t launch_rx_t(const RxArgs &a, int cus, hipStream_t s)
 		occ = nb;
 	}
 	uint64_t blocks = (((uint64_t)a.n + U - 1) / U * G + 255) / 256;
-	const uint64_t cap = (uint64_t)cus * occ;
+	const uint64_t cap = (uint64_t)cus * ((bpc > 0 && bpc < occ) ? bpc : occ);
 	if (blocks > cap)
 		blocks = cap;
 	if (blocks > RX_PART_MAX)
@@ -747,26 +764,30 @@ hipError_t launch_rx(const RxArgs &a, uint32_t len_hint, int cus, hipStream_t s)
 {
 	if (a.n == 0)
 		return hipSuccess;
-	int G, K, U = 1;
-	const char *e = getenv("XCSUM_RX_GEOMETRY");   /* "G,K[,U]" for sweeps and tests */
-	if (!(e && sscanf(e, "%d,%d,%d", &G, &K, &U) >= 2)) {
+	int G, K, U = 1, B = 0;
+	/* "G,K[,U[,B]]" for sweeps and tests; B = blocks per CU (0: occupancy) */
+	const char *e = getenv("XCSUM_RX_GEOMETRY");
+	if (!(e && sscanf(e, "%d,%d,%d,%d", &G, &K, &U, &B) >= 2)) {
 		U = 1;
+		B = 0;
 		/* chunks of a typical frame from eth+12 to its end: cover it in
 		 * one preload with as few lanes as that allows; without VERIFY
 		 * only the 6-chunk header stage is loaded.  Measured
 		 * (tools/bench_rx.py, profiles/r01/bench_rx_*.log): two frames per
-		 * group per stage pay for their registers only on small frames. */
+		 * group per stage pay for their registers only on small frames;
+		 * MTU frames run best at two waves per SIMD (B = 2), one frame
+		 * per group (profiles/r01/rx_mtu/). */
 		const uint32_t chunks = (len_hint + 6) / 16;  /* ceil((len + 3 - 12) / 16) */
 		if (!(a.flags & XCSUM_F_VERIFY)) { G = 4; K = 2; U = 2; }
 		else if (chunks <= 8) { G = 2; K = 4; U = 2; }
 		else if (chunks <= 16) { G = 8; K = 2; }
 		else if (chunks <= 32) { G = 16; K = 2; }
 		else if (chunks <= 48) { G = 16; K = 3; }
-		else if (chunks <= 96) { G = 16; K = 6; U = 2; }
+		else if (chunks <= 96) { G = 16; K = 6; B = 2; }
 		else { G = 64; K = 9; }
 	}
 #define X(g_, k_, u_) \
-	if (G == g_ && K == k_ && U == u_) return launch_rx_t<g_, k_, u_>(a, cus, s);
+	if (G == g_ && K == k_ && U == u_) return launch_rx_t<g_, k_, u_>(a, cus, B, s);
 	XCSUM_RX_GEOMETRIES(X)
 #undef X
 	return hipErrorInvalidValue;
