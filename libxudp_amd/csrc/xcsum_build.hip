@@ -81,24 +81,23 @@ static __device__ __forceinline__ Msg resolve_msg(const BuildArgs &a, u32x4 m, b
 
 __device__ u32x4 g_zero_block[4];
 
-/* the two aligned 16-byte blocks chunk c of the payload straddles; blocks
- * holding no payload byte load zeros instead (nothing is read past the
- * payload's last aligned block) */
+/* The payload's aligned 16-byte blocks, block c = lane + k*G in v[k]; with
+ * TWO (unaligned sources) also block K*G in lane 0's `vx`: chunk c of the
+ * payload straddles blocks c and c + 1.  Blocks holding no payload byte load
+ * zeros instead (nothing is read past the payload's last aligned block). */
 template <int G, int K, bool TWO>
-static __device__ __forceinline__ void issue_blocks(const Msg &g, uint32_t lane,
-						    u32x4 (&v)[K][TWO ? 2 : 1])
+static __device__ __forceinline__ void issue_blocks(const Msg &g, uint32_t lane, u32x4 (&v)[K],
+						    u32x4 &vx)
 {
 	const uint8_t *zero = (const uint8_t *)g_zero_block;
+	const uint32_t end = g.len + g.sh;          /* block offsets below hold payload */
 #pragma unroll
 	for (int k = 0; k < K; k++) {
-		uint32_t off = 16u * (lane + k * G);
-		bool has = off < g.len;
-		/* second block holds bytes [16 - sh, ...) of the chunk */
-		bool has2 = has && g.sh != 0 && 16u - g.sh < g.len - off;
-		v[k][0] = ld16(has ? g.blk + off : zero);
-		if (TWO)
-			v[k][TWO ? 1 : 0] = ld16(has2 ? g.blk + off + 16 : zero);
+		const uint32_t off = 16u * (lane + k * G);
+		v[k] = ld16(off < end ? g.blk + off : zero);
 	}
+	if (TWO)
+		vx = ld16(lane == 0 && 16u * K * G < end ? g.blk + 16u * K * G : zero);
 }
 
 /* a where the lane's bit of `lanes` is clear, b where it is set: v_cndmask
@@ -292,14 +291,26 @@ static __device__ __forceinline__ void finish_frame(const BuildArgs &a, const Ms
 	}
 }
 
+/* Dwords of the LDS stage per group (TWO): K*G + 1 blocks and one block of
+ * slack for the fifth dword the last chunk reads. */
+template <int G, int K>
+struct Stage {
+	static constexpr uint32_t DW = 4 * (K * G + 2);
+};
+
 /* Copy (unless in place), sum, header and descriptor of one message whose
- * payload blocks v[] have landed.  Group-uniform; every lane calls it. */
+ * payload blocks v[] have landed.  Group-uniform; every lane calls it.
+ * Unaligned sources (TWO) are realigned through the group's LDS stage: the
+ * blocks go in as they are, and chunk c comes back as the five dwords from
+ * byte sh + 16c, byte-shifted with v_alignbyte.  One load and no dword
+ * selects per chunk; loading both straddled blocks and selecting in
+ * registers took two loads, 15 v_cndmask and twice the registers. */
 template <int G, int K, bool TWO>
 static __device__ __forceinline__ void build_msg(const BuildArgs &a, const Msg &gc,
-						 const u32x4 (&vc)[K][TWO ? 2 : 1], uint32_t ic,
+						 const u32x4 (&vc)[K], const u32x4 &vx, uint32_t ic,
 						 uint32_t lane, bool inplace, const u32x4 *img,
 						 bool v6, uint32_t hdr, uint32_t sconst,
-						 uint32_t ipconst)
+						 uint32_t ipconst, uint32_t *st)
 {
 	uint32_t E = 0, O = 0;
 	if (__builtin_amdgcn_ballot_w64(gc.len > 16u * K * G)) {
@@ -310,14 +321,42 @@ static __device__ __forceinline__ void build_msg(const BuildArgs &a, const Msg &
 				store_payload(gc.data + off, v, gc.len - off);
 			accum(v, E, O);
 		}
+	} else if (TWO) {
+		/* the stage was last read by this group's previous message */
+		__builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+		__builtin_amdgcn_wave_barrier();
+		__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+		for (int k = 0; k < K; k++)
+			*((u32x4 *)(st + 4 * (lane + k * G))) = vc[k];
+		if (lane == 0)
+			*((u32x4 *)(st + 4 * K * G)) = vx;
+		__builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+		__builtin_amdgcn_wave_barrier();
+		__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+		const uint32_t s8 = gc.sh & 3u;
+#pragma unroll
+		for (int k = 0; k < K; k++) {
+			const uint32_t off = 16u * (lane + k * G);
+			if (off < gc.len) {
+				const uint32_t *q = st + (gc.sh >> 2) + 4 * (lane + k * G);
+				const uint32_t d0 = q[0], d1 = q[1], d2 = q[2], d3 = q[3], d4 = q[4];
+				u32x4 v = {__builtin_amdgcn_alignbyte(d1, d0, s8),
+					   __builtin_amdgcn_alignbyte(d2, d1, s8),
+					   __builtin_amdgcn_alignbyte(d3, d2, s8),
+					   __builtin_amdgcn_alignbyte(d4, d3, s8)};
+				v = shift_chunk(v, v, 0u, gc.len - off);     /* clear past the end */
+				if (!inplace)
+					store_payload(gc.data + off, v, gc.len - off);
+				accum(v, E, O);
+			}
+		}
 	} else {
 #pragma unroll
 		for (int k = 0; k < K; k++) {
 			uint32_t off = 16u * (lane + k * G);
 			if (off < gc.len) {
-				u32x4 v = TWO ? shift_chunk(vc[k][0], vc[k][TWO ? 1 : 0], gc.sh,
-							    gc.len - off)
-					      : shift_chunk(vc[k][0], vc[k][0], 0u, gc.len - off);
+				u32x4 v = shift_chunk(vc[k], vc[k], 0u, gc.len - off);
 				if (!inplace)
 					store_payload(gc.data + off, v, gc.len - off);
 				accum(v, E, O);
@@ -384,24 +423,30 @@ __global__ void __launch_bounds__(256) build_kernel(BuildArgs a)
 	uint32_t ib = idx(seg + nseg);
 	d = msg(ib);
 	__builtin_amdgcn_sched_barrier(0);
-	u32x4 va[K][TWO ? 2 : 1], vb[K][TWO ? 2 : 1];
-	issue_blocks<G, K, TWO>(ga, lane, va);
+	__shared__ __attribute__((aligned(16))) uint32_t stage[TWO ? (256 / G) * Stage<G, K>::DW : 4];
+	uint32_t *st = stage + (TWO ? (threadIdx.x / G) * Stage<G, K>::DW : 0u);
+	u32x4 va[K], vb[K], xa, xb;
+	issue_blocks<G, K, TWO>(ga, lane, va, xa);
 
 	for (uint32_t p = seg; p < a.ord.nlog; p += 2 * nseg) {
 		Msg gb = resolve_msg(a, d, ib < a.n, inplace);
 		const uint32_t ia2 = idx(p + 2 * nseg);
 		d = msg(ia2);
 		__builtin_amdgcn_sched_barrier(0);
-		issue_blocks<G, K, TWO>(gb, lane, vb);
-		build_msg<G, K, TWO>(a, ga, va, ia, lane, inplace, img, v6, hdr, sconst, ipconst);
+		issue_blocks<G, K, TWO>(gb, lane, vb, xb);
+		__builtin_amdgcn_sched_barrier(0);
+		build_msg<G, K, TWO>(a, ga, va, xa, ia, lane, inplace, img, v6, hdr, sconst, ipconst,
+				     st);
 
 		ga = resolve_msg(a, d, ia2 < a.n, inplace);
 		ia = ia2;
 		const uint32_t ib2 = idx(p + 3 * nseg);
 		d = msg(ib2);
 		__builtin_amdgcn_sched_barrier(0);
-		issue_blocks<G, K, TWO>(ga, lane, va);
-		build_msg<G, K, TWO>(a, gb, vb, ib, lane, inplace, img, v6, hdr, sconst, ipconst);
+		issue_blocks<G, K, TWO>(ga, lane, va, xa);
+		__builtin_amdgcn_sched_barrier(0);
+		build_msg<G, K, TWO>(a, gb, vb, xb, ib, lane, inplace, img, v6, hdr, sconst, ipconst,
+				     st);
 		ib = ib2;
 	}
 }
