@@ -61,3 +61,16 @@ def test_build_argument_validation():
     import ctypes
     assert L.xcsum_build_device(None, ctypes.byref(r), None, None, 1, None, 4096, 384, None,
                                 None, 0, 0, None) == -X.ERR_INVAL
+
+
+# every instantiation of build_kernel (csrc/xcsum_build.hip XCSUM_BUILD_GEOMETRIES);
+# tests/test_gpu_build.py runs each through XCSUM_BUILD_GEOMETRY
+BUILD_GEOMETRIES = [(4, 1), (8, 2), (16, 2), (16, 3), (16, 6), (32, 3), (64, 2), (64, 9)]
+
+
+def test_build_geometry_list_matches_kernel():
+    import re
+    src = open(os.path.join(os.path.dirname(X.__file__), "csrc", "xcsum_build.hip")).read()
+    body = src.split("#define XCSUM_BUILD_GEOMETRIES(X)")[1].split("\n\n")[0]
+    found = [tuple(map(int, m)) for m in re.findall(r"X\((\d+), (\d+)\)", body)]
+    assert found == BUILD_GEOMETRIES

@@ -150,3 +150,29 @@ def test_build_visiting_order(torch_cuda, engine, inplace):
                                  r["sport"], r["daddr"], r["dport"], False)
         eth = int(i) * 4096 + DATA_OFF - 42
         assert np.array_equal(after[eth:eth + len(exp)], exp), i
+
+
+from test_build import BUILD_GEOMETRIES  # noqa: E402
+
+
+@pytest.mark.parametrize("geom", BUILD_GEOMETRIES)
+def test_build_stage_edges_every_geometry(torch_cuda, engine, geom, monkeypatch):
+    """Payloads around one pass's capacity (16*K*G bytes) from every source
+    phase: the unaligned path reads the extra block K*G from its LDS stage
+    exactly when len + phase > 16*K*G, and longer payloads take the walk."""
+    G, K = geom
+    cap = 16 * K * G
+    monkeypatch.setenv("XCSUM_BUILD_GEOMETRY", f"{G},{K}")
+    rng = np.random.default_rng(G * 100 + K)
+    lens = sorted({L for L in (1, 15, 16, 17, cap - 17, cap - 16, cap - 15, cap - 1, cap,
+                               cap + 1, cap + 15) if 0 < L <= FRAME - DATA_OFF})
+    r = ROUTES[4]
+    for phase in (0, 1, 3, 4, 7, 12, 15):
+        pays = [rng.integers(0, 256, L, dtype=np.uint8) for L in lens]
+        after, desc, out, _ = device_build(torch_cuda, engine, route_of(4, r), pays,
+                                           src_phase=phase, flags=X.F_V4_RFC)
+        for i, p in enumerate(pays):
+            exp = oracle.build_frame(p.tobytes(), 4, r["smac"], r["dmac"], r["saddr"],
+                                     r["sport"], r["daddr"], r["dport"], True)
+            eth = i * FRAME + DATA_OFF - 42
+            assert np.array_equal(after[eth:eth + len(exp)], exp), (geom, phase, len(p))
