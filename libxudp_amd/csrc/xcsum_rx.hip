@@ -375,53 +375,6 @@ static __device__ __forceinline__ u32x4 keep_span(const uint32_t *tab, u32x4 v, 
 	return v & span_mask(tab, b) & ~span_mask(tab, a);
 }
 
-/* a where the lane's bit of `lanes` is clear, b where it is set: v_cndmask
- * through inline asm, so the compiler cannot fold a select chain back into a
- * runtime-indexed (scratch) array read */
-static __device__ __forceinline__ uint32_t pick(uint32_t a, uint32_t b, uint64_t lanes)
-{
-	uint32_t r;
-	asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "s"(lanes));
-	return r;
-}
-
-/* dword x of chunk C of the frame, in every lane of the group: the chunk is
- * held by lane C % G, slot C / G.  Cross-lane moves only, no LDS:
- *   G <= 4:  DPP quad_perm inside the quad;
- *   G == 8:  DPP row_newbcast (gfx90a+) from lanes C and 8 + C of the row,
- *            each half of the row picks its own group's;
- *   G == 16: DPP row_newbcast: the row is the group;
- *   G == 64: v_readlane (the frame is wave-uniform). */
-template <int G, int K, int C>
-static __device__ __forceinline__ uint32_t bcast_dword(const u32x4 (&vc)[K], int x)
-{
-	constexpr int k = C / G < K ? C / G : K - 1, src = C % G;
-	const uint32_t v = x == 0 ? vc[k].x : (x == 1 ? vc[k].y : (x == 2 ? vc[k].z : vc[k].w));
-	if (G <= 4) {
-		constexpr int ctrl = G == 4 ? (src | src << 2 | src << 4 | src << 6)
-				   : G == 2 ? (src | src << 2 | (2 + src) << 4 | (2 + src) << 6)
-					    : 0xE4;   /* G == 1: identity */
-		return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, ctrl, 0xF, 0xF, false);
-	} else if (G == 8) {
-		const uint32_t lo = (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x150 + src, 0xF, 0xF, false);
-		const uint32_t hi = (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x158 + src, 0xF, 0xF, false);
-		return (threadIdx.x & 8) ? hi : lo;
-	} else if (G == 16) {
-		return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x150 + src, 0xF, 0xF, false);
-	} else {
-		return (uint32_t)__builtin_amdgcn_readlane((int)v, src);
-	}
-}
-
-template <int G, int K, int C>
-static __device__ __forceinline__ void bcast_chunk(const u32x4 (&vc)[K], uint32_t *raw)
-{
-	raw[4 * C + 0] = bcast_dword<G, K, C>(vc, 0);
-	raw[4 * C + 1] = bcast_dword<G, K, C>(vc, 1);
-	raw[4 * C + 2] = bcast_dword<G, K, C>(vc, 2);
-	raw[4 * C + 3] = bcast_dword<G, K, C>(vc, 3);
-}
-
 /* Everything for frame p once its chunks v[] have landed: stage, parse,
  * verify, record.  Group-uniform; every lane of the wave must call it. */
 template <int G, int K>
@@ -438,40 +391,22 @@ static __device__ __forceinline__ void rx_frame(const RxArgs &a, uint32_t *st, c
 	 * field the fast path can use lies in bytes 12..61).  Chunks 0..5 of
 	 * the grid hold it, spread over the group's lanes. */
 	uint32_t hdr[13];
-	constexpr bool XL = G != 32;     /* cross-lane header (bcast_dword) */
-	if (XL) {
-		/* broadcast the 6 chunks to every lane of the group (no LDS round
-		 * trip), then realign by fh */
-		/* frame bytes 12..63 start at raw byte fh <= 15: chunks 0..4 */
-		uint32_t raw[20];
-		bcast_chunk<G, K, 0>(vc, raw);
-		bcast_chunk<G, K, 1>(vc, raw);
-		bcast_chunk<G, K, 2>(vc, raw);
-		bcast_chunk<G, K, 3>(vc, raw);
-		bcast_chunk<G, K, 4>(vc, raw);
-		const uint32_t q = fh >> 2, r = fh & 3u;
-		const uint64_t m1 = __builtin_amdgcn_ballot_w64(q == 1);
-		const uint64_t m2 = __builtin_amdgcn_ballot_w64(q == 2);
-		const uint64_t m3 = __builtin_amdgcn_ballot_w64(q == 3);
-		uint32_t sh[14];
+	/* Through the group's LDS stage: the lanes holding chunks 0..5 write
+	 * them, every lane reads the 14 dwords from frame byte 12 back in one
+	 * batch (same addresses across the group: broadcast reads) and realigns
+	 * them with v_alignbyte.  Measured against broadcasting the chunks with
+	 * DPP / v_readlane and selecting dwords with v_cndmask: 1-2% faster at
+	 * MTU and 64 B, 5% on config 5 (profiles/r01/rx_mtu/hdr_*). */
 #pragma unroll
-		for (int j = 0; j < 14; j++)
-			sh[j] = pick(pick(pick(raw[j], raw[j + 1], m1), raw[j + 2], m2), raw[j + 3], m3);
-#pragma unroll
-		for (int i = 0; i < 13; i++)
-			hdr[i] = __builtin_amdgcn_alignbyte(sh[i + 1], sh[i], r);
-	} else {
-		/* G == 32 (two rows): through a per-frame LDS stage, read back in
-		 * one batch of 14 dwords (no read waits on another). */
-#pragma unroll
-		for (int k = 0; k < K; k++) {
-			const uint32_t c = lane + k * G;
-			if (k * G < (int)STAGE_CHUNKS && c < STAGE_CHUNKS)
-				*((u32x4 *)(st + 4 * c)) = vc[k];
-		}
-		__builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-		__builtin_amdgcn_wave_barrier();
-		__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+	for (int k = 0; k < K; k++) {
+		const uint32_t c = lane + k * G;
+		if (k * G < (int)STAGE_CHUNKS && c < STAGE_CHUNKS)
+			*((u32x4 *)(st + 4 * c)) = vc[k];
+	}
+	__builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+	__builtin_amdgcn_wave_barrier();
+	__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+	{
 		const uint32_t *dw = st + (fh >> 2);
 		uint32_t d[14];
 #pragma unroll
@@ -609,12 +544,10 @@ static __device__ __forceinline__ void rx_frame(const RxArgs &a, uint32_t *st, c
 	if (lane == 0 && present && r.status == XCSUM_RX_OK)
 		delivered++;
 
-	if (!XL) {
-		/* the stage is rewritten next iteration: reads first */
-		__builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-		__builtin_amdgcn_wave_barrier();
-		__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-	}
+	/* the stage is rewritten by the next frame: reads first */
+	__builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+	__builtin_amdgcn_wave_barrier();
+	__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
 /*
@@ -630,7 +563,7 @@ __global__ void __launch_bounds__(256) rx_kernel(RxArgs a)
 {
 	/* per-frame header stage: STAGE_CHUNKS chunks + one dword of slack */
 	constexpr uint32_t SW = STAGE_CHUNKS * 4 + 4;   /* dwords per group */
-	__shared__ __attribute__((aligned(16))) uint32_t stage[G == 32 ? (256 / G) * SW : 4];
+	__shared__ __attribute__((aligned(16))) uint32_t stage[(256 / G) * SW];
 	const uint32_t lane = threadIdx.x & (G - 1);
 	const uint32_t grp = threadIdx.x / G;
 	uint32_t *st = stage + grp * SW;
