@@ -477,13 +477,12 @@ static __device__ __forceinline__ void rx_frame(const RxArgs &a, uint32_t *st, c
 #pragma unroll
 			for (int k = 0; k < K; k++) {
 				const int cb = rx_chunk_off(fh, lane + k * G);
-				/* the span's start lies in chunks 0..1 (k == 0) */
-				const bool edge = good && ((k == 0 && cb < lo) || cb + 16 > hi);
-				u32x4 v = vc[k];
-				if (__builtin_amdgcn_ballot_w64(edge))
-					v = edge ? (k == 0 ? keep_span(tab, v, lo - cb, hi - cb)
-						       : v & span_mask(tab, hi - cb))
-						 : v;
+				/* every chunk masked, no per-chunk branch (a ballot and a
+				 * branch per chunk measured 5-10% slower): the span's start
+				 * lies in chunks 0..1 (k == 0), its end anywhere; lanes
+				 * that are not `good` sum bytes nobody reads */
+				const u32x4 v = k == 0 ? keep_span(tab, vc[k], lo - cb, hi - cb)
+						       : vc[k] & span_mask(tab, hi - cb);
 				accum(v, E, O);
 			}
 		}
