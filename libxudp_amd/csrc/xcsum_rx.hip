@@ -26,8 +26,8 @@
  *      v_alignbyte, so no stage read waits on another;
  *   2. the span [pseudo-header addresses, udp + ulen) is summed from the
  *      chunk registers with v_dot4_u32_u8 (exact even/odd byte sums, as in
- *      xcsum_kernels.hip); only chunks that straddle a span edge are masked,
- *      and a chunk row is masked only if some lane of the wave needs it;
+ *      xcsum_kernels.hip), every chunk masked to the span with byte masks
+ *      from a 17-entry LDS table (no per-chunk branch);
  *   3. G-lane DPP reduction, RFC verify, the record (lanes 0..3 store one
  *      16-byte piece each).
  * Frames the stage cannot describe (IPv6 extension headers; IPv4 options
@@ -708,10 +708,12 @@ hipError_t launch_rx(const RxArgs &a, uint32_t len_hint, int cus, hipStream_t s)
 		 * (tools/bench_rx.py, profiles/r01/bench_rx_*.log): two frames per
 		 * group per stage pay for their registers only on small frames;
 		 * MTU frames run best at two waves per SIMD (B = 2), one frame
-		 * per group (profiles/r01/rx_mtu/). */
+		 * per group (profiles/r01/rx_mtu/); 64-byte frames (4,2,1): 17%
+		 * faster than (2,4,2) once the edge masks lost their branches
+		 * (profiles/r01/rx_mtu/geo_c3.log). */
 		const uint32_t chunks = (len_hint + 6) / 16;  /* ceil((len + 3 - 12) / 16) */
 		if (!(a.flags & XCSUM_F_VERIFY)) { G = 4; K = 2; U = 2; }
-		else if (chunks <= 8) { G = 2; K = 4; U = 2; }
+		else if (chunks <= 8) { G = 4; K = 2; }
 		else if (chunks <= 16) { G = 8; K = 2; }
 		else if (chunks <= 32) { G = 16; K = 2; }
 		else if (chunks <= 48) { G = 16; K = 3; }
