@@ -1,5 +1,3 @@
 set -e
-tools/gpu_run.sh s1/pytest_gpu4 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread
-tools/gpu_run.sh s1/bench12_2 200 python bench.py --no-cpu-baseline
-tools/gpu_run.sh s1/bench12_3 200 python bench.py --config 3 --no-cpu-baseline
-tools/gpu_run.sh s1/bench_rx12 300 python tools/bench_rx.py --configs 2,4,3
+tools/gpu_run.sh s2/pytest_rx 400 python -u -m pytest tests/test_gpu_rx.py tests/test_gpu_host_path.py -m gpu -x -q --timeout 120 --timeout-method thread
+tools/gpu_run.sh s2/bench_rx 300 python tools/bench_rx.py --configs 2,4,3,5
