@@ -50,6 +50,49 @@ extern "C" int probe_stream_read(const void *p, uint64_t nbytes, uint32_t *out, 
 	return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
+/* Read+write ceiling (the build kernel's copy modes move every byte twice):
+ * grid-stride dwordx4 copy, UNROLL loads in flight before the stores;
+ * NTS = nontemporal stores (the build kernel's destination is not re-read). */
+template <bool NTS, int UNROLL>
+__global__ void __launch_bounds__(256) stream_copy(const u32x4 *p, u32x4 *q, uint64_t n16)
+{
+	uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+	const uint64_t stride = (uint64_t)gridDim.x * 256;
+	typedef __attribute__((address_space(1))) u32x4 gw32x4;
+	for (; i + (UNROLL - 1) * stride < n16; i += UNROLL * stride) {
+		u32x4 v[UNROLL];
+#pragma unroll
+		for (int u = 0; u < UNROLL; u++)
+			v[u] = __builtin_nontemporal_load((gu32x4 *)(p + i + u * stride));
+#pragma unroll
+		for (int u = 0; u < UNROLL; u++) {
+			if (NTS)
+				__builtin_nontemporal_store(v[u], (gw32x4 *)(q + i + u * stride));
+			else
+				*((gw32x4 *)(q + i + u * stride)) = v[u];
+		}
+	}
+	for (; i < n16; i += stride)
+		q[i] = p[i];
+}
+
+extern "C" int probe_stream_copy(const void *p, void *q, uint64_t nbytes, int blocks, int nts,
+				 int unroll, void *stream)
+{
+	uint64_t n16 = nbytes / 16;
+	hipStream_t s = (hipStream_t)stream;
+	const u32x4 *a = (const u32x4 *)p;
+	u32x4 *b = (u32x4 *)q;
+#define L(N_, U_) hipLaunchKernelGGL((stream_copy<N_, U_>), dim3(blocks), dim3(256), 0, s, a, b, n16)
+	if (nts) {
+		if (unroll == 1) L(true, 1); else if (unroll == 2) L(true, 2); else if (unroll == 4) L(true, 4); else L(true, 8);
+	} else {
+		if (unroll == 1) L(false, 1); else if (unroll == 2) L(false, 2); else if (unroll == 4) L(false, 4); else L(false, 8);
+	}
+#undef L
+	return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
 /* Slot-layout probe: read span16*16 bytes at a 16-aligned offset inside each
  * slot_bytes slot (xudp's UMEM: one frame per 4096-B chunk), nothing else.
  * off(slot) = off0 + (slot * rot16 % nrot) * 16: rot16 = 0 is xudp's fixed
