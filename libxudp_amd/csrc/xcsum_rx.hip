@@ -645,6 +645,324 @@ __global__ void __launch_bounds__(256) rx_kernel(RxArgs a)
 	}
 }
 
+/* ---- lane-per-frame parse (geometry U = 0) ---------------------------------
+ * rx_kernel pays the header work (parse, masks, record) once per G-lane group,
+ * i.e. once per 64/G frames per wave instruction.  Here a wave takes 64
+ * frames at a time and lane l parses frame l from its own 6 header chunks, so
+ * the header work is paid once per 64 frames.  The wave then sums the 64
+ * spans 64/G frames per step, G lanes each, with the ping-pong pipeline; each
+ * group fetches its frame's parameters from the owning lane (ds_bpermute),
+ * the owning lane collects its frame's sum, finishes the verify and stores
+ * the whole 64-byte record (a wave stores 4 KB contiguous).  The next batch's
+ * descriptors and header chunks are in flight during the current batch's
+ * spans. */
+
+/* one frame's parse, lane = frame */
+struct WParse {
+	Rec r;
+	u32x4 saddr, daddr;
+	uint32_t wck;          /* udp len | check << 16 (wire bytes) */
+	uint32_t hsum;         /* IPv4 header word sum (iphdr verify) */
+	int hi;                /* frame-relative span end */
+	bool want, good, slow, v4;
+};
+
+/* per-lane header stage: 6 chunks, 16-byte aligned lane stride */
+constexpr uint32_t WSTAGE = 4 * STAGE_CHUNKS + 4;
+
+/* The batch's header chunks are loaded 8 lanes per frame (chunk wl % 8 of
+ * frame 8i + wl / 8 in hv[i]): 8 frames per load instruction instead of 64
+ * scattered lines per instruction with one lane per frame (measured 1.7x
+ * slower without VERIFY).  The lanes then write them to the owning frames'
+ * LDS stages. */
+constexpr int WHDR = 8;
+
+static __device__ __forceinline__ WParse rx_parse_lane(const RFrame &f, const u32x4 (&hv)[WHDR],
+						       uint32_t *hstage, uint32_t wl, bool verify)
+{
+	const uint32_t len = rx_len(f);
+	const uint32_t nc = rx_nchunks(f);
+	const uint32_t fh = rx_h(f, nc);
+	uint32_t *wst = hstage + (wl & ~63u) * WSTAGE;        /* the wave's stages */
+#pragma unroll
+	for (int i = 0; i < WHDR; i++)
+		if ((wl & 7u) < STAGE_CHUNKS)
+			*((u32x4 *)(wst + (8u * i + ((wl & 63u) >> 3)) * WSTAGE + 4u * (wl & 7u))) = hv[i];
+	__builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+	__builtin_amdgcn_wave_barrier();
+	__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+	/* hdr[i] = frame bytes [12 + 4i, 16 + 4i): from the lane's own stage
+	 * (dword offset fh / 4 is per lane; selects over registers made the
+	 * compiler index a scratch copy), realigned by fh % 4 */
+	const uint32_t *st = wst + (wl & 63u) * WSTAGE;
+	uint32_t d[14];
+#pragma unroll
+	for (int i = 0; i < 14; i++)
+		d[i] = st[(fh >> 2) + i];
+	/* the next batch rewrites the stages: reads first */
+	__builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+	__builtin_amdgcn_wave_barrier();
+	__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+	uint32_t hdr[13];
+#pragma unroll
+	for (int i = 0; i < 13; i++)
+		hdr[i] = __builtin_amdgcn_alignbyte(d[i + 1], d[i], fh & 3u);
+	auto f0 = [&](int x) { return hdr[(x - 12) >> 2]; };
+	auto f2 = [&](int x) {
+		const int i = (x - 12) >> 2;
+		return __builtin_amdgcn_alignbyte(hdr[i + 1], hdr[i], 2u);
+	};
+	/* packet_parse(), as rx_frame */
+	const uint32_t w12 = f0(12), w20 = f0(20), w26 = f2(26), w30 = f2(30);
+	const uint32_t p0 = w12 & 0xffu, p1 = (w12 >> 8) & 0xffu;
+	const uint32_t ihl = (w12 >> 16) & 0xfu;
+	const bool present = rx_present(f);
+	const bool eth_ok = present && len >= 14;
+	const bool is4 = eth_ok && (p0 == 0x08 || p1 == 0x00);
+	const uint32_t l4v4 = 14u + (ihl == 5 ? 20u : (ihl << 2));
+	const bool ok4 = is4 && len >= 34 && (w20 >> 24) == 17 && l4v4 + 8 <= len;
+	const bool is6 = eth_ok && !is4 && p0 == 0x86 && p1 == 0xDD && len >= 54;
+	const bool ok6 = is6 && (w20 & 0xffu) == 17 && len >= 62;
+	WParse P;
+	P.slow = (ok4 && ihl != 5) || (is6 && (w20 & 0xffu) != 17);
+	const bool ok = (ok4 && ihl == 5) || ok6;
+	P.v4 = ok4;
+	const uint32_t l4 = ok ? (ok4 ? 34u : 54u) : 0u;
+	P.wck = ok ? (ok4 ? f2(38) : f2(58)) : 0u;
+	P.r.family = ok ? (ok4 ? 4u : 6u) : 0u;
+	P.r.l4 = l4;
+	P.r.ports = ok ? (ok4 ? f2(34) : f2(54)) : 0u;
+	P.r.ulen = ((P.wck & 0xffu) << 8) | ((P.wck >> 8) & 0xffu);
+	P.r.status = !ok ? XCSUM_RX_PARSE : (w26 == w30 ? XCSUM_RX_STATS : XCSUM_RX_OK);
+	P.saddr = ok4 ? u32x4{w26, 0u, 0u, 0u} : u32x4{f2(22), w26, w30, f2(34)};
+	P.daddr = ok4 ? u32x4{w30, 0u, 0u, 0u} : u32x4{f2(38), f2(42), f2(46), f2(50)};
+	P.hsum = be_words4(f2(14)) + be_words4(f2(18)) + be_words4(f2(22)) + be_words4(w26) +
+		 be_words4(w30);
+	P.want = verify && P.r.status == XCSUM_RX_OK && !P.slow;
+	P.good = P.want && P.r.ulen >= 8 && l4 + P.r.ulen <= len;
+	P.hi = (int)(l4 + P.r.ulen);
+	return P;
+}
+
+static __device__ __forceinline__ uint32_t bperm(uint32_t src_lane, uint32_t v)
+{
+	return (uint32_t)__builtin_amdgcn_ds_bpermute((int)(src_lane << 2), (int)v);
+}
+
+/* a step's frame, fetched from its owning lane */
+struct WStep {
+	RFrame f;
+	int hi;
+	uint32_t fl;           /* bit 0: IPv4 span start, bit 1: good */
+};
+
+template <int G>
+static __device__ __forceinline__ WStep rx_step_frame(const RFrame &f, int hi, uint32_t fl,
+						      uint32_t src)
+{
+	const uint64_t e = (uint64_t)(uintptr_t)f.eth;
+	WStep s;
+	if (G == 64) {   /* one frame per step: wave-uniform, scalar reads */
+		const int j = (int)__builtin_amdgcn_readfirstlane(src);
+		s.f.eth = (const uint8_t *)(uintptr_t)(
+			((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(e >> 32), j) << 32) |
+			(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)e, j));
+		s.f.meta = (uint32_t)__builtin_amdgcn_readlane((int)f.meta, j);
+		s.hi = __builtin_amdgcn_readlane(hi, j);
+		s.fl = (uint32_t)__builtin_amdgcn_readlane((int)fl, j);
+		return s;
+	}
+	s.f.eth = (const uint8_t *)(uintptr_t)(((uint64_t)bperm(src, (uint32_t)(e >> 32)) << 32) |
+					       bperm(src, (uint32_t)e));
+	s.f.meta = bperm(src, f.meta);
+	s.hi = (int)bperm(src, (uint32_t)hi);
+	s.fl = bperm(src, fl);
+	return s;
+}
+
+/* the G-lane span sum of a step's frame (all lanes of the group get it) */
+template <int G, int K>
+static __device__ __forceinline__ uint32_t rx_step_sum(const uint32_t *tab, const WStep &s,
+						       const u32x4 (&v)[K], uint32_t lane)
+{
+	const uint32_t nchunks = rx_nchunks(s.f);
+	const uint32_t fh = rx_h(s.f, nchunks);
+	const int lo = (s.fl & 1u) ? 26 : 22;
+	const int hi = s.hi;
+	uint32_t E = 0, O = 0;
+	if (__builtin_amdgcn_ballot_w64((s.fl & 2u) && nchunks > K * G)) {
+		for (uint32_t c = lane; c < nchunks; c += G) {
+			const int cb = rx_chunk_off(fh, c);
+			u32x4 x = __builtin_nontemporal_load((gu32x4 *)(s.f.eth + cb));
+			if (cb < lo || cb + 16 > hi)
+				x = keep_span(tab, x, lo - cb, hi - cb);
+			accum(x, E, O);
+		}
+	} else {
+#pragma unroll
+		for (int k = 0; k < K; k++) {
+			const int cb = rx_chunk_off(fh, lane + k * G);
+			const u32x4 x = k == 0 ? keep_span(tab, v[k], lo - cb, hi - cb)
+					       : v[k] & span_mask(tab, hi - cb);
+			accum(x, E, O);
+		}
+	}
+	const uint32_t sum = ((uintptr_t)s.f.eth & 1u) ? (O << 8) + E : (E << 8) + O;
+	return seg_sum<G>(sum);
+}
+
+template <int G, int K>
+__global__ void __launch_bounds__(256) rx_wide_kernel(RxArgs a)
+{
+	constexpr uint32_t FPS = 64 / G;        /* frames per step */
+	constexpr uint32_t STEPS = G;           /* 64 frames per batch */
+	__shared__ __attribute__((aligned(16))) uint32_t span[SPAN_DWORDS];
+	__shared__ __attribute__((aligned(16))) uint32_t hstage[256 * WSTAGE];
+	span_init(span);
+	__syncthreads();
+	const uint32_t wl = threadIdx.x & 63u;  /* lane = frame of the batch */
+	const uint32_t lane = wl & (G - 1);     /* lane in the step's group */
+	const uint32_t grp = wl / G;
+	const uint32_t wid = __builtin_amdgcn_readfirstlane(blockIdx.x * 4u + (threadIdx.x >> 6));
+	const uint32_t nw = gridDim.x * 4u;
+	const bool verify = (a.flags & XCSUM_F_VERIFY) != 0;
+	const bool iphdr = (a.flags & XCSUM_F_IPHDR) != 0;
+	const uint32_t nb = (a.n + 63u) / 64u;
+	const uint8_t *zero = (const uint8_t *)g_rx_zero;
+	uint32_t delivered = 0;
+
+	auto hdr_issue = [&](const RFrame &f, u32x4 (&hv)[WHDR]) {
+		const uint32_t c = wl & 7u;
+#pragma unroll
+		for (int i = 0; i < WHDR; i++) {
+			const WStep s = rx_step_frame<8>(f, 0, 0u, 8u * i + (wl >> 3));
+			const uint32_t nc = rx_nchunks(s.f);
+			const uint32_t h = rx_h(s.f, nc);
+			hv[i] = __builtin_nontemporal_load(
+				(gu32x4 *)(c < nc && c < STAGE_CHUNKS ? s.f.eth + rx_chunk_off(h, c) : zero));
+		}
+	};
+	auto span_issue = [&](const WStep &s, u32x4 (&v)[K]) {
+		const uint32_t nc = (s.fl & 2u) ? rx_nchunks(s.f) : 0u;  /* only frames to verify */
+		const uint32_t h = rx_h(s.f, rx_nchunks(s.f));
+#pragma unroll
+		for (int k = 0; k < K; k++) {
+			const uint32_t c = lane + k * G;
+			v[k] = __builtin_nontemporal_load(
+				(gu32x4 *)(c < nc ? s.f.eth + rx_chunk_off(h, c) : zero));
+		}
+	};
+
+	uint32_t b = wid;
+	RFrame f = rx_resolve(a, rx_desc(a, b * 64u + wl), b * 64u + wl < a.n);
+	u32x4 hv[WHDR];
+	hdr_issue(f, hv);
+	for (; b < nb; b += nw) {
+		const uint32_t p = b * 64u + wl;
+		const uint32_t bn = b + nw;
+		const u32x3 dn = rx_desc(a, bn * 64u + wl);
+		WParse P = rx_parse_lane(f, hv, hstage, threadIdx.x, verify);
+		const RFrame fn = rx_resolve(a, dn, bn * 64u + wl < a.n);
+		__builtin_amdgcn_sched_barrier(0);
+		if (bn < nb)
+			hdr_issue(fn, hv);    /* the next batch's headers, during the spans */
+
+		if (__builtin_amdgcn_ballot_w64(P.want)) {
+			const uint32_t fl = (P.v4 ? 1u : 0u) | (P.good ? 2u : 0u);
+			uint32_t mysum = 0;
+			u32x4 va[K], vb[K];
+			WStep sa = rx_step_frame<G>(f, P.hi, fl, grp);
+			span_issue(sa, va);
+#pragma unroll 1
+			for (uint32_t t = 0; t < STEPS; t += 2) {
+				const WStep sb = rx_step_frame<G>(f, P.hi, fl, (t + 1) * FPS + grp);
+				__builtin_amdgcn_sched_barrier(0);
+				span_issue(sb, vb);
+				__builtin_amdgcn_sched_barrier(0);
+				uint32_t s = rx_step_sum<G, K>(span, sa, va, lane);
+				uint32_t x = G == 64 ? s : bperm((wl % FPS) * G, s);
+				if (wl / FPS == t)
+					mysum = x;
+				if (t + 2 < STEPS) {
+					sa = rx_step_frame<G>(f, P.hi, fl, (t + 2) * FPS + grp);
+					__builtin_amdgcn_sched_barrier(0);
+					span_issue(sa, va);
+					__builtin_amdgcn_sched_barrier(0);
+				}
+				s = rx_step_sum<G, K>(span, sb, vb, lane);
+				x = G == 64 ? s : bperm((wl % FPS) * G, s);
+				if (wl / FPS == t + 1)
+					mysum = x;
+			}
+			bool good = P.good;
+			if (good) {
+				const uint32_t s = mysum + 17u + P.r.ulen;
+				good = (P.wck >> 16) == 0 ? P.r.family == 4 : fold16(s) == 0xffffu;
+			}
+			if (iphdr && P.r.family == 4)
+				good = good && fold16(P.hsum) == 0xffffu;
+			if (P.want && !good)
+				P.r.status = XCSUM_RX_CSUM;
+		}
+
+		/* the general case, one frame at a time by the whole wave */
+		uint64_t sm = __builtin_amdgcn_ballot_w64(P.slow);
+		while (sm) {
+			const uint32_t j = __builtin_ctzll(sm);
+			sm &= sm - 1;
+			const uint64_t e = (uint64_t)(uintptr_t)f.eth;
+			const uint8_t *eth = (const uint8_t *)(uintptr_t)(
+				((uint64_t)__builtin_amdgcn_readlane((int)(e >> 32), (int)j) << 32) |
+				(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)e, (int)j));
+			const uint32_t len = (uint32_t)__builtin_amdgcn_readlane((int)rx_len(f), (int)j);
+			const Rec rs = rx_slow<64>(eth, len, wl, true, verify, iphdr);
+			if (wl == j) {
+				P.r = rs;
+				/* addresses from global memory, iph + 12 / iph6 + 8 */
+				auto ld4 = [&](uint32_t o) {
+					return (uint32_t)eth[o] | ((uint32_t)eth[o + 1] << 8) |
+					       ((uint32_t)eth[o + 2] << 16) | ((uint32_t)eth[o + 3] << 24);
+				};
+				if (rs.family == 4) {
+					P.saddr = u32x4{ld4(26), 0u, 0u, 0u};
+					P.daddr = u32x4{ld4(30), 0u, 0u, 0u};
+				} else if (rs.status != XCSUM_RX_PARSE) {
+					P.saddr = u32x4{ld4(22), ld4(26), ld4(30), ld4(34)};
+					P.daddr = u32x4{ld4(38), ld4(42), ld4(46), ld4(50)};
+				}
+			}
+		}
+
+		/* the record: 64 bytes per lane */
+		const Rec &r = P.r;
+		const bool pok = r.status != XCSUM_RX_PARSE;
+		const uint64_t addr = (uint64_t)(f.eth - a.umem);
+		const uint64_t body = pok ? addr + r.l4 + 8 : 0;
+		const u32x4 zero4 = {0u, 0u, 0u, 0u};
+		if (rx_present(f)) {
+			u32x4 *m = (u32x4 *)(a.msgs + p);
+			m[0] = u32x4{(uint32_t)addr, (uint32_t)(addr >> 32), (uint32_t)body,
+				     (uint32_t)(body >> 32)};
+			m[1] = u32x4{pok ? r.ulen - 8u : 0u,
+				     r.status | (r.family << 8) | ((pok ? r.l4 : 0u) << 16), r.ports, 0u};
+			m[2] = pok ? P.saddr : zero4;
+			m[3] = pok ? P.daddr : zero4;
+			if (r.status == XCSUM_RX_OK)
+				delivered++;
+		}
+		f = fn;
+	}
+	if (a.count) {
+		__shared__ uint32_t wsum[4];
+		const uint32_t tot = seg_sum<64>(delivered);
+		if ((threadIdx.x & 63) == 0)
+			wsum[threadIdx.x >> 6] = tot;
+		__syncthreads();
+		if (threadIdx.x == 0)
+			a.part[blockIdx.x] = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+	}
+}
+
 __global__ void __launch_bounds__(256) rx_count_kernel(const uint32_t *part, uint32_t nblocks,
 						      uint32_t *count)
 {
@@ -666,12 +984,18 @@ static hipError_t launch_rx_t(const RxArgs &a, int cus, int bpc, hipStream_t s)
 	static int occ = 0;
 	if (!occ) {
 		int nb = 0;
-		if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, rx_kernel<G, K, U>, 256, 0) !=
-			    hipSuccess || nb <= 0)
+		hipError_t e;
+		if constexpr (U == 0)
+			e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, rx_wide_kernel<G, K>, 256, 0);
+		else
+			e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, rx_kernel<G, K, U>, 256, 0);
+		if (e != hipSuccess || nb <= 0)
 			nb = 4;
 		occ = nb;
 	}
-	uint64_t blocks = (((uint64_t)a.n + U - 1) / U * G + 255) / 256;
+	/* U == 0: lane-per-frame parse, a wave per 64 frames */
+	uint64_t blocks = U == 0 ? ((uint64_t)a.n + 255) / 256
+				 : (((uint64_t)a.n + (U ? U : 1) - 1) / (U ? U : 1) * G + 255) / 256;
 	const uint64_t cap = (uint64_t)cus * ((bpc > 0 && bpc < occ) ? bpc : occ);
 	if (blocks > cap)
 		blocks = cap;
@@ -681,7 +1005,10 @@ static hipError_t launch_rx_t(const RxArgs &a, int cus, int bpc, hipStream_t s)
 		blocks = 1;
 	(void)hipGetLastError();  /* clear a stale error (e.g. hipErrorNotReady from
 	                           * someone's hipEventQuery) before checking ours */
-	hipLaunchKernelGGL((rx_kernel<G, K, U>), dim3((unsigned)blocks), dim3(256), 0, s, a);
+	if constexpr (U == 0)
+		hipLaunchKernelGGL((rx_wide_kernel<G, K>), dim3((unsigned)blocks), dim3(256), 0, s, a);
+	else
+		hipLaunchKernelGGL((rx_kernel<G, K, U>), dim3((unsigned)blocks), dim3(256), 0, s, a);
 	if (a.count)
 		hipLaunchKernelGGL(rx_count_kernel, dim3(1), dim3(256), 0, s, a.part,
 				   (uint32_t)blocks, a.count);
@@ -690,7 +1017,8 @@ static hipError_t launch_rx_t(const RxArgs &a, int cus, int bpc, hipStream_t s)
 
 #define XCSUM_RX_GEOMETRIES(X) \
 	X(2, 4, 1) X(2, 4, 2) X(4, 2, 1) X(4, 2, 2) X(8, 1, 2) X(8, 2, 1) \
-	X(16, 2, 1) X(16, 3, 1) X(16, 6, 1) X(16, 6, 2) X(64, 9, 1)
+	X(16, 2, 1) X(16, 3, 1) X(16, 6, 1) X(16, 6, 2) X(64, 9, 1) \
+	X(8, 2, 0) X(16, 3, 0) X(16, 6, 0) X(64, 9, 0)
 
 hipError_t launch_rx(const RxArgs &a, uint32_t len_hint, int cus, hipStream_t s)
 {
@@ -719,7 +1047,8 @@ hipError_t launch_rx(const RxArgs &a, uint32_t len_hint, int cus, hipStream_t s)
 		else if (chunks <= 32) { G = 16; K = 2; }
 		else if (chunks <= 48) { G = 16; K = 3; }
 		else if (chunks <= 96) { G = 16; K = 6; B = 2; }
-		else { G = 64; K = 9; }
+		else { G = 64; K = 9; U = 0; }   /* lane-per-frame parse: config 5
+						  * 7.73 -> 6.93 ms (rxwide/) */
 	}
 #define X(g_, k_, u_) \
 	if (G == g_ && K == k_ && U == u_) return launch_rx_t<g_, k_, u_>(a, cus, B, s);
