@@ -36,6 +36,10 @@
  * exactly as before; jumbo frames (more than K*G chunks) re-walk their
  * chunks from global memory.  Results never depend on the path.
  *
+ * rx_wide_kernel (geometries with U = 0, the default for jumbo frames) does
+ * the header work one frame per lane, 64 frames per wave, and then sums the
+ * spans G lanes per frame (see its comment).
+ *
  * d_umem must be 4-byte aligned: the first chunk may start up to 3 bytes
  * before a frame whose address is not (it never leaves the frame's dword).
  */
