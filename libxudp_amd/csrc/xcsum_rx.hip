@@ -1022,7 +1022,7 @@ static hipError_t launch_rx_t(const RxArgs &a, int cus, int bpc, hipStream_t s)
 #define XCSUM_RX_GEOMETRIES(X) \
 	X(2, 4, 1) X(2, 4, 2) X(4, 2, 1) X(4, 2, 2) X(8, 1, 2) X(8, 2, 1) \
 	X(16, 2, 1) X(16, 3, 1) X(16, 6, 1) X(16, 6, 2) X(64, 9, 1) \
-	X(8, 2, 0) X(16, 3, 0) X(16, 6, 0) X(64, 9, 0)
+	X(8, 2, 0) X(16, 3, 0) X(16, 6, 0) X(32, 3, 0) X(64, 2, 0) X(64, 9, 0)
 
 hipError_t launch_rx(const RxArgs &a, uint32_t len_hint, int cus, hipStream_t s)
 {
