@@ -842,8 +842,11 @@ __global__ void __launch_bounds__(256) rx_wide_kernel(RxArgs a)
 			const WStep s = rx_step_frame<8>(f, 0, 0u, 8u * i + (wl >> 3));
 			const uint32_t nc = rx_nchunks(s.f);
 			const uint32_t h = rx_h(s.f, nc);
-			hv[i] = __builtin_nontemporal_load(
-				(gu32x4 *)(c < nc && c < STAGE_CHUNKS ? s.f.eth + rx_chunk_off(h, c) : zero));
+			/* temporal: the span loads re-read these lines one batch
+			 * later; loaded nontemporal they were evicted first and
+			 * fetched twice (+220 B per MTU frame, FETCH_SIZE) */
+			hv[i] = *((gu32x4 *)(c < nc && c < STAGE_CHUNKS ? s.f.eth + rx_chunk_off(h, c)
+									 : zero));
 		}
 	};
 	auto span_issue = [&](const WStep &s, u32x4 (&v)[K]) {
@@ -1045,12 +1048,21 @@ hipError_t launch_rx(const RxArgs &a, uint32_t len_hint, int cus, hipStream_t s)
 		 * (profiles/r01/rx_mtu/geo_c3.log); the header-only pass at 2
 		 * blocks per CU: 9% faster than at full occupancy (geo_plain.log). */
 		const uint32_t chunks = (len_hint + 6) / 16;  /* ceil((len + 3 - 12) / 16) */
-		if (!(a.flags & XCSUM_F_VERIFY)) { G = 4; K = 2; U = 2; B = 2; }
+		if (!(a.flags & XCSUM_F_VERIFY)) {
+			/* header only: lane-per-frame parse above 16 chunks
+			 * (config 4 0.052 -> 0.043 ms, config 2 0.060 -> 0.058;
+			 * 64-byte frames stay faster on (4,2,2): rx_wide/rxwide6) */
+			if (chunks > 16) { G = 32; K = 3; U = 0; }
+			else { G = 4; K = 2; U = 2; B = 2; }
+		}
 		else if (chunks <= 8) { G = 4; K = 2; }
 		else if (chunks <= 16) { G = 8; K = 2; }
 		else if (chunks <= 32) { G = 16; K = 2; }
 		else if (chunks <= 48) { G = 16; K = 3; }
-		else if (chunks <= 96) { G = 16; K = 6; B = 2; }
+		else if (chunks <= 96) { G = 32; K = 3; U = 0; }  /* MTU: lane-per-frame
+								    * parse, 0.301 -> 0.291 ms
+								    * (config 2), 0.286 -> 0.282
+								    * (config 4), rxwide6 */
 		else { G = 64; K = 9; U = 0; }   /* lane-per-frame parse: config 5
 						  * 7.73 -> 6.93 ms (rxwide/) */
 	}
