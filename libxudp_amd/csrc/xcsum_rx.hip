@@ -656,8 +656,8 @@ __global__ void __launch_bounds__(256) rx_kernel(RxArgs a)
  * the header work is paid once per 64 frames.  The wave then sums the 64
  * spans 64/G frames per step, G lanes each, with the ping-pong pipeline; each
  * group fetches its frame's parameters from the owning lane (ds_bpermute),
- * the owning lane collects its frame's sum, finishes the verify and stores
- * the whole 64-byte record (a wave stores 4 KB contiguous).  The next batch's
+ * the owning lane collects its frame's sum and finishes the verify; the
+ * 64 records go out through LDS, 1 KB contiguous per store instruction.  The next batch's
  * descriptors and header chunks are in flight during the current batch's
  * spans. */
 
@@ -865,7 +865,6 @@ __global__ void __launch_bounds__(256) rx_wide_kernel(RxArgs a)
 	u32x4 hv[WHDR];
 	hdr_issue(f, hv);
 	for (; b < nb; b += nw) {
-		const uint32_t p = b * 64u + wl;
 		const uint32_t bn = b + nw;
 		const u32x3 dn = rx_desc(a, bn * 64u + wl);
 		WParse P = rx_parse_lane(f, hv, hstage, threadIdx.x, verify);
@@ -946,15 +945,33 @@ __global__ void __launch_bounds__(256) rx_wide_kernel(RxArgs a)
 		const uint64_t addr = (uint64_t)(f.eth - a.umem);
 		const uint64_t body = pok ? addr + r.l4 + 8 : 0;
 		const u32x4 zero4 = {0u, 0u, 0u, 0u};
-		if (rx_present(f)) {
-			u32x4 *m = (u32x4 *)(a.msgs + p);
-			m[0] = u32x4{(uint32_t)addr, (uint32_t)(addr >> 32), (uint32_t)body,
-				     (uint32_t)(body >> 32)};
-			m[1] = u32x4{pok ? r.ulen - 8u : 0u,
-				     r.status | (r.family << 8) | ((pok ? r.l4 : 0u) << 16), r.ports, 0u};
-			m[2] = pok ? P.saddr : zero4;
-			m[3] = pok ? P.daddr : zero4;
-			if (r.status == XCSUM_RX_OK)
+		/* through the wave's stage, so that each store instruction writes
+		 * 1 KB contiguous (lane l: bytes 16l.. of the i-th KB); per-lane
+		 * 64-byte stores measured 7-10% slower header-only, 1-2% with
+		 * VERIFY (profiles/r01/rx_wide/reclds) */
+		{
+			uint32_t *wst = hstage + (threadIdx.x & ~63u) * WSTAGE;
+			u32x4 *rs = (u32x4 *)(wst + 16u * wl);
+			rs[0] = u32x4{(uint32_t)addr, (uint32_t)(addr >> 32), (uint32_t)body,
+				      (uint32_t)(body >> 32)};
+			rs[1] = u32x4{pok ? r.ulen - 8u : 0u,
+				      r.status | (r.family << 8) | ((pok ? r.l4 : 0u) << 16), r.ports, 0u};
+			rs[2] = pok ? P.saddr : zero4;
+			rs[3] = pok ? P.daddr : zero4;
+			__builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+			__builtin_amdgcn_wave_barrier();
+			__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+			u32x4 *m = (u32x4 *)(a.msgs + b * 64u);
+#pragma unroll
+			for (uint32_t i = 0; i < 4; i++) {
+				const u32x4 v = *((const u32x4 *)(wst + 256u * i + 4u * wl));
+				if (b * 64u + 16u * i + (wl >> 2) < a.n)
+					m[64u * i + wl] = v;
+			}
+			__builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+			__builtin_amdgcn_wave_barrier();
+			__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+			if (rx_present(f) && r.status == XCSUM_RX_OK)
 				delivered++;
 		}
 		f = fn;
