@@ -1042,7 +1042,7 @@ static hipError_t launch_rx_t(const RxArgs &a, int cus, int bpc, hipStream_t s)
 #define XCSUM_RX_GEOMETRIES(X) \
 	X(2, 4, 1) X(2, 4, 2) X(4, 2, 1) X(4, 2, 2) X(8, 1, 2) X(8, 2, 1) \
 	X(16, 2, 1) X(16, 3, 1) X(16, 6, 1) X(16, 6, 2) X(64, 9, 1) \
-	X(8, 2, 0) X(16, 3, 0) X(16, 6, 0) X(32, 3, 0) X(64, 2, 0) X(64, 9, 0)
+	X(4, 2, 0) X(8, 2, 0) X(16, 3, 0) X(16, 6, 0) X(32, 3, 0) X(64, 2, 0) X(64, 9, 0)
 
 hipError_t launch_rx(const RxArgs &a, uint32_t len_hint, int cus, hipStream_t s)
 {
@@ -1066,11 +1066,12 @@ hipError_t launch_rx(const RxArgs &a, uint32_t len_hint, int cus, hipStream_t s)
 		 * blocks per CU: 9% faster than at full occupancy (geo_plain.log). */
 		const uint32_t chunks = (len_hint + 6) / 16;  /* ceil((len + 3 - 12) / 16) */
 		if (!(a.flags & XCSUM_F_VERIFY)) {
-			/* header only: lane-per-frame parse above 16 chunks
-			 * (config 4 0.052 -> 0.043 ms, config 2 0.060 -> 0.058;
-			 * 64-byte frames stay faster on (4,2,2): rx_wide/rxwide6) */
+			/* header only: lane-per-frame parse (no span loads, so
+			 * G and K only set the code size): config 4 0.052 ->
+			 * 0.039 ms, config 2 0.060 -> 0.057, config 3 0.040 ->
+			 * 0.0375 (rx_wide/rxwide6, reclds, rxsmall) */
 			if (chunks > 16) { G = 32; K = 3; U = 0; }
-			else { G = 4; K = 2; U = 2; B = 2; }
+			else { G = 4; K = 2; U = 0; }
 		}
 		else if (chunks <= 8) { G = 4; K = 2; }
 		else if (chunks <= 16) { G = 8; K = 2; }

@@ -53,7 +53,7 @@ def run_rx(torch, eng, umem, desc, flags, len_hint=0, geometry=None):
 
 
 GEOMETRIES = ["2,4,1", "2,4,2", "4,2,1", "4,2,2", "8,1,2", "8,2,1", "16,2,1", "16,3,1", "16,6,1", "16,6,2", "64,9,1",
-              "8,2,0", "16,3,0", "16,6,0", "32,3,0", "64,2,0", "64,9,0"]
+              "4,2,0", "8,2,0", "16,3,0", "16,6,0", "32,3,0", "64,2,0", "64,9,0"]
 
 
 def test_rx_geometry_list_matches_kernel():
