@@ -820,6 +820,10 @@ __global__ void __launch_bounds__(256) rx_wide_kernel(RxArgs a)
 {
 	constexpr uint32_t FPS = 64 / G;        /* frames per step */
 	constexpr uint32_t STEPS = G;           /* 64 frames per batch */
+#ifndef XCSUM_RX_WIDE_HDR_LEAD
+#define XCSUM_RX_WIDE_HDR_LEAD 4   /* 4 steps: config 2 -2.3%, config 5 -3.1% vs 0 (rx_wide/rxlead) */
+#endif
+	constexpr uint32_t HDR_LEAD = XCSUM_RX_WIDE_HDR_LEAD;   /* even */
 	__shared__ __attribute__((aligned(16))) uint32_t span[SPAN_DWORDS];
 	__shared__ __attribute__((aligned(16))) uint32_t hstage[256 * WSTAGE];
 	span_init(span);
@@ -870,10 +874,13 @@ __global__ void __launch_bounds__(256) rx_wide_kernel(RxArgs a)
 		WParse P = rx_parse_lane(f, hv, hstage, threadIdx.x, verify);
 		const RFrame fn = rx_resolve(a, dn, bn * 64u + wl < a.n);
 		__builtin_amdgcn_sched_barrier(0);
-		if (bn < nb)
-			hdr_issue(fn, hv);    /* the next batch's headers, during the spans */
+		const bool spans = __builtin_amdgcn_ballot_w64(P.want) != 0;
+		/* the next batch's headers: HDR_LEAD steps before this batch's
+		 * last (or now when there are no spans to sum) */
+		if (bn < nb && (!spans || HDR_LEAD == 0 || HDR_LEAD >= STEPS))
+			hdr_issue(fn, hv);
 
-		if (__builtin_amdgcn_ballot_w64(P.want)) {
+		if (spans) {
 			const uint32_t fl = (P.v4 ? 1u : 0u) | (P.good ? 2u : 0u);
 			uint32_t mysum = 0;
 			u32x4 va[K], vb[K];
@@ -881,6 +888,8 @@ __global__ void __launch_bounds__(256) rx_wide_kernel(RxArgs a)
 			span_issue(sa, va);
 #pragma unroll 1
 			for (uint32_t t = 0; t < STEPS; t += 2) {
+				if (HDR_LEAD > 0 && HDR_LEAD < STEPS && t + HDR_LEAD == STEPS && bn < nb)
+					hdr_issue(fn, hv);
 				const WStep sb = rx_step_frame<G>(f, P.hi, fl, (t + 1) * FPS + grp);
 				__builtin_amdgcn_sched_barrier(0);
 				span_issue(sb, vb);
