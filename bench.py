@@ -11,12 +11,20 @@ time).
 
 value    = algorithmic bytes of all ranks / max-over-ranks wall time, GiB/s
            (algorithmic bytes per frame = UDP length + pseudo-header address
-           bytes + 2-byte result)
+           bytes + 2-byte result).  Timing: W eager warm-up
+           launches, then >= --ramp-ms (300) of untimed back-to-back K-step
+           bodies so the clocks reach their working point, then --reps (5)
+           timed repetitions of exactly K steps, each bracketed by barrier +
+           synchronize; the median repetition is reported (all are listed)
 roofline = the checksum kernel's algorithmic bytes per launch / its average
            launch duration (HIP events on the launch stream), vs 8 TB/s HBM3E
 cpu_baseline = the reference's own checksum.h (oracle/_ref, compiled from
            /root/reference in the build container) on a bounded sample of the
-           same workload on this host's cores (rank 0, N=1 only)
+           same workload on this host's cores: 1, 16 and os.cpu_count()
+           threads (rank 0, N=1 only)
+parity   = the timed output's SHA-256 against the reference's digest of the
+           same frames (config 5 at N>1: all ranks' shards concatenated), plus
+           a 4096-frame spot check against the oracle
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--config C]
 """
@@ -97,8 +105,31 @@ def build_batch(cfg, rank, world, torch, dev, eng, stream):
     return desc, d_desc, bufs, out, first, count
 
 
-def cpu_baseline(cfg, seconds=10.0):
-    """The reference checksum.h timed on this host over a bounded sample."""
+def host_cpu_facts():
+    """CPUs this process may use: affinity mask and cgroup v2 quota (on the GPU
+    box os.cpu_count() is the whole machine, not this job's share)."""
+    facts = {"host_cpus": os.cpu_count()}
+    try:
+        facts["affinity_cpus"] = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        pass
+    try:
+        q, p = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        facts["cgroup_cpu_quota"] = None if q == "max" else round(int(q) / int(p), 2)
+    except (OSError, ValueError):
+        pass
+    try:
+        with open("/proc/cpuinfo") as f:
+            facts["cpu_model"] = next((ln.split(":", 1)[1].strip() for ln in f
+                                       if ln.startswith("model name")), "")
+    except OSError:
+        pass
+    return facts
+
+
+def cpu_baseline(cfg, seconds=15.0):
+    """The reference checksum.h timed on this host over a bounded sample:
+    1 thread, 16 threads and os.cpu_count() threads (static frame partition)."""
     import oracle  # test infrastructure, used here only as the CPU baseline
     seed = SEED_BASE ^ cfg["id"]
     m = min(cfg["n"], 1 << 16)
@@ -114,41 +145,137 @@ def cpu_baseline(cfg, seconds=10.0):
         kind, L = "port", oracle.port()
         timed = lambda th, reps: L.orc_batch_timed(umem.ctypes.data, desc.ctypes.data, m,
                                                    out.ctypes.data, mode, 0, th, reps)
-    threads = max(1, min(16, os.cpu_count() or 1))
+    allc = max(1, min(256, os.cpu_count() or 1))
+    legs = [(1, 0.3), (min(16, allc), 0.35)]
+    if allc > 16:
+        legs.append((allc, 0.35))
     res = {}
-    for th, budget in ((1, seconds * 0.35), (threads, seconds * 0.65)):
+    for th, share in legs:
         t1 = timed(th, 1)
-        reps = max(1, int(budget / max(t1, 1e-6)))
+        reps = max(1, int(seconds * share / max(t1, 1e-6)))
         t = timed(th, reps)
         res[th] = alg * reps / t / 2**30
     exp = oracle.ref_batch(umem, desc, mode) if kind == "reference" else oracle.batch(umem, desc,
                                                                                         mode)
     assert np.array_equal(out, exp)
-    model = ""
-    try:
-        with open("/proc/cpuinfo") as f:
-            model = next((ln.split(":", 1)[1].strip() for ln in f
-                          if ln.startswith("model name")), "")
-    except OSError:
-        pass
-    return {"value": round(res[threads], 3), "unit": "GiB/s", "cores": threads, "kind": kind,
-            "value_1core": round(res[1], 3), "cpu_model": model,
-            "host_cpus": os.cpu_count(),
+    best_th = max(res, key=lambda k: res[k])
+    facts = host_cpu_facts()
+    return {"value": round(res[best_th], 3), "unit": "GiB/s", "cores": best_th, "kind": kind,
+            "by_threads": {str(k): round(v, 3) for k, v in sorted(res.items())},
+            "value_1core": round(res[1], 3), **facts,
             "sample": f"{m} frames of the same config ({alg / 1e6:.1f} MB algorithmic), "
-                      f"repeated for ~{seconds:.0f} s; xudp/checksum.h "
+                      f"repeated for ~{seconds:.0f} s in all; xudp/checksum.h "
                       f"{'udp_csum6' if mode == 2 else 'udp_checksum'} compiled -O2 from the "
-                      f"reference, static frame partition over {threads} pthreads"}
+                      f"reference, static frame partition over 1, 16 and os.cpu_count() "
+                      f"pthreads; value = the fastest of those"}
 
 
-def pmc_traffic(cid):
-    """HBM bytes per launch from the committed rocprofv3 PMC summary, if any."""
-    path = os.path.join(ROOT, "profiles", f"pmc_config{cid}.json")
-    if os.path.exists(path):
-        try:
-            return json.load(open(path)).get("hbm_bytes_per_launch")
-        except Exception:
+def pmc_traffic(cid, layout):
+    """HBM bytes per launch from the rocprofv3 PMC summary committed under
+    profiles/ (FETCH_SIZE + WRITE_SIZE passes of this bench, tools/pmc_summary.py);
+    counters cannot be read inside the timed process itself."""
+    for rnd in ("r02", "r01", ""):
+        name = f"pmc_config{cid}{'_umem' if layout == 'umem' else ''}.json"
+        path = os.path.join(ROOT, "profiles", rnd, name)
+        if os.path.exists(path):
+            try:
+                return (json.load(open(path)).get("hbm_bytes_per_launch"),
+                        os.path.relpath(path, ROOT))
+            except Exception:
+                pass
+    return None, None
+
+
+def gpu_clocks(dev):
+    """Current SCLK / MCLK of this GPU from sysfs (the '*' level of
+    pp_dpm_sclk / pp_dpm_mclk), or None where not readable."""
+    try:
+        import torch
+        p = torch.cuda.get_device_properties(dev)
+        path = f"/sys/bus/pci/devices/{p.pci_domain_id:04x}:{p.pci_bus_id:02x}:" \
+               f"{p.pci_device_id:02x}.0"
+        res = {}
+        for k in ("sclk", "mclk", "fclk"):
+            try:
+                for ln in open(os.path.join(path, f"pp_dpm_{k}")):
+                    if "*" in ln:
+                        res[k] = ln.split(":", 1)[1].replace("*", "").strip()
+            except OSError:
+                pass
+        return res or None
+    except Exception:
+        return None
+
+
+def stream_ceiling(torch, dev, bufs, sptr):
+    """Same-run streaming-read ceiling: tools/libhbmprobe.so's dwordx4
+    grid-stride read (8 blocks/CU, nontemporal; the best setting of
+    tools/hbm_probe.py) over the very buffers the checksum kernel reads,
+    rotated the same way.  A measuring stick, not the product."""
+    path = os.path.join(ROOT, "tools", "libhbmprobe.so")
+    if not os.path.exists(path):
+        return None
+    L = ctypes.CDLL(path)
+    L.probe_stream_read.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
+                                    ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
+    cus = torch.cuda.get_device_properties(dev).multi_processor_count
+    blocks = cus * 8
+    scratch = torch.empty(blocks * 256, dtype=torch.int32, device=dev)
+    nbytes = (bufs[0].numel() - 64) & ~15
+    ts = []
+    for r in range(12 * len(bufs)):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s = torch.cuda.current_stream(dev)
+        a.record(s)
+        if L.probe_stream_read(bufs[r % len(bufs)].data_ptr(), nbytes, scratch.data_ptr(),
+                               blocks, 1, 1, sptr) != 0:
             return None
-    return None
+        b.record(s)
+        torch.cuda.synchronize(dev)
+        ts.append(a.elapsed_time(b))
+    t = float(np.median(ts[len(bufs):]))
+    return {"GBps": round(nbytes / (t * 1e-3) / 1e9, 1),
+            "what": f"stream read of the same {nbytes / 1e9:.3f} GB frame buffer"
+                    f"{'s' if len(bufs) > 1 else ''} (real bytes, headers and padding "
+                    f"included), tools/hbm_probe.hip, median of {len(ts) - len(bufs)}"}
+
+
+def digest_check(cfg, out, count, world, rank, dist, sdev):
+    """SHA-256 of the timed output against the digest the REFERENCE produced
+    over the same synthetic frames (tests/golden/digests.json, made by
+    tests/golden/make_golden.py with the compiled checksum.h).  Config 5 is
+    one job sharded by bytes: every rank's output is gathered to rank 0 and
+    the concatenation must equal the single-job digest.  Weak-scaling configs
+    give rank r frames r*n..: rank 0's batch is the digested one."""
+    import hashlib
+    path = os.path.join(ROOT, "tests", "golden", "digests.json")
+    key = f"config{cfg['id']}"
+    if not os.path.exists(path):
+        return None
+    want = json.load(open(path)).get(key, {}).get("sha256_out")
+    if not want:
+        return None
+    import torch
+    mine = out[:count].view(torch.uint8) if count else out[:0].view(torch.uint8)
+    if cfg["shard"] and world > 1:
+        cnt = torch.tensor([count], dtype=torch.int64, device=sdev)
+        cnts = [torch.zeros_like(cnt) for _ in range(world)]
+        dist.all_gather(cnts, cnt)
+        cmax = max(int(c) for c in cnts)
+        pad = torch.zeros(2 * cmax, dtype=torch.uint8, device=sdev)
+        pad[:2 * count] = mine.to(sdev)
+        parts = [torch.zeros_like(pad) for _ in range(world)]
+        dist.all_gather(parts, pad)
+        if rank != 0:
+            return None
+        blob = b"".join(p[:2 * int(c)].cpu().numpy().tobytes() for p, c in zip(parts, cnts))
+        what = f"{key} sha256_out over the concatenated outputs of {world} ranks"
+    else:
+        if rank != 0:
+            return None
+        blob = mine.cpu().numpy().tobytes()
+        what = f"{key} sha256_out over rank 0's timed output"
+    return {"ok": hashlib.sha256(blob).hexdigest() == want, "what": what}
 
 
 def main():
@@ -167,7 +294,13 @@ def main():
                     help="process group for the barrier / timing reductions (nccl = RCCL)")
     ap.add_argument("--same-device", action="store_true",
                     help="rehearsal only: every rank on cuda:0 (1-GPU box)")
-    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--reps", type=int, default=5,
+                    help="timed repetitions of the K steps (the median is reported)")
+    ap.add_argument("--ramp-ms", type=float, default=300.0,
+                    help="untimed back-to-back K-step bodies before timing (clock ramp)")
+    ap.add_argument("--no-ceiling", action="store_true",
+                    help="skip the same-run streaming-read ceiling probe")
     args = ap.parse_args()
 
     import torch
@@ -222,49 +355,83 @@ def main():
                     eng.batch_device(bufs[k % len(bufs)], d_desc, count, out, cfg["mode"], 0,
                                      len_hint, stream=cptr)
             stream.wait_stream(cap)
-            graph.replay()  # warm replay
             torch.cuda.synchronize(dev)
         except Exception as e:  # capture unsupported: fall back to eager launches
             print(f"note: graph capture failed ({e}); timing eager launches", file=sys.stderr)
             graph = None
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-           for _ in range(1 if graph is not None else args.steps)]
-    torch.cuda.synchronize(dev)
-    barrier()
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    if graph is not None:
-        evs[0][0].record(stream)
-        graph.replay()
-        evs[0][1].record(stream)
-    else:
-        for k in range(args.steps):
-            evs[k][0].record(stream)
-            step(k)
-            evs[k][1].record(stream)
-    torch.cuda.synchronize(dev)
-    barrier()
-    t1 = time.perf_counter()
-    elapsed = t1 - t0
-    if graph is not None:
-        # HIP events around the replayed launches on the stream they run on;
-        # per launch = region / K (includes the ~1 us graph node boundaries)
-        kern_ms = evs[0][0].elapsed_time(evs[0][1]) / args.steps
-    else:
-        kern_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
 
-    # whole-job numbers: max elapsed over ranks, sum of bytes over ranks
+    def run_k():
+        """the K steps, enqueued on `stream`"""
+        if graph is not None:
+            graph.replay()
+        else:
+            for k in range(args.steps):
+                step(k)
+
+    # Clock ramp (untimed): the GPU's clocks take tens of milliseconds of
+    # sustained load to reach their working point; a few warm-up launches
+    # (the driver's --warmup 5 is ~1 ms of work) leave the timed region on a
+    # ramping clock (round 1: 274 us first replays vs 241 us steady).  So the
+    # K-step body runs back to back for at least --ramp-ms of wall time
+    # before anything is timed, whatever --warmup says.
+    torch.cuda.synchronize(dev)
+    t_r = time.perf_counter()
+    n_ramp = 0
+    while True:
+        run_k()
+        torch.cuda.synchronize(dev)
+        n_ramp += 1
+        ramp_ms = (time.perf_counter() - t_r) * 1e3
+        if ramp_ms >= args.ramp_ms and n_ramp >= 2:
+            break
+    # clocks while the kernel is running: enqueue ~40 ms more, sample, drain
+    per_body = ramp_ms / n_ramp
+    for _ in range(max(1, int(40.0 / max(per_body, 1e-3)))):
+        run_k()
+    clocks_load = gpu_clocks(dev)
+    torch.cuda.synchronize(dev)
+
+    # Timed region: R repetitions of exactly K steps, each bracketed by a
+    # barrier and a device synchronize on both sides; the reported step time
+    # is the median repetition (max over ranks per repetition).
+    reps = max(1, args.reps)
+    walls, kms = [], []
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          for _ in range(reps)]
+    for r in range(reps):
+        torch.cuda.synchronize(dev)
+        barrier()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        ev[r][0].record(stream)
+        run_k()
+        ev[r][1].record(stream)
+        torch.cuda.synchronize(dev)
+        barrier()
+        t1 = time.perf_counter()
+        walls.append(t1 - t0)
+    for r in range(reps):
+        # HIP events around the K launches on the stream they run on; per
+        # launch = region / K (includes the ~1 us graph node boundaries)
+        kms.append(ev[r][0].elapsed_time(ev[r][1]) / args.steps)
+    clocks_after = gpu_clocks(dev)
+
+    # whole-job numbers: per repetition the max elapsed over ranks, then the
+    # median repetition; bytes summed over ranks
     sdev = dev if args.dist_backend == "nccl" else torch.device("cpu")
-    stats = torch.tensor([elapsed, float(alg), float(count), kern_ms], dtype=torch.float64,
-                         device=sdev)
+    wt = torch.tensor(walls, dtype=torch.float64, device=sdev)
+    tot = torch.tensor([float(alg), float(count)], dtype=torch.float64, device=sdev)
     if world > 1:
-        tmax = stats[0:1].clone()
-        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
-        tot = stats[1:3].clone()
+        dist.all_reduce(wt, op=dist.ReduceOp.MAX)
         dist.all_reduce(tot, op=dist.ReduceOp.SUM)
-        elapsed_max, alg_all, frames_all = float(tmax[0]), float(tot[0]), float(tot[1])
-    else:
-        elapsed_max, alg_all, frames_all = elapsed, float(alg), float(count)
+    walls_max = [float(x) for x in wt.cpu()]
+    elapsed_max = float(np.median(walls_max))
+    alg_all, frames_all = float(tot[0]), float(tot[1])
+    kern_ms = float(np.median(kms))
+
+    ceiling = None
+    if rank == 0 and not args.no_ceiling:
+        ceiling = stream_ceiling(torch, dev, bufs, sptr)
 
     # parity spot check of the timed output (rank's last buffer pass)
     ok = None
@@ -275,11 +442,19 @@ def main():
         ubytes = int(desc["addr"][m - 1]) + int(desc["len"][m - 1])
         hu = bufs[0][:ubytes].cpu().numpy()
         ok = bool(np.array_equal(got, oracle.batch(hu, desc[:m], cfg["mode"])))
+    digest = digest_check(cfg, out, count, world, rank, dist, sdev)
 
     if rank == 0:
         value = alg_all * args.steps / elapsed_max / 2**30
         achieved = alg / (kern_ms * 1e-3) / 1e9  # GB/s, this rank's kernel
-        traffic = pmc_traffic(args.config) if args.config in CONFIGS else None
+        traffic, traffic_src = pmc_traffic(args.config, args.layout)
+        roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                "traffic": traffic, "traffic_source": traffic_src}
+        if ceiling:
+            roof["ceiling_measured"] = ceiling["GBps"]
+            roof["frac_vs_ceiling"] = round(achieved / ceiling["GBps"], 4)
+            roof["ceiling_probe"] = ceiling["what"]
         line = {
             "metric": "device-resident UDP checksum GiB/s + %HBM-peak, 1M x 1472B IPv4 packets"
                       if args.config == 2 else f"device-resident UDP checksum GiB/s (config "
@@ -307,11 +482,16 @@ def main():
             "pct_hbm_peak": round(100 * achieved / HBM_PEAK_GBS, 2),
             "mpps": round(frames_all * args.steps / elapsed_max / 1e6, 1),
             "kernel_ms": round(kern_ms, 4),
-            "timing": "hipGraph replay of the K launches" if graph is not None else "eager",
+            "kernel_ms_reps": [round(x, 4) for x in kms],
+            "wall_ms_reps": [round(x * 1e3, 4) for x in walls_max],
+            "timing": (f"median of {reps} repetitions of the K steps "
+                       f"({'hipGraph replay' if graph is not None else 'eager launches'}), "
+                       f"each bracketed by barrier + synchronize"),
+            "clock_ramp_ms": round(ramp_ms, 1),
+            "clocks": {"under_load": clocks_load, "after_timing": clocks_after},
             "parity_spot_check": ok,
-            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                         "traffic": traffic},
+            "parity_digest": digest,
+            "roofline": roof,
         }
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(cfg, args.cpu_seconds)
