@@ -105,6 +105,8 @@ extern "C" int xcsum_ctx_create(int device, xcsum_ctx **out)
 		c->h_out[s] = nullptr;
 		c->d_rx_msgs[s] = nullptr;
 		c->h_rx_msgs[s] = nullptr;
+		c->h_stage[s] = nullptr;
+		c->h_dstage[s] = nullptr;
 	}
 	c->frame_cap = 0;
 	c->desc_cap = 0;
@@ -126,6 +128,10 @@ static void free_staging(xcsum_ctx *c)
 		if (c->h_out[s]) (void)hipHostFree(c->h_out[s]);
 		if (c->d_rx_msgs[s]) (void)hipFree(c->d_rx_msgs[s]);
 		if (c->h_rx_msgs[s]) (void)hipHostFree(c->h_rx_msgs[s]);
+		if (c->h_stage[s]) (void)hipHostFree(c->h_stage[s]);
+		if (c->h_dstage[s]) (void)hipHostFree(c->h_dstage[s]);
+		c->h_stage[s] = nullptr;
+		c->h_dstage[s] = nullptr;
 		c->d_rx_msgs[s] = nullptr;
 		c->h_rx_msgs[s] = nullptr;
 		c->streams[s] = nullptr;
@@ -468,6 +474,13 @@ static void retire(const Pending &pd, const uint16_t *h_res, uint8_t *h_umem,
 			const struct xcsum_desc &d = h_desc[pd.first + i];
 			uint8_t *eth = h_umem + d.addr;
 			int fam = host_family(eth, mode);
+			/* frames the kernel rejects as malformed (resolve(): too short
+			 * for the headers, or a UDP length past 16 bits) are left
+			 * untouched, as on the device path: for a truncated frame the
+			 * check field's offset may lie in the next frame */
+			const uint32_t hdr = fam == 6 ? 54u : 34u;
+			if (d.len < hdr + 8u || d.len - hdr > 65535u)
+				continue;
 			if (fam == 6) {
 				memcpy(eth + 60, &res[i], 2);
 			} else if (fam == 4) {
@@ -482,7 +495,7 @@ static void retire(const Pending &pd, const uint16_t *h_res, uint8_t *h_umem,
 namespace xcsum {
 
 int batch_host_impl(xcsum_ctx *c, uint8_t *h_umem, const struct xcsum_desc *h_desc, uint32_t n,
-		    uint16_t *h_out, uint16_t *h_out_ip, uint32_t mode, uint32_t flags)
+		    uint16_t *h_out, uint16_t *h_out_ip, uint32_t mode, uint32_t flags, bool gather)
 {
 	if (!c || mode > XCSUM_MODE_AUTO)
 		return -XCSUM_ERR_INVAL;
@@ -511,6 +524,19 @@ int batch_host_impl(xcsum_ctx *c, uint8_t *h_umem, const struct xcsum_desc *h_de
 			return -XCSUM_ERR_NOT_REGISTERED;
 	}
 
+	if (zc)
+		gather = false;
+	if (gather) {
+		for (int s = 0; s < Ctx::NSLOT; s++) {
+			if (!c->h_stage[s] && hipHostMalloc(&c->h_stage[s], c->frame_cap, 0) != hipSuccess)
+				return -XCSUM_ERR_NOMEM;
+			if (!c->h_dstage[s] &&
+			    hipHostMalloc(&c->h_dstage[s], c->desc_cap * sizeof(struct xcsum_desc), 0) !=
+				    hipSuccess)
+				return -XCSUM_ERR_NOMEM;
+		}
+	}
+
 	/* zero-copy + INPLACE: the kernel already wrote the host frames */
 	const uint32_t rflags = zc ? (flags & ~XCSUM_F_INPLACE) : flags;
 	Pending pend[Ctx::NSLOT];
@@ -519,13 +545,28 @@ int batch_host_impl(xcsum_ctx *c, uint8_t *h_umem, const struct xcsum_desc *h_de
 
 	uint32_t i = 0;
 	int slot = 0;
+	/* staged offset of a gathered frame: packed, each at its UMEM 16-byte
+	 * phase (the kernel sees the same address parity and alignment) */
+	auto stage_off = [](uint64_t pos, uint64_t addr) {
+		return ((pos + 15) & ~(uint64_t)15) + (addr & 15);
+	};
 	while (i < n) {
-		/* grow a chunk: <= desc_cap frames, UMEM range <= frame_cap */
+		/* grow a chunk: <= desc_cap frames, UMEM range (or gathered bytes)
+		 * <= frame_cap */
 		uint64_t lo = h_desc[i].addr, hi = h_desc[i].addr + h_desc[i].len;
-		if (!zc && hi - lo > c->frame_cap)
+		if (!zc && hi - lo > c->frame_cap - 16)
 			return -XCSUM_ERR_INVAL;
 		uint32_t cnt = 1;
-		while (i + cnt < n && cnt < c->desc_cap) {
+		uint64_t gpos = stage_off(0, lo) + h_desc[i].len;   /* gathered bytes so far */
+		while (gather && i + cnt < n && cnt < c->desc_cap) {
+			const struct xcsum_desc &d = h_desc[i + cnt];
+			const uint64_t e = stage_off(gpos, d.addr) + d.len;
+			if (e > c->frame_cap)
+				break;
+			gpos = e;
+			cnt++;
+		}
+		while (!gather && i + cnt < n && cnt < c->desc_cap) {
 			const struct xcsum_desc &d = h_desc[i + cnt];
 			uint64_t nlo = d.addr < lo ? d.addr : lo;
 			uint64_t nhi = d.addr + d.len > hi ? d.addr + d.len : hi;
@@ -554,6 +595,22 @@ int batch_host_impl(xcsum_ctx *c, uint8_t *h_umem, const struct xcsum_desc *h_de
 			a.bias = 0;
 			a.flags = flags & (XCSUM_F_INPLACE | XCSUM_F_IPHDR | XCSUM_F_V4_RFC |
 					   XCSUM_F_VERIFY);
+		} else if (gather) {
+			/* each frame copied on its own into the pinned stage, then
+			 * one DMA of the packed bytes and one of their descriptors */
+			uint64_t pos = 0;
+			for (uint32_t k = 0; k < cnt; k++) {
+				const struct xcsum_desc &d = h_desc[i + k];
+				const uint64_t off = stage_off(pos, d.addr);
+				memcpy(c->h_stage[slot] + off, h_umem + d.addr, d.len);
+				c->h_dstage[slot][k] = xcsum_desc{off, d.len, 0};
+				pos = off + d.len;
+			}
+			HIPCHK(hipMemcpyAsync(c->d_frames[slot], c->h_stage[slot], pos,
+					      hipMemcpyHostToDevice, st));
+			a.umem = c->d_frames[slot];
+			a.bias = 0;
+			a.flags = flags & (XCSUM_F_IPHDR | XCSUM_F_V4_RFC | XCSUM_F_VERIFY);
 		} else {
 			/* 16-byte aligned copy of [lo, hi) keeps every frame's address
 			 * parity and 16-byte phase identical to the host UMEM */
@@ -565,9 +622,9 @@ int batch_host_impl(xcsum_ctx *c, uint8_t *h_umem, const struct xcsum_desc *h_de
 			/* the device copy is scratch: in-place writes happen on the host */
 			a.flags = flags & (XCSUM_F_IPHDR | XCSUM_F_V4_RFC | XCSUM_F_VERIFY);
 		}
-		HIPCHK(hipMemcpyAsync(c->d_desc[slot], h_desc + i, cnt * sizeof(struct xcsum_desc),
-				      hipMemcpyHostToDevice, st));
-		uint32_t avg = (uint32_t)((hi - lo) / cnt);
+		HIPCHK(hipMemcpyAsync(c->d_desc[slot], gather ? c->h_dstage[slot] : h_desc + i,
+				      cnt * sizeof(struct xcsum_desc), hipMemcpyHostToDevice, st));
+		uint32_t avg = (uint32_t)((gather ? gpos : hi - lo) / cnt);
 		HIPCHK(launch_csum(a, geometry_for(c, avg), c->cus, st));
 		HIPCHK(hipMemcpyAsync(c->h_out[slot], c->d_out[slot],
 				      (want_ip ? 2 : 1) * cnt * sizeof(uint16_t),

@@ -100,8 +100,13 @@ struct Geometry {
 };
 
 Geometry pick_geometry(uint32_t len_hint);
+/* gather: stage each frame on its own (pinned host copy, frames packed)
+ * instead of copying the UMEM range the chunk's frames span -- for frames
+ * that are not known to lie in one mapped buffer (the packet.c mirror's
+ * absolute pointers) and to move only the bytes the kernel reads */
 int batch_host_impl(struct xcsum_ctx *c, uint8_t *h_umem, const struct xcsum_desc *h_desc,
-		    uint32_t n, uint16_t *h_out, uint16_t *h_out_ip, uint32_t mode, uint32_t flags);
+		    uint32_t n, uint16_t *h_out, uint16_t *h_out_ip, uint32_t mode, uint32_t flags,
+		    bool gather = false);
 bool geometry_supported(Geometry g);
 hipError_t launch_csum(const CsumArgs &a, Geometry g, int cus, hipStream_t s);
 hipError_t launch_gen(uint8_t *d_umem, const struct xcsum_desc *d_desc, uint32_t n,
@@ -137,6 +142,8 @@ struct Ctx {
 	uint16_t *h_out[NSLOT];        /* pinned */
 	struct xcsum_rx_msg *d_rx_msgs[NSLOT];  /* receive records (lazy) */
 	struct xcsum_rx_msg *h_rx_msgs[NSLOT];  /* pinned */
+	uint8_t *h_stage[NSLOT];       /* gathered frames (pinned, lazy) */
+	struct xcsum_desc *h_dstage[NSLOT];     /* their descriptors (pinned, lazy) */
 	size_t frame_cap;              /* bytes per slot */
 	uint32_t desc_cap;             /* frames per slot */
 };

@@ -32,21 +32,11 @@
  *     preloaded), the rest of a jumbo frame streams in a tail loop.
  */
 #include "xcsum_internal.h"
+#include "xcsum_device.h"
 #include "xcsum_gen.h"
 #include <stdlib.h>
 
 namespace xcsum {
-
-typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-
-static __device__ __forceinline__ uint32_t dot_even(uint32_t w, uint32_t acc)
-{
-	return __builtin_amdgcn_udot4(w, 0x00010001u, acc, false);
-}
-static __device__ __forceinline__ uint32_t dot_odd(uint32_t w, uint32_t acc)
-{
-	return __builtin_amdgcn_udot4(w, 0x01000100u, acc, false);
-}
 
 /* Per-frame geometry: the span [lo, hi) is covered by nchunks 16-byte
  * chunks from base, with `head` bytes before lo in the first chunk and
@@ -71,12 +61,11 @@ struct Frame {
 	int mode;               /* 0 legacy, 1 rfc, 2 v6, -1 malformed, -2 absent */
 	uint32_t ck;            /* VERIFY: the frame's udp->check (raw 16 bits),
 				   loaded a pipeline step ahead */
+	uint32_t ul;            /* VERIFY: udp->len (raw 16 bits), same load step */
 	uint32_t ih[6];         /* IPHDR: the dwords holding the IPv4 header
 				   [eth+14, eth+34), loaded a step ahead */
 	uint32_t ihs;           /* byte phase of eth+14 in ih[0] */
 };
-
-typedef __attribute__((address_space(1))) const u32x4 gu32x4;
 
 /* 16 zero bytes: lanes past the end of their frame load these, so the
  * accumulation needs no data masking (one select per chunk) */
@@ -134,6 +123,27 @@ static __device__ __forceinline__ u32x4 load_desc(const CsumArgs &a, uint32_t p)
 	return *((gu32x4 *)(a.desc + q));
 }
 
+/* chunk grid of the span [lo, hi) (see the Frame comment) */
+template <bool DW>
+static __device__ __forceinline__ void set_span(Frame &f, uintptr_t lo, uintptr_t hi)
+{
+	f.odd = (uint32_t)lo & 1u;
+	if (DW) {
+		const uintptr_t e4 = (hi + 3) & ~(uintptr_t)3;
+		f.nchunks = (uint32_t)(e4 - lo + 15) >> 4;
+		const uintptr_t base = e4 - 16u * f.nchunks;
+		f.base = (const uint8_t *)base;
+		f.head = (uint32_t)(lo - base);
+		f.tail = (uint32_t)(e4 - hi);
+	} else {
+		const uintptr_t base = lo & ~(uintptr_t)15;
+		f.nchunks = (uint32_t)(hi - base + 15) >> 4;
+		f.base = (const uint8_t *)base;
+		f.head = (uint32_t)(lo - base);
+		f.tail = (f.nchunks << 4) - (uint32_t)(hi - base);
+	}
+}
+
 template <bool DW, bool IPH>
 static __device__ __forceinline__ Frame resolve(const CsumArgs &a, u32x4 d, bool present)
 {
@@ -158,22 +168,7 @@ static __device__ __forceinline__ Frame resolve(const CsumArgs &a, u32x4 d, bool
 		mode = -1;
 	uintptr_t lo = (uintptr_t)f.eth + hdr - pre;
 	f.udp_len = len - hdr;
-	const uintptr_t hi = lo + (len + pre - hdr);
-	f.odd = (uint32_t)lo & 1u;
-	if (DW) {
-		const uintptr_t e4 = (hi + 3) & ~(uintptr_t)3;
-		f.nchunks = (uint32_t)(e4 - lo + 15) >> 4;
-		const uintptr_t base = e4 - 16u * f.nchunks;
-		f.base = (const uint8_t *)base;
-		f.head = (uint32_t)(lo - base);
-		f.tail = (uint32_t)(e4 - hi);
-	} else {
-		const uintptr_t base = lo & ~(uintptr_t)15;
-		f.nchunks = (uint32_t)(hi - base + 15) >> 4;
-		f.base = (const uint8_t *)base;
-		f.head = (uint32_t)(lo - base);
-		f.tail = (f.nchunks << 4) - (uint32_t)(hi - base);
-	}
+	set_span<DW>(f, lo, lo + (len + pre - hdr));
 	if (mode < 0 || !present)
 		f.nchunks = 0;
 	f.mode = present ? mode : -2;
@@ -183,9 +178,15 @@ static __device__ __forceinline__ Frame resolve(const CsumArgs &a, u32x4 d, bool
 	 * until then: any branch or arithmetic on it here makes the compiler
 	 * wait for the load on the spot. */
 	f.ck = 0;
-	if (a.flags & XCSUM_F_VERIFY)   /* wave-uniform: no load otherwise */
-		f.ck = *(const uint16_t *)(f.nchunks ? f.eth + (mode == 2 ? 60 : 40)
-						     : (const uint8_t *)g_zero_chunk);
+	f.ul = 0;
+	if (a.flags & XCSUM_F_VERIFY) { /* wave-uniform: no load otherwise */
+		/* udp->len too: a received frame may carry Ethernet padding, so
+		 * the span ends at udp + ntohs(udp->len), not at the frame end */
+		const uint8_t *u = f.nchunks ? f.eth + (mode == 2 ? 58 : 38)
+					     : (const uint8_t *)g_zero_chunk;
+		f.ul = *(const uint16_t *)u;
+		f.ck = *(const uint16_t *)(u + 2);
+	}
 	/* IPHDR: the IPv4 header too (six dwords, same reasoning) */
 	if (IPH && (a.flags & XCSUM_F_IPHDR)) {
 		const uint8_t *ih = f.nchunks && mode != 2 ? f.eth + 14
@@ -199,15 +200,6 @@ static __device__ __forceinline__ Frame resolve(const CsumArgs &a, u32x4 d, bool
 	return f;
 }
 
-
-/* whole 16-byte chunk into E (bytes at even addresses) and O (odd) */
-static __device__ __forceinline__ void accum(u32x4 v, uint32_t &E, uint32_t &O)
-{
-	E = dot_even(v.x, E); O = dot_odd(v.x, O);
-	E = dot_even(v.y, E); O = dot_odd(v.y, O);
-	E = dot_even(v.z, E); O = dot_odd(v.z, O);
-	E = dot_even(v.w, E); O = dot_odd(v.w, O);
-}
 
 /* Edge masks, applied to the chunks before they are summed: the first
  * chunk keeps bytes [head, 16), the last keeps all but the top `tail` bytes
@@ -376,38 +368,6 @@ struct Grid {
 	static constexpr bool DW = XCSUM_GRID_DW || (!(G == 16 && K >= 6) && !(G == 8 && K >= 12));
 };
 
-/* Sum over each aligned group of G lanes, result in every lane of the group.
- * DPP adds within a 16-lane row (quad_perm xor 1, xor 2, row_half_mirror,
- * row_mirror), then gfx950's v_permlane16_swap / v_permlane32_swap across
- * rows: ~8 VALU instructions for 64 lanes, no LDS round trip.  Must run with
- * every lane of the wave active. */
-template <int G>
-static __device__ __forceinline__ uint32_t seg_sum(uint32_t v)
-{
-	if (G >= 2)
-		v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false); /* ^1 */
-	if (G >= 4)
-		v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, false); /* ^2 */
-	if (G >= 8)
-		v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x141, 0xF, 0xF, false);
-	if (G >= 16)
-		v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x140, 0xF, 0xF, false);
-	if (G >= 32) {
-		auto p = __builtin_amdgcn_permlane16_swap(v, v, false, false);
-		v = p[0] + p[1];
-	}
-	if (G >= 64) {
-		auto q = __builtin_amdgcn_permlane32_swap(v, v, false, false);
-		v = q[0] + q[1];
-	}
-	return v;
-}
-
-static __device__ __forceinline__ uint16_t bswap16(uint32_t x)
-{
-	return (uint16_t)(((x >> 8) & 0xffu) | ((x & 0xffu) << 8));
-}
-
 static __device__ __forceinline__ void store_u16(uint8_t *p, uint16_t v)
 {
 	if (((uintptr_t)p & 1) == 0) {
@@ -518,7 +478,8 @@ static __device__ __forceinline__ void finalize(const CsumArgs &a, const Frame &
 				a.out_ip[p] = ipc;
 		}
 	} else {
-		atomicAdd(a.err, 1ull);
+		if (f.mode != -3)        /* -3: UDP length does not fit (VERIFY) */
+			atomicAdd(a.err, 1ull);
 		if (a.flags & XCSUM_F_VERIFY)
 			wire = 0xffffu;  /* a malformed frame never verifies */
 	}
@@ -549,6 +510,41 @@ static __device__ __forceinline__ uint32_t fidx(const CsumArgs &a, uint32_t p)
 	return ORD ? frame_of(a.ord, p) : p;
 }
 
+/* VERIFY on a received frame whose UDP length is not the descriptor's
+ * (Ethernet padding, or a length that does not fit): true if the span must
+ * be re-cut before summing.  Reading f.ul waits for its load, which was
+ * issued before this step's chunks, so it costs no extra round trip. */
+static __device__ __forceinline__ bool verify_recut(const CsumArgs &a, const Frame &f)
+{
+	if (!(a.flags & XCSUM_F_VERIFY) || f.mode < 0)
+		return false;
+	return bswap16(f.ul) != f.udp_len;
+}
+
+/* Re-cut f's span to end at udp + ntohs(udp->len) (RFC 768: the pseudo
+ * header and the sum use the UDP length; trailing bytes are link padding),
+ * or fail the frame (mode -3: out 0xffff, not counted as malformed) when
+ * that length is below 8 or runs past the frame.  Branch-free, every field
+ * written through a select: a conditional update of some fields made the
+ * compiler keep the Frame in scratch memory. */
+template <bool DW>
+static __device__ __forceinline__ void verify_span(Frame &f, bool recut)
+{
+	const uint32_t ul = bswap16(f.ul);
+	const bool bad = ul < 8u || ul > f.udp_len;
+	const uint32_t pre = f.mode == 2 ? 32u : 8u;
+	const uintptr_t lo = (uintptr_t)f.eth + (f.mode == 2 ? 54u : 34u) - pre;
+	Frame g = f;
+	set_span<DW>(g, lo, lo + pre + ul);
+	f.base = recut ? g.base : f.base;
+	f.head = recut ? g.head : f.head;
+	f.tail = recut ? g.tail : f.tail;
+	f.odd = recut ? g.odd : f.odd;
+	f.nchunks = recut ? (bad ? 0u : g.nchunks) : f.nchunks;
+	f.udp_len = recut ? ul : f.udp_len;
+	f.mode = recut && bad ? -3 : f.mode;
+}
+
 template <int G, int U, int K, bool TAIL, bool ORD, bool IPH>
 static __device__ __forceinline__ void consume(const CsumArgs &a, const Frame (&fc)[U],
 					       const u32x4 (&vc)[U][K], uint32_t lane,
@@ -556,12 +552,27 @@ static __device__ __forceinline__ void consume(const CsumArgs &a, const Frame (&
 {
 #pragma unroll
 	for (int u = 0; u < U; u++) {
-		const Frame &f = fc[u];
 		uint32_t E = 0, O = 0;
-		if (!TAIL || f.nchunks <= K * G)
+		if (!TAIL) {
+			const Frame &f = fc[u];
 			sum_frame<G, K, U, Grid<G, K>::DW>(f, vc[u], lane, E, O);
+			uint32_t s = f.odd ? (O << 8) + E : (E << 8) + O;
+			s = seg_sum<G>(s);
+			if (lane == 0 && f.mode != -2)
+				finalize<IPH>(a, f, fidx<ORD>(a, p0 + u * nseg), s);
+			continue;
+		}
+		/* the uniform slow path: jumbo frames walk their chunks; VERIFY
+		 * frames with a UDP length != the descriptor's are re-cut, and then
+		 * the preloaded chunks no longer fit either */
+		Frame f = fc[u];
+		const bool recut = verify_recut(a, f);
+		if (a.flags & XCSUM_F_VERIFY)   /* wave-uniform */
+			verify_span<Grid<G, K>::DW>(f, recut);
+		if (f.nchunks > K * G || recut)
+			sum_walk<G, Grid<G, K>::DW>(f, lane, E, O);
 		else
-			sum_walk<G, Grid<G, K>::DW>(f, lane, E, O);   /* jumbo frame */
+			sum_frame<G, K, U, Grid<G, K>::DW>(f, vc[u], lane, E, O);
 		uint32_t s = f.odd ? (O << 8) + E : (E << 8) + O;
 		s = seg_sum<G>(s);
 		if (lane == 0 && f.mode != -2)
@@ -585,7 +596,7 @@ static __device__ __forceinline__ void consume_any(const CsumArgs &a, const Fram
 	bool big = false;
 #pragma unroll
 	for (int u = 0; u < U; u++)
-		big |= fc[u].nchunks > K * G;
+		big |= fc[u].nchunks > K * G || verify_recut(a, fc[u]);
 	if (__builtin_amdgcn_ballot_w64(big))
 		consume<G, U, K, true, ORD, IPH>(a, fc, vc, lane, p0, nseg);
 	else
@@ -787,9 +798,12 @@ __global__ void __launch_bounds__(256) csum_lds_kernel(CsumArgs a)
 			__builtin_amdgcn_sched_barrier(0);
 			issue_stage(fn, d);
 			__builtin_amdgcn_sched_barrier(0);
-			const Frame &f = fs[d];
+			Frame f = fs[d];
 			uint32_t E = 0, O = 0;
-			if (__builtin_amdgcn_ballot_w64(f.nchunks > K * G))
+			const bool recut = verify_recut(a, f);
+			if (a.flags & XCSUM_F_VERIFY)
+				verify_span<Grid<G, K>::DW>(f, recut);
+			if (__builtin_amdgcn_ballot_w64(f.nchunks > K * G || recut))
 				sum_walk<G, Grid<G, K>::DW>(f, lane, E, O);
 			else
 				sum_frame<G, K, 2, Grid<G, K>::DW>(f, v, lane, E, O);
@@ -807,16 +821,16 @@ template <int K, int D>
 static hipError_t launch_lds_t(const CsumArgs &a, int cus, int bpc, hipStream_t s)
 {
 	const size_t lds = (size_t)4 * D * K * 64 * 16;
-	static int occ = 0;
-	if (!occ) {
+	static std::atomic<int> occ_cache[OCC_MAX_DEVICES];
+	const int occ = occupancy_cached(occ_cache, [&] {
 		int nb = 0;
 		(void)hipFuncSetAttribute((const void *)csum_lds_kernel<K, D>,
 					  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
 		if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, csum_lds_kernel<K, D>, 256,
 								 lds) != hipSuccess || nb <= 0)
 			nb = 1;
-		occ = nb;
-	}
+		return nb;
+	});
 	int per_cu = (bpc > 0 && bpc < occ) ? bpc : occ;
 	uint64_t waves = ((uint64_t)a.n + 3) / 4;
 	uint64_t blocks = (waves + 3) / 4;
@@ -861,14 +875,14 @@ static hipError_t launch_t(const CsumArgs &a, int cus, int bpc, hipStream_t s)
 {
 	/* persistent grid: at most what the device keeps resident, so no second
 	 * wave of late blocks; fewer per CU when that streams better (Geometry.B) */
-	static int occ = 0;
-	if (!occ) {
+	static std::atomic<int> occ_cache[OCC_MAX_DEVICES];
+	const int occ = occupancy_cached(occ_cache, [] {
 		int nb = 0;
 		if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, csum_kernel<G, U, K, IPH>, 256, 0) !=
 			    hipSuccess || nb <= 0)
 			nb = 4;
-		occ = nb;
-	}
+		return nb;
+	});
 	int per_cu = (bpc > 0 && bpc < occ) ? bpc : occ;
 	uint64_t segs = ((uint64_t)a.ord.nlog + U - 1) / U;
 	uint64_t blocks = (segs * G + 255) / 256;

@@ -44,52 +44,11 @@
  * before a frame whose address is not (it never leaves the frame's dword).
  */
 #include "xcsum_internal.h"
+#include "xcsum_device.h"
 #include <stdio.h>
 #include <stdlib.h>
 
 namespace xcsum {
-
-typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-typedef __attribute__((address_space(1))) const u32x4 gu32x4;
-
-static __device__ __forceinline__ uint32_t dot_even(uint32_t w, uint32_t acc)
-{
-	return __builtin_amdgcn_udot4(w, 0x00010001u, acc, false);
-}
-static __device__ __forceinline__ uint32_t dot_odd(uint32_t w, uint32_t acc)
-{
-	return __builtin_amdgcn_udot4(w, 0x01000100u, acc, false);
-}
-
-static __device__ __forceinline__ void accum(u32x4 v, uint32_t &E, uint32_t &O)
-{
-	E = dot_even(v.x, E); O = dot_odd(v.x, O);
-	E = dot_even(v.y, E); O = dot_odd(v.y, O);
-	E = dot_even(v.z, E); O = dot_odd(v.z, O);
-	E = dot_even(v.w, E); O = dot_odd(v.w, O);
-}
-
-template <int G>
-static __device__ __forceinline__ uint32_t seg_sum(uint32_t v)
-{
-	if (G >= 2)
-		v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false);
-	if (G >= 4)
-		v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, false);
-	if (G >= 8)
-		v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x141, 0xF, 0xF, false);
-	if (G >= 16)
-		v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x140, 0xF, 0xF, false);
-	if (G >= 32) {
-		auto p = __builtin_amdgcn_permlane16_swap(v, v, false, false);
-		v = p[0] + p[1];
-	}
-	if (G >= 64) {
-		auto q = __builtin_amdgcn_permlane32_swap(v, v, false, false);
-		v = q[0] + q[1];
-	}
-	return v;
-}
 
 static __device__ __forceinline__ uint32_t be16(const uint8_t *p)
 {
@@ -1014,8 +973,8 @@ __global__ void __launch_bounds__(256) rx_count_kernel(const uint32_t *part, uin
 template <int G, int K, int U>
 static hipError_t launch_rx_t(const RxArgs &a, int cus, int bpc, hipStream_t s)
 {
-	static int occ = 0;
-	if (!occ) {
+	static std::atomic<int> occ_cache[OCC_MAX_DEVICES];
+	const int occ = occupancy_cached(occ_cache, [] {
 		int nb = 0;
 		hipError_t e;
 		if constexpr (U == 0)
@@ -1024,8 +983,8 @@ static hipError_t launch_rx_t(const RxArgs &a, int cus, int bpc, hipStream_t s)
 			e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, rx_kernel<G, K, U>, 256, 0);
 		if (e != hipSuccess || nb <= 0)
 			nb = 4;
-		occ = nb;
-	}
+		return nb;
+	});
 	/* U == 0: lane-per-frame parse, a wave per 64 frames */
 	uint64_t blocks = U == 0 ? ((uint64_t)a.n + 255) / 256
 				 : (((uint64_t)a.n + (U ? U : 1) - 1) / (U ? U : 1) * G + 255) / 256;

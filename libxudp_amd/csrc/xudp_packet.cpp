@@ -94,11 +94,10 @@ extern "C" int xudp_packet_udp_batch(xcsum_ctx *ctx, struct packet_info *infos, 
 		return 0;
 	if (!infos)
 		return -XCSUM_ERR_INVAL;
-	if (!ctx)
-		ctx = default_ctx();
-	if (!ctx)
-		return -XCSUM_ERR_NODEV;
-
+	/* headers first, as packet.c does: every frame is built (info->packet
+	 * and info->len set, both check fields 0) even if no device can
+	 * checksum it -- the caller then sees the error, never a half-built
+	 * frame */
 	uint8_t *lo = nullptr, *hi = nullptr;
 	for (uint32_t i = 0; i < n; i++) {
 		xudp_packet_build_headers(&infos[i]);
@@ -106,24 +105,38 @@ extern "C" int xudp_packet_udp_batch(xcsum_ctx *ctx, struct packet_info *infos, 
 		if (!lo || p < lo) lo = p;
 		if (!hi || e > hi) hi = e;
 	}
+	if (!ctx)
+		ctx = default_ctx();
+	if (!ctx)
+		return -XCSUM_ERR_NODEV;
 	/* descriptors relative to a registered UMEM when every frame is inside
 	 * one (pinned DMA / zero-copy), else relative to address 0 */
 	uint8_t *base = nullptr;
 	for (auto &r : ctx->regions)
 		if (lo >= r.host && hi <= r.host + r.size)
 			base = r.host;
+	/* IPv4 without XCSUM_F_V4_RFC: udp->check stays 0 (packet.c:125) and
+	 * only iph->check is computed, from the 20-byte header (its tot_len
+	 * field included), so the kernel is handed eth + IP + UDP headers only
+	 * (42 bytes; the UDP result it also returns is not used) */
+	const bool v4_rfc = (flags & XCSUM_F_V4_RFC) != 0;
 	std::vector<struct xcsum_desc> desc(n);
 	std::vector<uint16_t> out(n), out_ip(n);
 	for (uint32_t i = 0; i < n; i++) {
 		desc[i].addr = (uint64_t)((uint8_t *)infos[i].packet - base);
 		desc[i].len = (uint32_t)infos[i].len;
+		if (infos[i].family == AF_INET && !v4_rfc && desc[i].len > 42u)
+			desc[i].len = 42u;
 		desc[i].options = 0;
 	}
 	uint32_t kflags = XCSUM_F_IPHDR | (flags & (XCSUM_F_V4_RFC | XCSUM_F_ZEROCOPY));
 	if (!base)
 		kflags &= ~XCSUM_F_ZEROCOPY;
+	/* staged copies gather frame by frame: the frames are the caller's
+	 * buffers anywhere in memory, and a copy of the address range they
+	 * span could read unmapped pages between them */
 	int rc = xcsum::batch_host_impl(ctx, base, desc.data(), n, out.data(), out_ip.data(),
-					XCSUM_MODE_AUTO, kflags);
+					XCSUM_MODE_AUTO, kflags, !(kflags & XCSUM_F_ZEROCOPY));
 	if (rc)
 		return rc;
 	for (uint32_t i = 0; i < n; i++) {

@@ -255,7 +255,12 @@ static u16 orc_verify(const u8 *frame, u32 len, int fam6, u32 flags)
 	u16 r;
 	if (len < hdr + 8 || len - hdr > 0xffff)
 		return 0xffff;
-	size = len - hdr;
+	/* RFC 768: the UDP length is the header's, not the frame's -- received
+	 * frames may carry Ethernet padding (xudp_fill_msg, group/channel.c:86, reads it the
+	 * same way); a length below 8 or past the frame never verifies */
+	size = ((u32)udp[4] << 8) | udp[5];
+	if (size < 8 || size > len - hdr)
+		return 0xffff;
 	sum = orc_do_csum(udp, size);
 	if (fam6) {
 		sum = orc_udp6_hdr_csum(sum, ip + 8, ip + 24, size);

@@ -5,47 +5,34 @@
  * (oracle/liboracle.so, pinned to the reference by tests/test_oracle.py) and
  * from the reference's known-answer frames.
  *
+ * Also the process model libxudp runs in:
+ *   - fork() before any HIP call (the master/worker model forks its workers,
+ *     test/case/lib.c:169); each child initialises HIP lazily through its own
+ *     context and checks a batch;
+ *   - two host threads, each with its own context and stream on device 0,
+ *     running concurrently (one TX channel per thread, xudp/xsk.c:303-304);
+ *   - the UMEM allocated exactly as xudp does (anon_map, include/common.h:37-41,
+ *     xudp/xsk.c:234), registered, checksummed staged / zero-copy / in place.
+ *
  * Exit 0 = all checks passed, 77 = no GPU (skip), 1 = a check failed.
- * Run by tests/test_gpu_capi.py on the GPU box; built by tests/c/Makefile.
+ * `capi_check --threads` runs only the thread test (the TSan build,
+ * tests/c/Makefile `tsan`).  Run by tests/test_capi.py on the GPU box.
  */
 #define _GNU_SOURCE
 #include <arpa/inet.h>
 #include <netinet/in.h>
+#include <pthread.h>
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <sys/wait.h>
+#include <unistd.h>
 
 #include <hip/hip_runtime_api.h>
 
-#include "xcsum.h"
+#include "harness.h"
 #include "xudp_packet.h"
-
-/* oracle/xcsum_oracle.c (struct orc_desc has the xdp_desc layout) */
-void orc_batch(const uint8_t *umem, const struct xcsum_desc *desc, uint32_t n, uint16_t *out,
-	       int mode, uint32_t flags);
-
-static int failures;
-static int checks;
-
-#define CHECK(cond, ...)                                                   \
-	do {                                                               \
-		checks++;                                                  \
-		if (!(cond)) {                                             \
-			failures++;                                        \
-			fprintf(stderr, "FAIL %s:%d: ", __FILE__, __LINE__); \
-			fprintf(stderr, __VA_ARGS__);                      \
-			fputc('\n', stderr);                               \
-		}                                                          \
-	} while (0)
-
-static uint32_t count_diff(const uint16_t *a, const uint16_t *b, uint32_t n)
-{
-	uint32_t d = 0;
-	for (uint32_t i = 0; i < n; i++)
-		d += a[i] != b[i];
-	return d;
-}
 
 static int hex_eq(const uint8_t *p, const char *hex)
 {
@@ -60,14 +47,21 @@ static int hex_eq(const uint8_t *p, const char *hex)
 
 /* Host-resident batches (xcsum_batch_host) and the device path
  * (xcsum_batch_device on hipMalloc'ed frames) against the oracle. */
-static void check_batches(xcsum_ctx *c, uint32_t family, uint32_t stride, uint32_t offset)
+static void check_batches(xcsum_ctx *c, uint32_t family, uint32_t stride, uint32_t offset,
+			  int xudp_map)
 {
 	const uint32_t n = 4000;
 	struct xcsum_desc *desc = calloc(n, sizeof(*desc));
 	uint64_t bytes = 0;
 	CHECK(xcsum_gen_layout(n, family, 0, 3000, 7 + family, 0, 8, stride, offset, desc,
 			       &bytes) == 0, "gen_layout");
-	uint8_t *umem = calloc(bytes + 64, 1);
+	/* xudp_map: the UMEM as xudp maps it (anon_map), else the C heap */
+	int locked = 0;
+	const size_t map_bytes = (bytes + 64 + 4095) & ~(size_t)4095;
+	uint8_t *umem = xudp_map ? xudp_anon_map(map_bytes, &locked) : calloc(bytes + 64, 1);
+	CHECK(umem != NULL, "umem allocation");
+	if (!umem)
+		return;
 	CHECK(xcsum_gen_fill_host(umem, desc, n, family, 7 + family, 0) == 0, "gen_fill_host");
 	uint16_t *exp = calloc(n, 2), *got = calloc(n, 2);
 	const uint32_t mode = family == 6 ? XCSUM_MODE_V6 : XCSUM_MODE_V4_LEGACY;
@@ -78,8 +72,13 @@ static void check_batches(xcsum_ctx *c, uint32_t family, uint32_t stride, uint32
 	CHECK(count_diff(got, exp, n) == 0, "batch_host v%u: %u mismatches", family,
 	      count_diff(got, exp, n));
 
-	/* registered UMEM, zero-copy, results written into the frames */
+	/* registered UMEM: staged copies through the pinned mapping ... */
 	CHECK(xcsum_register_umem(c, umem, bytes + 64) == 0, "register_umem");
+	memset(got, 0, 2 * n);
+	CHECK(xcsum_batch_host(c, umem, desc, n, got, mode, 0) == 0, "batch_host registered");
+	CHECK(count_diff(got, exp, n) == 0, "registered v%u: %u mismatches", family,
+	      count_diff(got, exp, n));
+	/* ... and zero-copy, results written into the frames */
 	memset(got, 0, 2 * n);
 	CHECK(xcsum_batch_host(c, umem, desc, n, got, mode, XCSUM_F_ZEROCOPY | XCSUM_F_INPLACE) ==
 	      0, "batch_host zerocopy");
@@ -148,7 +147,10 @@ static void check_batches(xcsum_ctx *c, uint32_t family, uint32_t stride, uint32
 	(void)hipFree(d_desc);
 	(void)hipFree(d_out);
 	free(desc);
-	free(umem);
+	if (xudp_map)
+		munmap(umem, map_bytes);
+	else
+		free(umem);
 	free(exp);
 	free(got);
 }
@@ -223,8 +225,157 @@ static void check_errors(xcsum_ctx *c)
 	      (unsigned long long)e);
 }
 
-int main(void)
+/* ---- fork: HIP initialised lazily, after fork, in each child ------------- */
+
+/* one small batch through a fresh context, checked against the oracle;
+ * returns the exit status for a child: 0 ok, 1 mismatch, 77 no GPU */
+static int child_batch(uint32_t family, uint64_t seed)
 {
+	xcsum_ctx *c = NULL;
+	int rc = xcsum_ctx_create(-1, &c);
+	if (rc == -XCSUM_ERR_NODEV)
+		return 77;
+	if (rc)
+		return 1;
+	const uint32_t n = 1500;
+	struct xcsum_desc *desc = calloc(n, sizeof(*desc));
+	uint64_t bytes = 0;
+	int ok = xcsum_gen_layout(n, family, 0, 1500, seed, 0, 8, 0, 0, desc, &bytes) == 0;
+	uint8_t *umem = calloc(bytes + 64, 1);
+	ok &= xcsum_gen_fill_host(umem, desc, n, family, seed, 0) == 0;
+	uint16_t *exp = calloc(n, 2), *got = calloc(n, 2);
+	const int mode = family == 6 ? XCSUM_MODE_V6 : XCSUM_MODE_V4_LEGACY;
+	orc_batch(umem, desc, n, exp, mode, 0);
+	ok &= xcsum_batch_host(c, umem, desc, n, got, (uint32_t)mode, 0) == 0;
+	ok &= count_diff(got, exp, n) == 0;
+	xcsum_ctx_destroy(c);
+	free(desc);
+	free(umem);
+	free(exp);
+	free(got);
+	return ok ? 0 : 1;
+}
+
+/* Called first in main(), before this process has made any HIP call: two
+ * workers forked like libxudp's (test/case/lib.c:169), both checksumming at
+ * once; the parent initialises HIP only after they are done.  Returns 77
+ * when no child found a GPU. */
+static int check_fork(void)
+{
+	pid_t pid[2];
+	for (int k = 0; k < 2; k++) {
+		fflush(NULL);
+		pid[k] = fork();
+		if (pid[k] == 0)
+			exit(child_batch(k ? 6 : 4, 100 + (uint64_t)k));
+		CHECK(pid[k] > 0, "fork");
+	}
+	int nodev = 0;
+	for (int k = 0; k < 2; k++) {
+		int st = 0;
+		if (pid[k] <= 0)
+			continue;
+		CHECK(waitpid(pid[k], &st, 0) == pid[k], "waitpid");
+		CHECK(WIFEXITED(st), "worker %d did not exit normally (status 0x%x)", k, st);
+		if (WIFEXITED(st) && WEXITSTATUS(st) == 77)
+			nodev++;
+		else
+			CHECK(WIFEXITED(st) && WEXITSTATUS(st) == 0, "forked worker %d: status 0x%x", k,
+			      st);
+	}
+	return nodev == 2 ? 77 : 0;
+}
+
+/* ---- two host threads, two contexts, two streams, device 0 --------------- */
+
+struct thread_job {
+	uint32_t family;
+	uint64_t seed;
+	int iters;
+	int bad;        /* mismatching iterations */
+	int err;        /* a call failed */
+};
+
+static void *thread_main(void *arg)
+{
+	struct thread_job *j = arg;
+	xcsum_ctx *c = NULL;
+	if (xcsum_ctx_create(0, &c) != 0) {
+		j->err = 1;
+		return NULL;
+	}
+	hipStream_t st = NULL;
+	if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) {
+		j->err = 1;
+		xcsum_ctx_destroy(c);
+		return NULL;
+	}
+	const uint32_t n = 20000;
+	struct xcsum_desc *desc = calloc(n, sizeof(*desc));
+	uint64_t bytes = 0;
+	j->err |= xcsum_gen_layout(n, j->family, 0, 1472, j->seed, 0, 8, 0, 0, desc, &bytes) != 0;
+	uint8_t *umem = calloc(bytes + 64, 1);
+	uint16_t *exp = calloc(n, 2), *got = calloc(n, 2);
+	const uint32_t mode = j->family == 6 ? XCSUM_MODE_V6 : XCSUM_MODE_V4_LEGACY;
+	uint8_t *d_umem = NULL;
+	struct xcsum_desc *d_desc = NULL;
+	uint16_t *d_out = NULL;
+	j->err |= hipMalloc((void **)&d_umem, bytes + 64) != hipSuccess;
+	j->err |= hipMalloc((void **)&d_desc, n * sizeof(*desc)) != hipSuccess;
+	j->err |= hipMalloc((void **)&d_out, 2 * n) != hipSuccess;
+	if (!j->err) {
+		j->err |= hipMemcpyAsync(d_desc, desc, n * sizeof(*desc), hipMemcpyHostToDevice,
+					 st) != hipSuccess;
+		j->err |= xcsum_gen_fill_device(d_umem, d_desc, n, j->family, j->seed, 0, st) != 0;
+		j->err |= xcsum_gen_fill_host(umem, desc, n, j->family, j->seed, 0) != 0;
+		orc_batch(umem, desc, n, exp, (int)mode, 0);
+	}
+	for (int it = 0; it < j->iters && !j->err; it++) {
+		/* device-resident batch on this thread's stream ... */
+		memset(got, 0, 2 * n);
+		j->err |= hipMemsetAsync(d_out, 0, 2 * n, st) != hipSuccess;
+		j->err |= xcsum_batch_device(c, d_umem, d_desc, n, d_out, mode, 0, 0, st) != 0;
+		j->err |= hipMemcpyAsync(got, d_out, 2 * n, hipMemcpyDeviceToHost, st) != hipSuccess;
+		j->err |= xcsum_sync(c, st) != 0;
+		j->bad += count_diff(got, exp, n) != 0;
+		/* ... and a host-resident one through the context's own staging */
+		memset(got, 0, 2 * n);
+		j->err |= xcsum_batch_host(c, umem, desc, n, got, mode, 0) != 0;
+		j->bad += count_diff(got, exp, n) != 0;
+	}
+	(void)hipFree(d_umem);
+	(void)hipFree(d_desc);
+	(void)hipFree(d_out);
+	(void)hipStreamDestroy(st);
+	xcsum_ctx_destroy(c);
+	free(desc);
+	free(umem);
+	free(exp);
+	free(got);
+	return NULL;
+}
+
+static void check_threads(void)
+{
+	struct thread_job jobs[2] = {{4, 31, 25, 0, 0}, {6, 32, 25, 0, 0}};
+	pthread_t th[2];
+	for (int k = 0; k < 2; k++)
+		CHECK(pthread_create(&th[k], NULL, thread_main, &jobs[k]) == 0, "pthread_create");
+	for (int k = 0; k < 2; k++) {
+		pthread_join(th[k], NULL);
+		CHECK(!jobs[k].err, "thread %d: a call failed", k);
+		CHECK(jobs[k].bad == 0, "thread %d: %d of %d iterations mismatched", k, jobs[k].bad,
+		      2 * jobs[k].iters);
+	}
+}
+
+int main(int argc, char **argv)
+{
+	const int threads_only = argc > 1 && strcmp(argv[1], "--threads") == 0;
+	if (!threads_only && check_fork() == 77) {
+		printf("capi_check: no GPU, skipped\n");
+		return 77;
+	}
 	xcsum_ctx *c = NULL;
 	int rc = xcsum_ctx_create(-1, &c);
 	if (rc == -XCSUM_ERR_NODEV) {
@@ -235,11 +386,16 @@ int main(void)
 		fprintf(stderr, "xcsum_ctx_create: %d\n", rc);
 		return 1;
 	}
-	check_batches(c, 4, 0, 0);
-	check_batches(c, 6, 0, 0);
-	check_batches(c, 4, 4096, 342);   /* xudp TX UMEM layout, SURVEY a14 */
-	check_packet_kats();
-	check_errors(c);
+	if (!threads_only) {
+		check_batches(c, 4, 0, 0, 0);
+		check_batches(c, 6, 0, 0, 0);
+		check_batches(c, 4, 4096, 342, 0);   /* xudp TX UMEM layout, SURVEY a14 */
+		check_batches(c, 4, 4096, 342, 1);   /* ... in xudp's own anon_map UMEM */
+		check_batches(c, 6, 4096, 322, 1);
+		check_packet_kats();
+		check_errors(c);
+	}
+	check_threads();
 	xcsum_ctx_destroy(c);
 	printf("capi_check: %d checks, %d failures\n", checks, failures);
 	return failures ? 1 : 0;

@@ -10,6 +10,8 @@ if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 
 GOLDEN = os.path.join(ROOT, "tests", "golden")
+if GOLDEN not in sys.path:
+    sys.path.insert(0, GOLDEN)   # rx_frames, the receive-corpus builder
 
 
 def pytest_configure(config):

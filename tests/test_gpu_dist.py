@@ -1,0 +1,51 @@
+"""GPU: bench.py's N > 1 path on the HIP engine.  Two ranks (gloo, both on
+cuda:0 -- the box has one GPU; on an 8-GPU node the driver runs the same code
+with RCCL, one rank per GPU) launched by torch.distributed.run as a fresh
+child process.  Config 5 is one 8M-frame job sharded by bytes: the ranks'
+outputs, gathered and concatenated, must equal the reference's digest of the
+whole job; config 2 is weak scaling: rank 0's batch is the digested one."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+pytestmark = pytest.mark.gpu
+
+
+def free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def run_dist(config, steps=2):
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()),
+           os.path.join(ROOT, "bench.py"), "--gpus", "2", "--same-device", "--dist-backend",
+           "gloo", "--config", str(config), "--steps", str(steps), "--warmup", "1",
+           "--reps", "2", "--ramp-ms", "0", "--no-ceiling", "--no-cpu-baseline"]
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, cwd=ROOT, env=env)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    return json.loads(lines[0])
+
+
+def test_two_ranks_config5_sharded_digest():
+    line = run_dist(5)
+    assert line["n_gpus"] == 2 and line["config"]["frames_total"] == 8 << 20
+    assert line["parity_digest"]["ok"] is True, line["parity_digest"]
+    assert "concatenated outputs of 2 ranks" in line["parity_digest"]["what"]
+    assert line["parity_spot_check"] is True
+
+
+def test_two_ranks_config2_weak_scaling():
+    line = run_dist(2, steps=4)
+    assert line["n_gpus"] == 2 and line["config"]["frames_total"] == 2 << 20
+    assert line["scaling"] == "weak"
+    assert line["parity_digest"]["ok"] is True

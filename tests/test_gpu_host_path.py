@@ -9,6 +9,7 @@ import pytest
 import libxudp_amd as X
 import oracle
 from conftest import golden_desc
+from test_gpu_parity import run_device
 from test_oracle import KAT3, KAT4
 
 pytestmark = pytest.mark.gpu
@@ -169,3 +170,90 @@ def test_packet_udp_batch_random(engine, register):
         desc = np.zeros(1, dtype=X.DESC_DTYPE)
         desc["len"] = len(f)
         assert int(f[40:42].view("<u2")[0]) == oracle.batch(z, desc, X.MODE_V4_RFC)[0]
+
+
+def _guarded_pages(npages=3, hole=1):
+    """An anonymous mapping of `npages` pages whose page `hole` is PROT_NONE:
+    reading the address range across it faults."""
+    import ctypes
+    import mmap
+    pg = mmap.PAGESIZE
+    mm = mmap.mmap(-1, npages * pg, flags=mmap.MAP_PRIVATE | mmap.MAP_ANONYMOUS,
+                   prot=mmap.PROT_READ | mmap.PROT_WRITE)
+    buf = np.frombuffer(mm, dtype=np.uint8)
+    libc = ctypes.CDLL(None, use_errno=True)
+    libc.mprotect.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+    assert libc.mprotect(buf.ctypes.data + hole * pg, pg, 0) == 0
+    return mm, buf, pg
+
+
+@pytest.mark.parametrize("rfc", [False, True])
+def test_packet_udp_batch_frames_around_unmapped_page(engine, rfc):
+    """Frames in the caller's buffers with an unmapped page between them: the
+    staged path copies frame by frame (the address range they span is not
+    readable), and IPv4 without V4_RFC ships headers only."""
+    mm, buf, pg = _guarded_pages()
+    rng = np.random.default_rng(9)
+    pas = []
+    for fam, off, L in ((4, 100, 1000), (6, 2 * pg + 40, 900), (4, 2 * pg + 2000, 77)):
+        alen = 16 if fam == 6 else 4
+        pa = X.PacketArgs(fam, rng.integers(0, 256, L, dtype=np.uint8).tobytes(), MAC1, MAC2,
+                          rng.integers(0, 256, alen, dtype=np.uint8).tobytes(), 1000 + L,
+                          rng.integers(0, 256, alen, dtype=np.uint8).tobytes(), 2000 + L,
+                          buf=buf, offset=off)
+        buf[off + 64:off + 64 + L] = pa.payload[:L]
+        pas.append(pa)
+    X.packet_udp_batch(engine, pas, X.F_V4_RFC if rfc else 0)
+    for pa in pas:
+        f = pa.frame()
+        z = f.copy()
+        desc = np.zeros(1, dtype=X.DESC_DTYPE)
+        desc["len"] = len(f)
+        if pa.family == 6:
+            z[60:62] = 0
+            assert int(f[60:62].view("<u2")[0]) == oracle.batch(z, desc, X.MODE_V6)[0]
+        else:
+            assert int(f[24:26].view("<u2")[0]) == oracle.ip_header_rfc(f)
+            if rfc:
+                z[40:42] = 0
+                assert int(f[40:42].view("<u2")[0]) == oracle.batch(z, desc, X.MODE_V4_RFC)[0]
+            else:
+                assert f[40:42].tobytes() == b"\0\0"
+    del pas, buf   # the mapping goes with its last view
+
+
+@pytest.mark.parametrize("how", ["device", "pageable", "registered", "zerocopy"])
+def test_inplace_skips_truncated_frame(torch_cuda, engine, how):
+    """INPLACE never writes for a frame the kernel rejects as malformed: a
+    20-byte runt packed right before a valid frame would otherwise get its
+    'udp->check' (runt + 40) stored into the next frame's bytes."""
+    umem, desc = X.gen_frames_host(2, 4, 50, 50, seed=3, align=1)
+    runt = np.zeros(1, dtype=X.DESC_DTYPE)
+    big = np.zeros(len(umem) + 20, dtype=np.uint8)
+    big[20:] = umem
+    big[:20] = 0x33
+    d = np.concatenate([runt, desc])
+    d["addr"][1:] += 20
+    d["len"][0] = 20
+    exp = oracle.batch(big, d, X.MODE_V4_RFC)
+    before = big.copy()
+    engine.take_errors()   # clear what earlier tests left
+    if how == "device":
+        got, after = run_device(torch_cuda, engine, big, d, X.MODE_V4_RFC, X.F_INPLACE)
+    else:
+        after = big
+        flags = X.F_INPLACE
+        if how != "pageable":
+            engine.register_umem(big)
+        if how == "zerocopy":
+            flags |= X.F_ZEROCOPY
+        try:
+            got = host_batch(engine, big, d, X.MODE_V4_RFC, flags)
+        finally:
+            if how != "pageable":
+                engine.unregister_umem(big)
+    assert np.array_equal(got, exp) and got[0] == 0
+    assert engine.take_errors() == 1
+    changed = set(np.nonzero(after != before)[0].tolist())
+    own = {int(a) + k for a in d["addr"][1:] for k in (40, 41)}
+    assert changed <= own            # only the valid frames' own udp->check fields

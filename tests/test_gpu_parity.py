@@ -314,3 +314,63 @@ def test_launch_ignores_stale_hip_error(torch_cuda, engine, golden):
     got, _ = run_device(torch, engine, golden["umem"].copy(), desc, X.MODE_V4_LEGACY)
     assert np.array_equal(got, golden["exp_legacy"][np.nonzero(golden["family"] == 4)[0][:64]])
     torch.cuda.synchronize()
+
+
+# ---- VERIFY on received frames: the span ends at udp + ntohs(udp->len) ----
+
+import rx_frames  # noqa: E402  (tests/golden, put on sys.path by conftest)
+
+
+def received_batch(seed=11):
+    """The receive corpus (Ethernet padding with zeros or junk, udp->len that
+    does not fit, corrupted bytes, IPv4 options, extension headers, junk)
+    plus padded frames of every size class up to jumbo: frames whose
+    descriptor length exceeds the UDP datagram."""
+    rng = np.random.default_rng(seed)
+    frames = [f for f, _ in rx_frames.corpus(seed)]
+    for plen in (0, 3, 17, 40, 100, 700, 1472, 3000, 8990):
+        for pad in (1, 2, 15, 16, 33, 200):
+            frames.append(rx_frames.v4_frame(rng, plen) + rx_frames.rand_bytes(rng, pad))
+            frames.append(rx_frames.v6_frame(rng, plen) + rx_frames.rand_bytes(rng, pad))
+    umem, addr, ln = rx_frames.layout(frames, rng)
+    desc = np.zeros(len(frames), dtype=X.DESC_DTYPE)
+    desc["addr"] = addr
+    desc["len"] = ln
+    return umem, desc
+
+
+@pytest.mark.parametrize("geom", FEATURE_GEOMS + [(16, 2, 6), (4, 1, 2), (64, 1, 9)])
+def test_verify_received_frames(torch_cuda, engine, geom):
+    umem, desc = received_batch()
+    with geometry(engine, geom):
+        for hint in (0, 100, 1500):
+            for mode in (X.MODE_AUTO, X.MODE_V4_RFC, X.MODE_V6):
+                for flags in (X.F_VERIFY, X.F_VERIFY | X.F_IPHDR):
+                    got, after = run_device(torch_cuda, engine, umem, desc, mode, flags, hint)
+                    assert np.array_equal(got, oracle.batch(umem, desc, mode, flags)), \
+                        (hint, mode, flags)
+                    assert np.array_equal(after, umem)
+
+
+def test_verify_padded_frames_pass(torch_cuda, engine):
+    """Valid datagrams in padded frames verify (0); before the fix the pad
+    bytes were summed and the frame length used as the UDP length."""
+    rng = np.random.default_rng(5)
+    frames = []
+    for plen in (0, 1, 5, 10, 17):
+        frames.append(rx_frames.pad60(rx_frames.v4_frame(rng, plen)))
+        frames.append(rx_frames.pad60(rx_frames.v4_frame(rng, plen), rx_frames.rand_bytes(rng, 60)))
+    for plen in (64, 1472, 8000):
+        frames.append(rx_frames.v4_frame(rng, plen) + b"\xff" * 7)
+        frames.append(rx_frames.v6_frame(rng, plen) + b"\x5a" * 24)
+    umem, addr, ln = rx_frames.layout(frames, rng)
+    desc = np.zeros(len(frames), dtype=X.DESC_DTYPE)
+    desc["addr"] = addr
+    desc["len"] = ln
+    engine.take_errors()   # clear what earlier tests left
+    got, _ = run_device(torch_cuda, engine, umem, desc, X.MODE_AUTO, X.F_VERIFY | X.F_IPHDR)
+    assert (got == 0).all()
+    out = np.full(len(desc), 7, dtype=np.uint16)
+    engine.batch_host(umem, desc, out, X.MODE_AUTO, X.F_VERIFY | X.F_IPHDR)
+    assert (out == 0).all()
+    assert engine.take_errors() == 0

@@ -282,3 +282,29 @@ def test_verify_zero_check_and_corruption(golden):
         bad_ip[int(desc["addr"][i]) + 22] ^= 0x01          # TTL byte
     assert (oracle.batch(bad_ip, desc, oracle.MODE_AUTO, VERIFY | IPHDR)[fam == 4] != 0).all()
     assert (oracle.batch(bad_ip, desc, oracle.MODE_AUTO, VERIFY)[fam == 4] == 0).all()
+
+
+def test_oracle_verify_uses_udp_length():
+    """RFC 768 verify on received frames: the datagram ends at udp +
+    ntohs(udp->len); Ethernet padding (zeros or junk) is not summed, and a
+    UDP length below 8 or past the frame never verifies."""
+    import rx_frames
+    rng = np.random.default_rng(3)
+    good, bad = [], []
+    for plen in (0, 1, 5, 10, 17):
+        good.append(rx_frames.pad60(rx_frames.v4_frame(rng, plen)))
+        good.append(rx_frames.pad60(rx_frames.v4_frame(rng, plen), rx_frames.rand_bytes(rng, 60)))
+    for plen in (64, 1472):
+        good.append(rx_frames.v4_frame(rng, plen) + b"\x01" * 9)
+        good.append(rx_frames.v6_frame(rng, plen) + b"\x80" * 3)
+    for ulen in (0, 7, 200):
+        f = bytearray(rx_frames.v4_frame(rng, 50))
+        f[38:40] = ulen.to_bytes(2, "big")
+        bad.append(bytes(f))
+    for frames, ok in ((good, True), (bad, False)):
+        umem, addr, ln = rx_frames.layout(frames, rng)
+        desc = np.zeros(len(frames), dtype=X.DESC_DTYPE)
+        desc["addr"] = addr
+        desc["len"] = ln
+        got = oracle.batch(umem, desc, oracle.MODE_AUTO, 0x10 | 0x2)
+        assert ((got == 0) == ok).all(), got
