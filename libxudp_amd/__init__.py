@@ -137,6 +137,14 @@ def lib():
             raise ImportError(
                 f"{LIB_PATH} is missing: build it with `make -C libxudp_amd` "
                 "or `python -c 'import __graft_entry__ as g; g.build()'`")
+        # One HIP runtime per process: torch ships its own libamdhip64.so
+        # (same SONAME as /opt/rocm's).  Loaded first, it also serves
+        # libxcsum.so's DT_NEEDED; loaded after ours, it would be a second
+        # runtime in the process and torch.cuda would see no device.
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         L = ctypes.CDLL(LIB_PATH)
         for name, (res, args) in _SIGS.items():
             fn = getattr(L, name)
