@@ -49,7 +49,10 @@ REG_GEOMETRIES = [(64, 1, 2), (64, 1, 9), (32, 1, 3), (32, 1, 6), (16, 1, 2), (1
                   (1, 2, 6)]
 # LDS-DMA staged variant (csum_lds_kernel<K, D>): G = 16, U = 10 + ring depth D
 LDS_GEOMETRIES = [(16, 12, 6), (16, 13, 6), (16, 12, 3), (16, 14, 3)]
-GEOMETRIES = REG_GEOMETRIES + LDS_GEOMETRIES
+# stream kernel (csum_stream_kernel<KC>): a wave per 64 packed frames, the
+# region they occupy streamed through a KC-KiB LDS stage: G = 64, U = 0, K = KC
+STREAM_GEOMETRIES = [(64, 0, 4), (64, 0, 8), (64, 0, 16)]
+GEOMETRIES = REG_GEOMETRIES + LDS_GEOMETRIES + STREAM_GEOMETRIES
 
 F_BUILD_INPLACE = 0x20
 F_SRC_ALIGNED = 0x40

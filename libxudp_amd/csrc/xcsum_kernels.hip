@@ -699,13 +699,19 @@ static __device__ __forceinline__ void csum_loop(const CsumArgs &a)
  * batches pay nothing for the region order; which copy runs is decided once
  * per launch (uniform branch, after resolve_order). */
 template <int G, int U, int K, bool IPH>
-__global__ void __launch_bounds__(256) csum_kernel(CsumArgs a)
+static __device__ __forceinline__ void csum_body(CsumArgs &a)
 {
 	resolve_order(a);
 	if (a.ord.rshift == 0)
 		csum_loop<G, U, K, false, IPH>(a);
 	else
 		csum_loop<G, U, K, true, IPH>(a);
+}
+
+template <int G, int U, int K, bool IPH>
+__global__ void __launch_bounds__(256) csum_kernel(CsumArgs a)
+{
+	csum_body<G, U, K, IPH>(a);
 }
 
 /* ---- LDS-staged variant ---------------------------------------------------
@@ -845,6 +851,252 @@ static hipError_t launch_lds_t(const CsumArgs &a, int cus, int bpc, hipStream_t 
 	return hipGetLastError();
 }
 
+/* ---- stream kernel: packed batches of small frames -------------------------
+ * A wave takes 64 consecutive descriptors (one per lane) and reads the UMEM
+ * region their frames occupy -- [min eth, max end) -- as one coalesced stream:
+ * chunk k*64 + lane of the region for k < KC (1 KiB per load instruction, no
+ * per-frame chunk grid, no edge masks on the loads).  The chunks go to the
+ * wave's LDS stage; then every lane sums ITS frame's span from LDS (16-byte
+ * reads, the head/tail bytes taken back out once) and finalizes it.  The
+ * frame boundaries are the descriptors, held one per lane: a segmented
+ * reduction of the stream, done per lane instead of per chunk.
+ * While one region is summed from LDS, the next region's loads are in flight
+ * in registers (KC dwordx4 per lane), and the descriptors after it.
+ * Header fields the finalize needs (h_proto for AUTO, udp->len / check for
+ * VERIFY, the IPv4 header for IPHDR) come from the same LDS copy.
+ * A wave whose frames do not fit in KC KiB (irregular batch, jumbo frame)
+ * walks them from global memory, one frame per wave; a sparse batch (xudp's
+ * 4096-byte slots) runs the frame-group kernel instead (checked once per
+ * launch, like resolve_order). */
+
+struct StreamSpan {
+	uint64_t eth;       /* UMEM offset of the frame (desc.addr - bias) */
+	uint32_t len;
+	uint32_t present;   /* frame index < n */
+};
+
+/* dense batch: the first and last descriptors span at most twice the bytes
+ * of n frames of their mean length (the converse of resolve_order) */
+static __device__ __forceinline__ bool dense_batch(const CsumArgs &a)
+{
+	if (a.n < 2)
+		return true;
+	const u32x4 d0 = *((cu32x4 *)(a.desc));
+	const u32x4 dl = *((cu32x4 *)(a.desc + (a.n - 1)));
+	const uint64_t a0 = ((uint64_t)d0.y << 32) | d0.x;
+	const uint64_t al = ((uint64_t)dl.y << 32) | dl.x;
+	const uint64_t mean = ((uint64_t)d0.z + dl.z) / 2 + 1;
+	return !(al > a0 && al + dl.z - a0 > 2ull * a.n * mean);
+}
+
+/* the 4 LDS bytes at byte offset o (any alignment), little-endian */
+static __device__ __forceinline__ uint32_t lds_bytes4(const uint8_t *st, uint32_t o)
+{
+	const uint32_t *w = (const uint32_t *)(st + (o & ~3u));
+	return __builtin_amdgcn_alignbyte(w[1], w[0], o & 3u);
+}
+
+template <int KC>
+static __device__ __forceinline__ void stream_loop(const CsumArgs &a, u32x4 *stage)
+{
+	const uint32_t lane = threadIdx.x & 63;
+	const uint32_t nw = gridDim.x * 4;
+	const uint8_t *zero = (const uint8_t *)g_zero_chunk;
+	const uint8_t *st8 = (const uint8_t *)stage;
+	uint32_t w = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
+
+	auto span_of = [&](uint32_t wi, u32x4 d) {
+		StreamSpan sp;
+		const uint32_t p = 64u * wi + lane;
+		sp.present = p < a.n;
+		sp.eth = ((((uint64_t)d.y << 32) | d.x) - a.bias);
+		sp.len = d.z;
+		return sp;
+	};
+	/* Region of a wave-iteration: base (16-aligned UMEM offset) and chunk
+	 * count, or ~0u when the frames do not fit the stage.  The bounds are
+	 * the first lane's frame start and the last present lane's frame end
+	 * (two readlanes -- a packed batch is in UMEM order); every frame must
+	 * then lie inside them (one ballot), else the wave walks its frames. */
+	auto region = [&](uint32_t wi, const StreamSpan &sp, uint64_t &base, uint32_t &nch) {
+		const uint64_t rem = a.n - 64ull * wi;
+		const uint32_t last = rem > 64 ? 63u : (uint32_t)rem - 1u;
+		const uint64_t end = sp.eth + sp.len;
+		const uint64_t lo =
+			((uint64_t)__builtin_amdgcn_readlane((uint32_t)(sp.eth >> 32), 0) << 32) |
+			__builtin_amdgcn_readlane((uint32_t)sp.eth, 0);
+		const uint64_t hi =
+			((uint64_t)__builtin_amdgcn_readlane((uint32_t)(end >> 32), last) << 32) |
+			__builtin_amdgcn_readlane((uint32_t)end, last);
+		base = lo & ~15ull;
+		const bool out = sp.present && (sp.eth < lo || end > hi);
+		nch = (__builtin_amdgcn_ballot_w64(out) || hi < lo || hi - base > (uint64_t)KC * 1024u)
+			      ? ~0u : (uint32_t)((hi - base + 15) >> 4);
+	};
+	auto issue_region = [&](uint64_t base, uint32_t nch, u32x4 (&v)[KC]) {
+#pragma unroll
+		for (int k = 0; k < KC; k++) {
+			const uint32_t c = (uint32_t)k * 64u + lane;
+			v[k] = load_chunk(nch != ~0u && c < nch ? a.umem + base + 16u * c : zero);
+		}
+	};
+	auto load_d = [&](uint32_t wi) {
+		const uint32_t p = 64u * wi + lane;
+		return *((gu32x4 *)(a.desc + (p < a.n ? p : a.n - 1)));
+	};
+
+	if (64ull * w >= a.n)
+		return;
+	u32x4 d = load_d(w);
+	StreamSpan sc = span_of(w, d);
+	uint64_t bc;
+	uint32_t nc;
+	region(w, sc, bc, nc);
+	u32x4 v[KC];
+	issue_region(bc, nc, v);
+	d = load_d(w + nw);
+	for (; 64ull * w < a.n; w += nw) {
+		/* this iteration's region -> LDS (waits for its loads only: the
+		 * descriptors issued after them may still be in flight) */
+#pragma unroll
+		for (int k = 0; k < KC; k++)
+			stage[k * 64 + lane] = v[k];
+		const StreamSpan cur = sc;
+		const uint64_t cbase = bc;
+		const uint32_t cnch = nc;
+		/* next iteration: its region's loads go out before this one is summed */
+		if (64ull * (w + nw) < a.n) {
+			sc = span_of(w + nw, d);
+			region(w + nw, sc, bc, nc);
+			__builtin_amdgcn_sched_barrier(0);
+			issue_region(bc, nc, v);
+			d = load_d(w + 2 * nw);
+		}
+		__builtin_amdgcn_sched_barrier(0);
+		__builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+		__builtin_amdgcn_wave_barrier();
+		__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+
+		if (cnch == ~0u) {
+			/* does not fit the stage: the whole wave walks each frame */
+			for (uint32_t i = 0; i < 64; i++) {
+				const uint32_t p = 64u * w + i;
+				if (p >= a.n)
+					break;
+				const u32x4 di = *((cu32x4 *)(a.desc + p));
+				Frame f = resolve<false, false>(a, di, true);
+				const bool rc = verify_recut(a, f);
+				if (a.flags & XCSUM_F_VERIFY)
+					verify_span<false>(f, rc);
+				uint32_t E = 0, O = 0;
+				sum_walk<64, false>(f, lane, E, O);
+				uint32_t s = f.odd ? (O << 8) + E : (E << 8) + O;
+				s = seg_sum<64>(s);
+				if (lane == 0)
+					finalize<false>(a, f, p, s);
+			}
+		} else if (cur.present) {
+			/* lane = frame: everything from the LDS copy of the region */
+			const uint32_t oe = (uint32_t)(cur.eth - cbase);   /* frame in the stage */
+			Frame f;
+			f.eth = a.umem + cur.eth;
+			int mode = (int)a.mode;
+			if (mode == XCSUM_MODE_AUTO) {
+				const uint32_t pr = lds_bytes4(st8, oe + 12) & 0xffffu;  /* h_proto, LE */
+				mode = pr == 0x0008u ? ((a.flags & XCSUM_F_V4_RFC) ? 1 : 0)
+				     : pr == 0xDD86u ? 2 : -1;
+			}
+			const uint32_t hdr = mode == 2 ? 54u : 34u, pre = mode == 2 ? 32u : 8u;
+			if (mode < 0 || cur.len < hdr + 8u || cur.len - hdr > 65535u)
+				mode = -1;
+			f.udp_len = cur.len - hdr;
+			f.ck = 0;
+			if (mode >= 0 && (a.flags & XCSUM_F_VERIFY)) {
+				const uint32_t uw = lds_bytes4(st8, oe + hdr + 4);  /* len, check */
+				const uint32_t ul = bswap16(uw);
+				f.ck = uw >> 16;
+				if (ul != f.udp_len) {
+					if (ul < 8u || ul > f.udp_len)
+						mode = -3;  /* never verifies */
+					else
+						f.udp_len = ul;
+				}
+			}
+			f.mode = mode;
+			uint32_t E = 0, O = 0;
+			const uint32_t lo = oe + hdr - pre, hi = oe + hdr + f.udp_len;
+			f.odd = lo & 1u;
+			if (mode >= 0) {
+				const uint32_t c0 = lo >> 4, c1 = (hi + 15) >> 4;
+				for (uint32_t c = c0; c < c1; c++)
+					accum(stage[c], E, O);
+				drop_prefix(stage[c0], lo & 15u, E, O);
+				drop_suffix(stage[c1 - 1], (16u - (hi & 15u)) & 15u, E, O);
+				if (a.flags & XCSUM_F_IPHDR) {
+					const uint32_t ih = oe + 14;
+					f.ihs = ih & 3u;
+#pragma unroll
+					for (int j = 0; j < 6; j++)
+						f.ih[j] = ((const uint32_t *)(st8 + (ih & ~3u)))[j];
+				}
+			}
+			const uint32_t s = f.odd ? (O << 8) + E : (E << 8) + O;
+			finalize<true>(a, f, 64u * w + lane, s);
+		}
+		/* the stage is rewritten next iteration: all reads done first */
+		__builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+		__builtin_amdgcn_wave_barrier();
+		__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+	}
+}
+
+/* XCSUM_STREAM_WPE=N builds a variant capped for N waves per SIMD (A/B) */
+#if defined(XCSUM_STREAM_WPE) && XCSUM_STREAM_WPE > 0
+#define STREAM_ATTR __attribute__((amdgpu_waves_per_eu(XCSUM_STREAM_WPE)))
+#else
+#define STREAM_ATTR
+#endif
+
+template <int KC>
+__global__ void __launch_bounds__(256) STREAM_ATTR csum_stream_kernel(CsumArgs a)
+{
+	extern __shared__ u32x4 stream_stage[];   /* [4 waves][KC * 64] chunks */
+	if (!dense_batch(a)) {
+		/* sparse batch: the frame-group kernel, region order as usual */
+		csum_body<4, 1, 2, true>(a);
+		return;
+	}
+	stream_loop<KC>(a, stream_stage + (threadIdx.x >> 6) * (KC * 64));
+}
+
+template <int KC>
+static hipError_t launch_stream_t(const CsumArgs &a, int cus, int bpc, hipStream_t s)
+{
+	const size_t lds = (size_t)4 * KC * 64 * 16;
+	static std::atomic<int> occ_cache[OCC_MAX_DEVICES];
+	const int occ = occupancy_cached(occ_cache, [&] {
+		int nb = 0;
+		(void)hipFuncSetAttribute((const void *)csum_stream_kernel<KC>,
+					  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+		if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, csum_stream_kernel<KC>, 256,
+								 lds) != hipSuccess || nb <= 0)
+			nb = 1;
+		return nb;
+	});
+	const int per_cu = (bpc > 0 && bpc < occ) ? bpc : occ;
+	/* a wave per 64 frames; the sparse fallback sizes its own loop from the
+	 * same grid (persistent, strided) */
+	uint64_t blocks = ((uint64_t)a.n + 255) / 256;
+	const uint64_t cap = (uint64_t)cus * per_cu;
+	if (blocks > cap)
+		blocks = cap;
+	if (blocks == 0)
+		blocks = 1;
+	(void)hipGetLastError();
+	hipLaunchKernelGGL((csum_stream_kernel<KC>), dim3((unsigned)blocks), dim3(256), lds, s, a);
+	return hipGetLastError();
+}
+
 /* Geometry from the typical frame length (bytes): enough lanes x chunks to
  * cover a typical frame in one preload (frames beyond K*G chunks still work,
  * through the jumbo path), as few lanes per frame as that allows (per-frame
@@ -858,7 +1110,8 @@ Geometry pick_geometry(uint32_t len_hint)
 	 * plus up to 15 bytes of 16-byte misalignment */
 	uint32_t chunks = (len_hint + 8) / 16;
 	if (chunks <= 8)
-		return Geometry{4, 1, 2, 4};   /* 64-byte payloads: 3.1 TB/s algorithmic */
+		return Geometry{64, 0, 8, 0};  /* 64-byte payloads: the stream kernel, 3.8 TB/s
+						  algorithmic (frame groups (4,1,2): 3.1-3.4) */
 	if (chunks <= 16)
 		return Geometry{8, 1, 2, 0};
 	if (chunks <= 32)
@@ -905,6 +1158,8 @@ static hipError_t launch_t(const CsumArgs &a, int cus, int bpc, hipStream_t s)
 
 bool geometry_supported(Geometry g)
 {
+	if (g.G == 64 && g.U == 0 && (g.K == 4 || g.K == 8 || g.K == 16))
+		return true;
 	if (g.G == 16 && ((g.U == 12 || g.U == 13) && g.K == 6))
 		return true;
 	if (g.G == 16 && ((g.U == 12 || g.U == 14) && g.K == 3))
@@ -920,6 +1175,13 @@ hipError_t launch_csum(const CsumArgs &a, Geometry g, int cus, hipStream_t s)
 	if (a.n == 0)
 		return hipSuccess;
 	/* LDS-staged variant: G = 16, U = 10 + ring depth; identity order */
+	/* stream kernel: G = 64 lanes per 64 frames, U = 0, K = KiB of stage */
+	if (g.G == 64 && g.U == 0) {
+		if (g.K == 4) return launch_stream_t<4>(a, cus, g.B, s);
+		if (g.K == 8) return launch_stream_t<8>(a, cus, g.B, s);
+		if (g.K == 16) return launch_stream_t<16>(a, cus, g.B, s);
+		return hipErrorInvalidValue;
+	}
 	CsumArgs b = a;
 	b.ord = order_identity(a.n);
 	if (g.G == 16 && g.U == 12 && g.K == 6) return launch_lds_t<6, 2>(b, cus, g.B, s);

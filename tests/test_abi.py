@@ -137,7 +137,8 @@ def test_argument_validation_without_gpu():
 
 def test_geometry_list_matches_kernel_source():
     """X.GEOMETRIES (what the parity tests sweep) == the instantiations in
-    csrc/xcsum_kernels.hip: the XCSUM_GEOMETRIES table + the LDS dispatch."""
+    csrc/xcsum_kernels.hip: the XCSUM_GEOMETRIES table + the LDS and stream
+    dispatch."""
     import re
     src = open(os.path.join(ROOT, "libxudp_amd", "csrc", "xcsum_kernels.hip")).read()
     table = src[src.index("#define XCSUM_GEOMETRIES"):]
@@ -145,8 +146,11 @@ def test_geometry_list_matches_kernel_source():
     reg = [tuple(map(int, m)) for m in re.findall(r"X\((\d+), (\d+), (\d+)\)", table)]
     lds = [tuple(map(int, m)) for m in re.findall(
         r"g\.G == (\d+) && g\.U == (\d+) && g\.K == (\d+)\) return launch_lds_t", src)]
+    stream = [(64, 0, int(k)) for k in re.findall(
+        r"if \(g\.K == (\d+)\) return launch_stream_t", src)]
     assert reg == X.REG_GEOMETRIES
     assert sorted(lds) == sorted(X.LDS_GEOMETRIES)
+    assert sorted(stream) == sorted(X.STREAM_GEOMETRIES)
 
 
 def test_rx_msg_layout_matches_c():

@@ -75,3 +75,16 @@ def test_two_rank_partition_matches_single_process():
     big = dict(CFG_WEAK, n=2 * CFG_WEAK["n"])
     whole = rank_outputs(big, 0, 1)
     assert np.array_equal(np.concatenate([got[0]["weak"][1], got[1]["weak"][1]]), whole[1])
+
+
+def test_bench_helpers_present_and_real_bytes():
+    """bench.py's helpers exist (the GPU-only main() calls them) and the real
+    byte count is the union of touched 64-byte lines + 18 bytes per frame."""
+    import bench
+    for name in ("digest_check", "stream_ceiling", "gpu_clocks", "cpu_baseline", "pmc_traffic",
+                 "host_cpu_facts", "real_bytes", "rank_slice", "build_batch"):
+        assert callable(getattr(bench, name)), name
+    d = np.zeros(3, dtype=X.DESC_DTYPE)
+    d["addr"] = [0, 100, 4096]
+    d["len"] = [100, 28, 64]
+    assert bench.real_bytes(d) == (2 + 1) * 64 + 3 * 18
