@@ -15,17 +15,23 @@ import argparse
 import csv
 import json
 import os
+import re
 import statistics
 
-KERNEL = "csum_kernel"
+# the checksum kernels: csum_kernel<G,U,K,IPH> and csum_stream_kernel<KC>
+KERNEL = re.compile(r"csum_(stream_)?kernel")
+
+
+names = set()
 
 
 def counter_values(path, name):
     vals = {}
     with open(path) as f:
         for row in csv.DictReader(f):
-            if KERNEL not in row.get("Kernel_Name", ""):
+            if not KERNEL.search(row.get("Kernel_Name", "")):
                 continue
+            names.add(row["Kernel_Name"])
             if row.get("Counter_Name") != name:
                 continue
             key = row.get("Dispatch_Id") or row.get("Correlation_Id")
@@ -48,14 +54,14 @@ def main():
     f_kib = statistics.median(fetch)
     w_kib = statistics.median(write)
     hbm = (2 * f_kib + w_kib) * 1024
-    rec = {"config": args.config, "kernel": KERNEL, "dispatches": [len(fetch), len(write)],
+    rec = {"config": args.config, "kernel": sorted(names), "dispatches": [len(fetch), len(write)],
            "FETCH_SIZE_KiB_median": f_kib, "WRITE_SIZE_KiB_median": w_kib,
            "hbm_bytes_per_launch": round(hbm), "alg_bytes_per_launch": args.alg_bytes,
            "traffic_over_alg": round(hbm / args.alg_bytes, 4),
            "formula": "(2*FETCH_SIZE + WRITE_SIZE) * 1024  (gfx950 FETCH_SIZE = half of "
                       "wide streaming read bytes, MI355X_MICROARCH.md HBM)"}
     out = args.out or os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(
-        __file__))), "profiles", f"pmc_config{args.config}.json")
+        __file__))), "profiles", "r02", f"pmc_config{args.config}.json")
     json.dump(rec, open(out, "w"), indent=1)
     print(json.dumps(rec))
 
