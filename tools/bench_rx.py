@@ -11,7 +11,9 @@ Bytes moved per frame: descriptor 16 + record 64 + the frame bytes the
 kernel must read -- the whole frame with XCSUM_F_VERIFY, the 64-byte header
 line without.  For comparison the checksum kernel's VERIFY mode (2-byte
 result instead of the 64-byte record) runs on the same buffers.
-One JSON line per (config, flags, geometry).
+One JSON line per (config, flags, geometry), all modes timed in interleaved
+rounds in one process after a >= 300 ms clock ramp; vs_csum_verify = time /
+the checksum kernel's VERIFY time in the same rounds.
 Usage: python tools/bench_rx.py [--configs 2,3,4] [--geoms "auto;4,2,1;16,6,1"]"""
 import argparse
 import json
@@ -32,7 +34,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--configs", default="2,3,4")
     ap.add_argument("--geoms", default="auto")
-    ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--reps", type=int, default=7, help="interleaved rounds")
     ap.add_argument("--no-count", action="store_true", help="pass d_count = NULL")
     ap.add_argument("--reverse", action="store_true", help="time the modes in reverse order")
     args = ap.parse_args()
@@ -58,63 +60,84 @@ def main():
         d_out = torch.empty(n, dtype=torch.int16, device=dev)
         frame_bytes = int(desc["len"].astype(np.int64).sum())
         hint = int(desc["len"].mean())
-        # ~50 ms of launches first: the clocks ramp over the first tens of
-        # milliseconds, and the first mode timed would pay for it
-        for k in range(200):
-            eng.batch_device(bufs[k % nrot], d_desc, n, d_out, mode, X.F_VERIFY, hint,
-                             stream=s.cuda_stream)
-        torch.cuda.synchronize()
-
-        def timed(fn):
-            for k in range(10):
-                fn(k)
-            evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-                   for _ in range(args.reps)]
-            for k, (e0, e1) in enumerate(evs):
-                e0.record(s)
-                fn(k)
-                e1.record(s)
+        # clock ramp: >= 300 ms of launches before anything is timed (the
+        # clocks take tens of milliseconds to reach their working point)
+        import time
+        t0 = time.perf_counter()
+        k = 0
+        while time.perf_counter() - t0 < 0.3:
+            for _ in range(20):
+                eng.batch_device(bufs[k % nrot], d_desc, n, d_out, mode, X.F_VERIFY, hint,
+                                 stream=s.cuda_stream)
+                k += 1
             torch.cuda.synchronize()
-            return float(np.median([a.elapsed_time(b) for a, b in evs])) * 1e-3
 
-        for gname in args.geoms.split(";"):
-            if gname == "auto":
-                os.environ.pop("XCSUM_RX_GEOMETRY", None)
-            else:
-                os.environ["XCSUM_RX_GEOMETRY"] = gname
-            modes = (("plain", 0), ("verify", X.F_VERIFY), ("verify_iphdr", X.F_VERIFY | X.F_IPHDR))
-            for fname, flags in (modes[::-1] if args.reverse else modes):
-                def rx(k):
-                    eng.rx_device(bufs[k % nrot], d_desc, n, d_msgs,
-                                  None if args.no_count else d_count, flags, hint,
-                                  stream=s.cuda_stream)
-                t = timed(rx)
-                if args.no_count:
-                    st = d_msgs.view(-1, 64)[:, 20].cpu()
-                    ok = bool((st == 0).all().item())
+        def rx_fn(flags, gname):
+            def rx(k):
+                if gname == "auto":
+                    os.environ.pop("XCSUM_RX_GEOMETRY", None)
                 else:
-                    ok = int(d_count.item()) == n
-                read = frame_bytes if flags else 64 * n
-                moved = read + n * (16 + 64)
-                print(json.dumps({"kernel": "rx", "config": cid, "flags": fname,
-                                  "geometry": gname, "frames": n, "ms": round(t * 1e3, 4),
-                                  "mpps": round(n / t / 1e6, 1),
-                                  "GBps_moved": round(moved / t / 1e9, 1),
-                                  "pct_hbm_peak": round(100 * moved / t / 8e12, 1),
-                                  "all_delivered": ok}), flush=True)
-        os.environ.pop("XCSUM_RX_GEOMETRY", None)
+                    os.environ["XCSUM_RX_GEOMETRY"] = gname
+                eng.rx_device(bufs[k % nrot], d_desc, n, d_msgs,
+                              None if args.no_count else d_count, flags, hint,
+                              stream=s.cuda_stream)
+            return rx
 
-        def ver(k):
-            eng.batch_device(bufs[k % nrot], d_desc, n, d_out, mode, X.F_VERIFY, hint,
-                             stream=s.cuda_stream)
-        t = timed(ver)
-        ok = bool((d_out == 0).all().item())
-        moved = frame_bytes + n * (16 + 2)
-        print(json.dumps({"kernel": "csum_verify", "config": cid, "frames": n,
-                          "ms": round(t * 1e3, 4), "mpps": round(n / t / 1e6, 1),
-                          "GBps_moved": round(moved / t / 1e9, 1),
-                          "pct_hbm_peak": round(100 * moved / t / 8e12, 1),
-                          "all_valid": ok}), flush=True)
+        def csum_fn(flags):
+            def ver(k):
+                eng.batch_device(bufs[k % nrot], d_desc, n, d_out, mode, flags, hint,
+                                 stream=s.cuda_stream)
+            return ver
+
+        runs = []   # (record, fn, check)
+        names = (("plain", 0), ("verify", X.F_VERIFY), ("verify_iphdr", X.F_VERIFY | X.F_IPHDR))
+        for gname in args.geoms.split(";"):
+            for fname, flags in (names[::-1] if args.reverse else names):
+                read = frame_bytes if flags else 64 * n
+                runs.append(({"kernel": "rx", "config": cid, "flags": fname, "geometry": gname,
+                              "moved": read + n * (16 + 64)}, rx_fn(flags, gname), flags))
+        runs.append(({"kernel": "csum_verify", "config": cid, "flags": "verify",
+                      "moved": frame_bytes + n * 18}, csum_fn(X.F_VERIFY), None))
+        runs.append(({"kernel": "csum", "config": cid, "flags": "none",
+                      "moved": frame_bytes + n * 18}, csum_fn(0), None))
+        # interleaved rounds in one process: every mode sees the same clocks;
+        # per round K back-to-back launches between two events
+        K = max(5, min(50, int(0.02 / max(frame_bytes / 5e12, 1e-6))))
+        times = [[] for _ in runs]
+        for r in range(args.reps):
+            for i, (rec, fn, _) in enumerate(runs):
+                fn(0)
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(s)
+                for k in range(K):
+                    fn(k)
+                e1.record(s)
+                torch.cuda.synchronize()
+                times[i].append(e0.elapsed_time(e1) / K * 1e-3)
+        os.environ.pop("XCSUM_RX_GEOMETRY", None)
+        t_csum = float(np.median(times[-2]))
+        for (rec, fn, flags), ts in zip(runs, times):
+            t = float(np.median(ts))
+            if rec["kernel"] == "rx":
+                if args.no_count:
+                    ok = bool((d_msgs.view(-1, 64)[:, 20].cpu() == 0).all().item())
+                else:
+                    fn(0)
+                    torch.cuda.synchronize()
+                    ok = int(d_count.item()) == n
+                rec["all_delivered"] = ok
+            else:
+                fn(0)
+                torch.cuda.synchronize()
+                if rec["flags"] == "verify":
+                    rec["all_valid"] = bool((d_out == 0).all().item())
+            moved = rec.pop("moved")
+            rec.update({"frames": n, "ms": round(t * 1e3, 4), "mpps": round(n / t / 1e6, 1),
+                        "GBps_moved": round(moved / t / 1e9, 1),
+                        "pct_hbm_peak": round(100 * moved / t / 8e12, 1),
+                        "vs_csum_verify": round(t / t_csum, 3), "launches_per_round": K,
+                        "rounds": args.reps})
+            print(json.dumps(rec), flush=True)
         del bufs, d_msgs
         torch.cuda.empty_cache()
     eng.close()
