@@ -182,10 +182,16 @@ static __device__ __forceinline__ Frame resolve(const CsumArgs &a, u32x4 d, bool
 	if (a.flags & XCSUM_F_VERIFY) { /* wave-uniform: no load otherwise */
 		/* udp->len too: a received frame may carry Ethernet padding, so
 		 * the span ends at udp + ntohs(udp->len), not at the frame end */
-		const uint8_t *u = f.nchunks ? f.eth + (mode == 2 ? 58 : 38)
-					     : (const uint8_t *)g_zero_chunk;
-		f.ul = *(const uint16_t *)u;
-		f.ck = *(const uint16_t *)(u + 2);
+		/* Two 2-byte loads whose addresses differ by no constant (the
+		 * absent-frame fallbacks are 8 bytes apart), so the compiler
+		 * cannot merge them: merged, they were one dword load at eth + 38
+		 * (2 mod 4 in every xudp frame), and that misaligned load cost the
+		 * MTU kernel 45 % (tools/verify_probe.py).  An empty asm to keep
+		 * them apart cost every mode 20 %: it coarsened the waitcnts. */
+		const uint8_t *z = (const uint8_t *)g_zero_chunk;
+		const uint32_t lo = mode == 2 ? 58u : 38u;
+		f.ul = *(const uint16_t *)(f.nchunks ? f.eth + lo : z);
+		f.ck = *(const uint16_t *)(f.nchunks ? f.eth + lo + 2 : z + 8);
 	}
 	/* IPHDR: the IPv4 header too (six dwords, same reasoning) */
 	if (IPH && (a.flags & XCSUM_F_IPHDR)) {
@@ -431,7 +437,34 @@ static __device__ __forceinline__ void finalize(const CsumArgs &a, const Frame &
 {
 	uint16_t wire = 0;
 	if (f.mode >= 0) {
-		uint32_t S = s + 17u + (f.udp_len >> 16) + (f.udp_len & 0xffffu);
+		uint32_t udp_len = f.udp_len;
+		bool bad_len = false;
+		if (a.flags & XCSUM_F_VERIFY) {
+			/* A received frame may carry Ethernet padding or trailing
+			 * bytes: the datagram ends at udp + ntohs(udp->len) (RFC 768;
+			 * xudp_fill_msg reads it the same way, channel.c:86).  Rare,
+			 * so handled here by this one lane, re-summing the span from
+			 * memory; tested in the pipelined loop it cost 36 % at MTU
+			 * (one wave per SIMD has nothing to hide the check behind).
+			 * f.ul was loaded with the frame's chunks, opaque until here. */
+			uint32_t ul = f.ul;
+			asm volatile("" : "+v"(ul));
+			ul = bswap16(ul);
+			if (ul != udp_len) {
+				bad_len = ul < 8u || ul > udp_len;   /* never verifies */
+				if (!bad_len) {
+					Frame g = f;
+					const uint32_t pre = f.mode == 2 ? 32u : 8u;
+					const uintptr_t lo = (uintptr_t)f.eth + (f.mode == 2 ? 54u : 34u) - pre;
+					set_span<false>(g, lo, lo + pre + ul);
+					uint32_t E = 0, O = 0;
+					sum_walk<1, false>(g, 0, E, O);
+					s = g.odd ? (O << 8) + E : (E << 8) + O;
+					udp_len = ul;
+				}
+			}
+		}
+		uint32_t S = s + 17u + (udp_len >> 16) + (udp_len & 0xffffu);
 		uint32_t r;
 		if (a.flags & XCSUM_F_VERIFY) {
 			/* the frame's check field was summed with everything else:
@@ -445,6 +478,8 @@ static __device__ __forceinline__ void finalize(const CsumArgs &a, const Frame &
 			asm volatile("" : "+v"(ck));
 			if ((ck & 0xffffu) == 0)  /* no checksum: IPv4 ok, IPv6 invalid */
 				r = f.mode == 2 ? 0xffffu : 0u;
+			if (bad_len)
+				r = 0xffffu;
 			wire = bswap16(r);
 			if ((a.flags & XCSUM_F_IPHDR) && f.mode != 2) {
 				uint16_t ipr = ip_header_csum<IPH>(f, true);
@@ -510,41 +545,6 @@ static __device__ __forceinline__ uint32_t fidx(const CsumArgs &a, uint32_t p)
 	return ORD ? frame_of(a.ord, p) : p;
 }
 
-/* VERIFY on a received frame whose UDP length is not the descriptor's
- * (Ethernet padding, or a length that does not fit): true if the span must
- * be re-cut before summing.  Reading f.ul waits for its load, which was
- * issued before this step's chunks, so it costs no extra round trip. */
-static __device__ __forceinline__ bool verify_recut(const CsumArgs &a, const Frame &f)
-{
-	if (!(a.flags & XCSUM_F_VERIFY) || f.mode < 0)
-		return false;
-	return bswap16(f.ul) != f.udp_len;
-}
-
-/* Re-cut f's span to end at udp + ntohs(udp->len) (RFC 768: the pseudo
- * header and the sum use the UDP length; trailing bytes are link padding),
- * or fail the frame (mode -3: out 0xffff, not counted as malformed) when
- * that length is below 8 or runs past the frame.  Branch-free, every field
- * written through a select: a conditional update of some fields made the
- * compiler keep the Frame in scratch memory. */
-template <bool DW>
-static __device__ __forceinline__ void verify_span(Frame &f, bool recut)
-{
-	const uint32_t ul = bswap16(f.ul);
-	const bool bad = ul < 8u || ul > f.udp_len;
-	const uint32_t pre = f.mode == 2 ? 32u : 8u;
-	const uintptr_t lo = (uintptr_t)f.eth + (f.mode == 2 ? 54u : 34u) - pre;
-	Frame g = f;
-	set_span<DW>(g, lo, lo + pre + ul);
-	f.base = recut ? g.base : f.base;
-	f.head = recut ? g.head : f.head;
-	f.tail = recut ? g.tail : f.tail;
-	f.odd = recut ? g.odd : f.odd;
-	f.nchunks = recut ? (bad ? 0u : g.nchunks) : f.nchunks;
-	f.udp_len = recut ? ul : f.udp_len;
-	f.mode = recut && bad ? -3 : f.mode;
-}
-
 template <int G, int U, int K, bool TAIL, bool ORD, bool IPH>
 static __device__ __forceinline__ void consume(const CsumArgs &a, const Frame (&fc)[U],
 					       const u32x4 (&vc)[U][K], uint32_t lane,
@@ -552,27 +552,12 @@ static __device__ __forceinline__ void consume(const CsumArgs &a, const Frame (&
 {
 #pragma unroll
 	for (int u = 0; u < U; u++) {
+		const Frame &f = fc[u];
 		uint32_t E = 0, O = 0;
-		if (!TAIL) {
-			const Frame &f = fc[u];
+		if (!TAIL || f.nchunks <= K * G)
 			sum_frame<G, K, U, Grid<G, K>::DW>(f, vc[u], lane, E, O);
-			uint32_t s = f.odd ? (O << 8) + E : (E << 8) + O;
-			s = seg_sum<G>(s);
-			if (lane == 0 && f.mode != -2)
-				finalize<IPH>(a, f, fidx<ORD>(a, p0 + u * nseg), s);
-			continue;
-		}
-		/* the uniform slow path: jumbo frames walk their chunks; VERIFY
-		 * frames with a UDP length != the descriptor's are re-cut, and then
-		 * the preloaded chunks no longer fit either */
-		Frame f = fc[u];
-		const bool recut = verify_recut(a, f);
-		if (a.flags & XCSUM_F_VERIFY)   /* wave-uniform */
-			verify_span<Grid<G, K>::DW>(f, recut);
-		if (f.nchunks > K * G || recut)
-			sum_walk<G, Grid<G, K>::DW>(f, lane, E, O);
 		else
-			sum_frame<G, K, U, Grid<G, K>::DW>(f, vc[u], lane, E, O);
+			sum_walk<G, Grid<G, K>::DW>(f, lane, E, O);   /* jumbo frame */
 		uint32_t s = f.odd ? (O << 8) + E : (E << 8) + O;
 		s = seg_sum<G>(s);
 		if (lane == 0 && f.mode != -2)
@@ -596,7 +581,7 @@ static __device__ __forceinline__ void consume_any(const CsumArgs &a, const Fram
 	bool big = false;
 #pragma unroll
 	for (int u = 0; u < U; u++)
-		big |= fc[u].nchunks > K * G || verify_recut(a, fc[u]);
+		big |= fc[u].nchunks > K * G;
 	if (__builtin_amdgcn_ballot_w64(big))
 		consume<G, U, K, true, ORD, IPH>(a, fc, vc, lane, p0, nseg);
 	else
@@ -804,12 +789,9 @@ __global__ void __launch_bounds__(256) csum_lds_kernel(CsumArgs a)
 			__builtin_amdgcn_sched_barrier(0);
 			issue_stage(fn, d);
 			__builtin_amdgcn_sched_barrier(0);
-			Frame f = fs[d];
+			const Frame &f = fs[d];
 			uint32_t E = 0, O = 0;
-			const bool recut = verify_recut(a, f);
-			if (a.flags & XCSUM_F_VERIFY)
-				verify_span<Grid<G, K>::DW>(f, recut);
-			if (__builtin_amdgcn_ballot_w64(f.nchunks > K * G || recut))
+			if (__builtin_amdgcn_ballot_w64(f.nchunks > K * G))
 				sum_walk<G, Grid<G, K>::DW>(f, lane, E, O);
 			else
 				sum_frame<G, K, 2, Grid<G, K>::DW>(f, v, lane, E, O);
@@ -984,10 +966,7 @@ static __device__ __forceinline__ void stream_loop(const CsumArgs &a, u32x4 *sta
 				if (p >= a.n)
 					break;
 				const u32x4 di = *((cu32x4 *)(a.desc + p));
-				Frame f = resolve<false, false>(a, di, true);
-				const bool rc = verify_recut(a, f);
-				if (a.flags & XCSUM_F_VERIFY)
-					verify_span<false>(f, rc);
+				const Frame f = resolve<false, false>(a, di, true);
 				uint32_t E = 0, O = 0;
 				sum_walk<64, false>(f, lane, E, O);
 				uint32_t s = f.odd ? (O << 8) + E : (E << 8) + O;
@@ -1015,6 +994,7 @@ static __device__ __forceinline__ void stream_loop(const CsumArgs &a, u32x4 *sta
 				const uint32_t uw = lds_bytes4(st8, oe + hdr + 4);  /* len, check */
 				const uint32_t ul = bswap16(uw);
 				f.ck = uw >> 16;
+				f.ul = uw & 0xffffu;   /* finalize sees udp_len == ul: no re-cut */
 				if (ul != f.udp_len) {
 					if (ul < 8u || ul > f.udp_len)
 						mode = -3;  /* never verifies */

@@ -132,11 +132,17 @@ extern "C" int xudp_packet_udp_batch(xcsum_ctx *ctx, struct packet_info *infos, 
 	uint32_t kflags = XCSUM_F_IPHDR | (flags & (XCSUM_F_V4_RFC | XCSUM_F_ZEROCOPY));
 	if (!base)
 		kflags &= ~XCSUM_F_ZEROCOPY;
-	/* staged copies gather frame by frame: the frames are the caller's
-	 * buffers anywhere in memory, and a copy of the address range they
-	 * span could read unmapped pages between them */
+	/* Staged copies gather frame by frame when the frames are the caller's
+	 * buffers anywhere in memory (a copy of the address range they span
+	 * could read unmapped pages between them), and when only headers are
+	 * needed (42 of ~1500 bytes per frame).  Whole frames inside one
+	 * registered UMEM go by DMA of the range, no host copy. */
+	bool hdr_only = !v4_rfc;
+	for (uint32_t i = 0; i < n && hdr_only; i++)
+		hdr_only = infos[i].family == AF_INET;
+	const bool gather = !(kflags & XCSUM_F_ZEROCOPY) && (!base || hdr_only);
 	int rc = xcsum::batch_host_impl(ctx, base, desc.data(), n, out.data(), out_ip.data(),
-					XCSUM_MODE_AUTO, kflags, !(kflags & XCSUM_F_ZEROCOPY));
+					XCSUM_MODE_AUTO, kflags, gather);
 	if (rc)
 		return rc;
 	for (uint32_t i = 0; i < n; i++) {
