@@ -843,30 +843,43 @@ __global__ void __launch_bounds__(256) rx_wide_kernel(RxArgs a)
 			const uint32_t fl = (P.v4 ? 1u : 0u) | (P.good ? 2u : 0u);
 			uint32_t mysum = 0;
 			u32x4 va[K], vb[K];
+			/* A step's frame parameters come from the owning lane
+			 * (ds_bpermute, ~100s of cycles) and its loads need them:
+			 * fetched two steps ahead, so the loads of step t + 2 go out
+			 * as soon as step t's registers are free instead of one
+			 * bpermute latency later (the pipeline then keeps two steps
+			 * in flight throughout). */
 			WStep sa = rx_step_frame<G>(f, P.hi, fl, grp);
 			span_issue(sa, va);
+			WStep sb = rx_step_frame<G>(f, P.hi, fl, FPS + grp);
 #pragma unroll 1
 			for (uint32_t t = 0; t < STEPS; t += 2) {
 				if (HDR_LEAD > 0 && HDR_LEAD < STEPS && t + HDR_LEAD == STEPS && bn < nb)
 					hdr_issue(fn, hv);
-				const WStep sb = rx_step_frame<G>(f, P.hi, fl, (t + 1) * FPS + grp);
 				__builtin_amdgcn_sched_barrier(0);
 				span_issue(sb, vb);
 				__builtin_amdgcn_sched_barrier(0);
+				/* parameters of steps t + 2 and t + 3 (clamped past the end:
+				 * never issued) */
+				const uint32_t t2 = t + 2 < STEPS ? t + 2 : t;
+				const uint32_t t3 = t + 3 < STEPS ? t + 3 : t + 1;
+				const WStep sc = rx_step_frame<G>(f, P.hi, fl, t2 * FPS + grp);
+				const WStep sd = rx_step_frame<G>(f, P.hi, fl, t3 * FPS + grp);
 				uint32_t s = rx_step_sum<G, K>(span, sa, va, lane);
 				uint32_t x = G == 64 ? s : bperm((wl % FPS) * G, s);
 				if (wl / FPS == t)
 					mysum = x;
 				if (t + 2 < STEPS) {
-					sa = rx_step_frame<G>(f, P.hi, fl, (t + 2) * FPS + grp);
 					__builtin_amdgcn_sched_barrier(0);
-					span_issue(sa, va);
+					span_issue(sc, va);
 					__builtin_amdgcn_sched_barrier(0);
 				}
 				s = rx_step_sum<G, K>(span, sb, vb, lane);
 				x = G == 64 ? s : bperm((wl % FPS) * G, s);
 				if (wl / FPS == t + 1)
 					mysum = x;
+				sa = sc;
+				sb = sd;
 			}
 			bool good = P.good;
 			if (good) {

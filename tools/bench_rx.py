@@ -37,6 +37,8 @@ def main():
     ap.add_argument("--reps", type=int, default=7, help="interleaved rounds")
     ap.add_argument("--no-count", action="store_true", help="pass d_count = NULL")
     ap.add_argument("--reverse", action="store_true", help="time the modes in reverse order")
+    ap.add_argument("--only", default="", help="comma list of modes to run: plain, verify, "
+                    "verify_iphdr, csum_verify, csum (default: all)")
     args = ap.parse_args()
     import torch
     dev = torch.device("cuda:0")
@@ -100,6 +102,11 @@ def main():
                       "moved": frame_bytes + n * 18}, csum_fn(X.F_VERIFY), None))
         runs.append(({"kernel": "csum", "config": cid, "flags": "none",
                       "moved": frame_bytes + n * 18}, csum_fn(0), None))
+        if args.only:
+            keep = set(args.only.split(","))
+            runs = [r for r in runs if (r[0]["flags"] if r[0]["kernel"] == "rx" else
+                                        ("csum_verify" if r[0]["kernel"] == "csum_verify"
+                                         else "csum")) in keep]
         # interleaved rounds in one process: every mode sees the same clocks;
         # per round K back-to-back launches between two events
         K = max(5, min(50, int(0.02 / max(frame_bytes / 5e12, 1e-6))))
@@ -115,7 +122,8 @@ def main():
                 torch.cuda.synchronize()
                 times[i].append(e0.elapsed_time(e1) / K * 1e-3)
         os.environ.pop("XCSUM_RX_GEOMETRY", None)
-        t_csum = float(np.median(times[-2]))
+        cv = [i for i, r in enumerate(runs) if r[0]["kernel"] == "csum_verify"]
+        t_csum = float(np.median(times[cv[0]])) if cv else float("nan")
         for (rec, fn, flags), ts in zip(runs, times):
             t = float(np.median(ts))
             if rec["kernel"] == "rx":
