@@ -77,7 +77,7 @@ static __device__ __forceinline__ u32x4 load_desc(const CsumArgs &a, uint32_t p)
 	return *((gu32x4 *)(a.desc + q));
 }
 
-template <bool DW, bool IPH>
+template <bool DW, int FEAT>
 static __device__ __forceinline__ Frame resolve(const CsumArgs &a, u32x4 d, bool present)
 {
 	Frame f;
@@ -112,7 +112,7 @@ static __device__ __forceinline__ Frame resolve(const CsumArgs &a, u32x4 d, bool
 	 * wait for the load on the spot. */
 	f.ck = 0;
 	f.ul = 0;
-	if (a.flags & XCSUM_F_VERIFY) { /* wave-uniform: no load otherwise */
+	if (FEAT >= 1 && (a.flags & XCSUM_F_VERIFY)) { /* wave-uniform: no load otherwise */
 		/* udp->len too: a received frame may carry Ethernet padding, so
 		 * the span ends at udp + ntohs(udp->len), not at the frame end */
 		/* Two 2-byte loads whose addresses differ by no constant (the
@@ -127,7 +127,7 @@ static __device__ __forceinline__ Frame resolve(const CsumArgs &a, u32x4 d, bool
 		f.ck = *(const uint16_t *)(f.nchunks ? f.eth + lo + 2 : z + 8);
 	}
 	/* IPHDR: the IPv4 header too (six dwords, same reasoning) */
-	if (IPH && (a.flags & XCSUM_F_IPHDR)) {
+	if (FEAT == 2 && (a.flags & XCSUM_F_IPHDR)) {
 		const uint8_t *ih = f.nchunks && mode != 2 ? f.eth + 14
 							   : (const uint8_t *)g_zero_chunk;
 		f.ihs = (uint32_t)(uintptr_t)ih & 3u;
@@ -158,7 +158,7 @@ static __device__ uint16_t ip_header_csum_mem(const uint8_t *iph, bool verify)
 }
 
 /* IPH: from the dwords resolve() prefetched; else from memory (a dependent
- * round trip -- the kernels are instantiated with IPH whenever IPHDR is set,
+ * round trip -- the kernels are instantiated with FEAT 2 whenever IPHDR is set,
  * the fallback only keeps results independent of the instantiation) */
 template <bool IPH>
 static __device__ uint16_t ip_header_csum(const Frame &f, bool verify)
@@ -187,7 +187,7 @@ static __device__ uint16_t ip_header_csum(const Frame &f, bool verify)
 	return bswap16(~sum & 0xffffu);
 }
 
-template <bool IPH>
+template <int FEAT>
 static __device__ __forceinline__ void finalize(const CsumArgs &a, const Frame &f, uint32_t p,
 						uint32_t s)
 {
@@ -195,7 +195,7 @@ static __device__ __forceinline__ void finalize(const CsumArgs &a, const Frame &
 	if (f.mode >= 0) {
 		uint32_t udp_len = f.udp_len;
 		bool bad_len = false;
-		if (a.flags & XCSUM_F_VERIFY) {
+		if (FEAT >= 1 && (a.flags & XCSUM_F_VERIFY)) {
 			/* A received frame may carry Ethernet padding or trailing
 			 * bytes: the datagram ends at udp + ntohs(udp->len) (RFC 768;
 			 * xudp_fill_msg reads it the same way, channel.c:86).  Rare,
@@ -222,7 +222,7 @@ static __device__ __forceinline__ void finalize(const CsumArgs &a, const Frame &
 		}
 		uint32_t S = s + 17u + (udp_len >> 16) + (udp_len & 0xffffu);
 		uint32_t r;
-		if (a.flags & XCSUM_F_VERIFY) {
+		if (FEAT >= 1 && (a.flags & XCSUM_F_VERIFY)) {
 			/* the frame's check field was summed with everything else:
 			 * a valid RFC checksum folds to 0xffff, i.e. r == 0 */
 			uint32_t t = (S & 0xffffu) + (S >> 16);
@@ -238,7 +238,7 @@ static __device__ __forceinline__ void finalize(const CsumArgs &a, const Frame &
 				r = 0xffffu;
 			wire = bswap16(r);
 			if ((a.flags & XCSUM_F_IPHDR) && f.mode != 2) {
-				uint16_t ipr = ip_header_csum<IPH>(f, true);
+				uint16_t ipr = ip_header_csum<FEAT == 2>(f, true);
 				if (a.out_ip)
 					a.out_ip[p] = ipr;
 				if (wire == 0)
@@ -262,7 +262,7 @@ static __device__ __forceinline__ void finalize(const CsumArgs &a, const Frame &
 		if (a.flags & XCSUM_F_INPLACE)
 			store_u16(f.eth + (f.mode == 2 ? 60 : 40), wire);
 		if ((a.flags & XCSUM_F_IPHDR) && f.mode != 2) {
-			uint16_t ipc = ip_header_csum<IPH>(f, false);
+			uint16_t ipc = ip_header_csum<FEAT == 2>(f, false);
 			if (a.flags & XCSUM_F_INPLACE)
 				store_u16(f.eth + 24, ipc);
 			if (a.out_ip)
@@ -287,7 +287,7 @@ static __device__ __forceinline__ uint32_t fidx(const CsumArgs &a, uint32_t p)
 	return ORD ? frame_of(a.ord, p) : p;
 }
 
-template <int G, int U, int K, bool TAIL, bool ORD, bool IPH>
+template <int G, int U, int K, bool TAIL, bool ORD, int FEAT>
 static __device__ __forceinline__ void consume(const CsumArgs &a, const Frame (&fc)[U],
 					       const u32x4 (&vc)[U][K], uint32_t lane,
 					       uint32_t p0, uint32_t nseg)
@@ -303,7 +303,7 @@ static __device__ __forceinline__ void consume(const CsumArgs &a, const Frame (&
 		uint32_t s = f.odd ? (O << 8) + E : (E << 8) + O;
 		s = seg_sum<G>(s);
 		if (lane == 0 && f.mode != -2)
-			finalize<IPH>(a, f, fidx<ORD>(a, p0 + u * nseg), s);
+			finalize<FEAT>(a, f, fidx<ORD>(a, p0 + u * nseg), s);
 	}
 }
 
@@ -315,7 +315,7 @@ static __device__ __forceinline__ void consume(const CsumArgs &a, const Frame (&
 
 /* wave-uniform split: the jumbo path lives in its own copy of the body, so
  * its drains never merge into the common path's vmcnt bookkeeping */
-template <int G, int U, int K, bool ORD, bool IPH>
+template <int G, int U, int K, bool ORD, int FEAT>
 static __device__ __forceinline__ void consume_any(const CsumArgs &a, const Frame (&fc)[U],
 						   const u32x4 (&vc)[U][K], uint32_t lane,
 						   uint32_t p0, uint32_t nseg)
@@ -325,9 +325,9 @@ static __device__ __forceinline__ void consume_any(const CsumArgs &a, const Fram
 	for (int u = 0; u < U; u++)
 		big |= fc[u].nchunks > K * G;
 	if (__builtin_amdgcn_ballot_w64(big))
-		consume<G, U, K, true, ORD, IPH>(a, fc, vc, lane, p0, nseg);
+		consume<G, U, K, true, ORD, FEAT>(a, fc, vc, lane, p0, nseg);
 	else
-		consume<G, U, K, false, ORD, IPH>(a, fc, vc, lane, p0, nseg);
+		consume<G, U, K, false, ORD, FEAT>(a, fc, vc, lane, p0, nseg);
 }
 
 /*
@@ -341,7 +341,7 @@ static __device__ __forceinline__ void consume_any(const CsumArgs &a, const Fram
  * at the loop latch, that copy needs the next step's loads to have landed,
  * and the ISA showed a vmcnt(0) there -- one step in flight, not two.
  */
-template <int G, int U, int K, bool ORD, bool IPH>
+template <int G, int U, int K, bool ORD, int FEAT>
 static __device__ __forceinline__ void csum_loop(const CsumArgs &a)
 {
 	const uint32_t lane = threadIdx.x & (G - 1);
@@ -363,7 +363,7 @@ static __device__ __forceinline__ void csum_loop(const CsumArgs &a)
 		d[u] = load_desc<G == 64>(a, fidx<ORD>(a, seg + u * nseg));
 #pragma unroll
 	for (int u = 0; u < U; u++)
-		fa[u] = resolve<Grid<G, K>::DW, IPH>(a, d[u], has(seg + u * nseg));
+		fa[u] = resolve<Grid<G, K>::DW, FEAT>(a, d[u], has(seg + u * nseg));
 #pragma unroll
 	for (int u = 0; u < U; u++)
 		d[u] = load_desc<G == 64>(a, fidx<ORD>(a, seg + step + u * nseg));
@@ -379,24 +379,24 @@ static __device__ __forceinline__ void csum_loop(const CsumArgs &a)
 	for (uint32_t p0 = seg; p0 < limit; p0 += 2 * step) {
 #pragma unroll
 		for (int u = 0; u < U; u++)
-			fb[u] = resolve<Grid<G, K>::DW, IPH>(a, d[u], has(p0 + step + u * nseg));
+			fb[u] = resolve<Grid<G, K>::DW, FEAT>(a, d[u], has(p0 + step + u * nseg));
 #pragma unroll
 		for (int u = 0; u < U; u++)
 			d[u] = load_desc<G == 64>(a, fidx<ORD>(a, p0 + 2 * step + u * nseg));
 		__builtin_amdgcn_sched_barrier(0);
 		issue<G, U, K>(fb, lane, vb);
-		consume_any<G, U, K, ORD, IPH>(a, fa, va, lane, p0, nseg);
+		consume_any<G, U, K, ORD, FEAT>(a, fa, va, lane, p0, nseg);
 
 #pragma unroll
 		for (int u = 0; u < U; u++)
-			fa[u] = resolve<Grid<G, K>::DW, IPH>(a, d[u],
+			fa[u] = resolve<Grid<G, K>::DW, FEAT>(a, d[u],
 							has(p0 + 2 * step + u * nseg));
 #pragma unroll
 		for (int u = 0; u < U; u++)
 			d[u] = load_desc<G == 64>(a, fidx<ORD>(a, p0 + 3 * step + u * nseg));
 		__builtin_amdgcn_sched_barrier(0);
 		issue<G, U, K>(fa, lane, va);
-		consume_any<G, U, K, ORD, IPH>(a, fb, vb, lane, p0 + step, nseg);
+		consume_any<G, U, K, ORD, FEAT>(a, fb, vb, lane, p0 + step, nseg);
 	}
 #else
 	for (uint32_t p0 = seg; p0 < limit; p0 += step) {
@@ -404,13 +404,13 @@ static __device__ __forceinline__ void csum_loop(const CsumArgs &a)
 		u32x4 vn[U][K];
 #pragma unroll
 		for (int u = 0; u < U; u++)
-			fn[u] = resolve<Grid<G, K>::DW, IPH>(a, d[u], has(p0 + step + u * nseg));
+			fn[u] = resolve<Grid<G, K>::DW, FEAT>(a, d[u], has(p0 + step + u * nseg));
 #pragma unroll
 		for (int u = 0; u < U; u++)
 			d[u] = load_desc<G == 64>(a, fidx<ORD>(a, p0 + 2 * step + u * nseg));
 		__builtin_amdgcn_sched_barrier(0);
 		issue<G, U, K>(fn, lane, vn);
-		consume_any<G, U, K, ORD, IPH>(a, fa, va, lane, p0, nseg);
+		consume_any<G, U, K, ORD, FEAT>(a, fa, va, lane, p0, nseg);
 #pragma unroll
 		for (int u = 0; u < U; u++) {
 			fa[u] = fn[u];
@@ -425,20 +425,20 @@ static __device__ __forceinline__ void csum_loop(const CsumArgs &a)
 /* The identity order gets its own copy of the loop, so descriptor-order
  * batches pay nothing for the region order; which copy runs is decided once
  * per launch (uniform branch, after resolve_order). */
-template <int G, int U, int K, bool IPH>
+template <int G, int U, int K, int FEAT>
 static __device__ __forceinline__ void csum_body(CsumArgs &a)
 {
 	resolve_order(a);
 	if (a.ord.rshift == 0)
-		csum_loop<G, U, K, false, IPH>(a);
+		csum_loop<G, U, K, false, FEAT>(a);
 	else
-		csum_loop<G, U, K, true, IPH>(a);
+		csum_loop<G, U, K, true, FEAT>(a);
 }
 
-template <int G, int U, int K, bool IPH>
+template <int G, int U, int K, int FEAT>
 __global__ void __launch_bounds__(256) csum_kernel(CsumArgs a)
 {
-	csum_body<G, U, K, IPH>(a);
+	csum_body<G, U, K, FEAT>(a);
 }
 
 /* ---- LDS-staged variant ---------------------------------------------------
@@ -489,7 +489,7 @@ __global__ void __launch_bounds__(256) csum_lds_kernel(CsumArgs a)
 		uint32_t f = frame0(j);
 		u32x4 d = pick(load_desc_scalar(a, f), load_desc_scalar(a, f + 1),
 			       load_desc_scalar(a, f + 2), load_desc_scalar(a, f + 3));
-		return resolve<Grid<G, K>::DW, true>(a, d, f + sub < a.n);
+		return resolve<Grid<G, K>::DW, 2>(a, d, f + sub < a.n);
 	};
 	auto issue_stage = [&](const Frame &f, int slot) {
 #pragma unroll
@@ -540,7 +540,7 @@ __global__ void __launch_bounds__(256) csum_lds_kernel(CsumArgs a)
 			uint32_t sum = f.odd ? (O << 8) + E : (E << 8) + O;
 			sum = seg_sum<G>(sum);
 			if (lane == 0 && f.mode != -2)
-				finalize<true>(a, f, frame0(j) + sub, sum);
+				finalize<2>(a, f, frame0(j) + sub, sum);
 			fs[d] = fn;
 		}
 	}
@@ -708,13 +708,13 @@ static __device__ __forceinline__ void stream_loop(const CsumArgs &a, u32x4 *sta
 				if (p >= a.n)
 					break;
 				const u32x4 di = *((cu32x4 *)(a.desc + p));
-				const Frame f = resolve<false, false>(a, di, true);
+				const Frame f = resolve<false, 2>(a, di, true);
 				uint32_t E = 0, O = 0;
 				sum_walk<64, false>(f, lane, E, O);
 				uint32_t s = f.odd ? (O << 8) + E : (E << 8) + O;
 				s = seg_sum<64>(s);
 				if (lane == 0)
-					finalize<false>(a, f, p, s);
+					finalize<2>(a, f, p, s);
 			}
 		} else if (cur.present) {
 			/* lane = frame: everything from the LDS copy of the region */
@@ -763,7 +763,7 @@ static __device__ __forceinline__ void stream_loop(const CsumArgs &a, u32x4 *sta
 				}
 			}
 			const uint32_t s = f.odd ? (O << 8) + E : (E << 8) + O;
-			finalize<true>(a, f, 64u * w + lane, s);
+			finalize<2>(a, f, 64u * w + lane, s);
 		}
 		/* the stage is rewritten next iteration: all reads done first */
 		__builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -785,7 +785,7 @@ __global__ void __launch_bounds__(256) STREAM_ATTR csum_stream_kernel(CsumArgs a
 	extern __shared__ u32x4 stream_stage[];   /* [4 waves][KC * 64] chunks */
 	if (!dense_batch(a)) {
 		/* sparse batch: the frame-group kernel, region order as usual */
-		csum_body<4, 1, 2, true>(a);
+		csum_body<4, 1, 2, 2>(a);
 		return;
 	}
 	stream_loop<KC>(a, stream_stage + (threadIdx.x >> 6) * (KC * 64));
@@ -845,7 +845,7 @@ Geometry pick_geometry(uint32_t len_hint)
 	return Geometry{64, 1, 9, 2};          /* jumbo / mixed up to 9 KB: 6.2 TB/s */
 }
 
-template <int G, int U, int K, bool IPH>
+template <int G, int U, int K, int FEAT>
 static hipError_t launch_t(const CsumArgs &a, int cus, int bpc, hipStream_t s)
 {
 	/* persistent grid: at most what the device keeps resident, so no second
@@ -853,7 +853,7 @@ static hipError_t launch_t(const CsumArgs &a, int cus, int bpc, hipStream_t s)
 	static std::atomic<int> occ_cache[OCC_MAX_DEVICES];
 	const int occ = occupancy_cached(occ_cache, [] {
 		int nb = 0;
-		if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, csum_kernel<G, U, K, IPH>, 256, 0) !=
+		if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, csum_kernel<G, U, K, FEAT>, 256, 0) !=
 			    hipSuccess || nb <= 0)
 			nb = 4;
 		return nb;
@@ -868,7 +868,7 @@ static hipError_t launch_t(const CsumArgs &a, int cus, int bpc, hipStream_t s)
 		blocks = 1;
 	(void)hipGetLastError();  /* clear a stale error (e.g. hipErrorNotReady from
 	                           * someone's hipEventQuery) before checking ours */
-	hipLaunchKernelGGL((csum_kernel<G, U, K, IPH>), dim3((unsigned)blocks), dim3(256), 0, s, a);
+	hipLaunchKernelGGL((csum_kernel<G, U, K, FEAT>), dim3((unsigned)blocks), dim3(256), 0, s, a);
 	return hipGetLastError();
 }
 
@@ -910,12 +910,16 @@ hipError_t launch_csum(const CsumArgs &a, Geometry g, int cus, hipStream_t s)
 	if (g.G == 16 && g.U == 13 && g.K == 6) return launch_lds_t<6, 3>(b, cus, g.B, s);
 	if (g.G == 16 && g.U == 14 && g.K == 3) return launch_lds_t<3, 4>(b, cus, g.B, s);
 	if (g.G == 16 && g.U == 12 && g.K == 3) return launch_lds_t<3, 2>(b, cus, g.B, s);
-	/* IPHDR kernels prefetch the IPv4 header a pipeline step ahead: a
-	 * separate instantiation, so the plain path keeps its registers */
+	/* Three instantiations per geometry (FEAT): 0 plain, 1 + VERIFY
+	 * (udp->len and udp->check prefetched a pipeline step ahead), 2 + IPHDR
+	 * (the IPv4 header prefetched too).  Each keeps only the registers and
+	 * code it needs: run in the IPHDR instantiation, VERIFY alone cost
+	 * 45 % at MTU (tools/verify_probe.py) */
 #define X(g_, u_, k_)                                                                  \
 	if (g.G == g_ && g.U == u_ && g.K == k_)                                        \
-		return (a.flags & XCSUM_F_IPHDR) ? launch_t<g_, u_, k_, true>(a, cus, g.B, s)  \
-						 : launch_t<g_, u_, k_, false>(a, cus, g.B, s);
+		return (a.flags & XCSUM_F_IPHDR)    ? launch_t<g_, u_, k_, 2>(a, cus, g.B, s) \
+		       : (a.flags & XCSUM_F_VERIFY) ? launch_t<g_, u_, k_, 1>(a, cus, g.B, s) \
+						    : launch_t<g_, u_, k_, 0>(a, cus, g.B, s);
 	XCSUM_GEOMETRIES(X)
 #undef X
 	return hipErrorInvalidValue;
