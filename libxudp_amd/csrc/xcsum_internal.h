@@ -109,6 +109,10 @@ int batch_host_impl(struct xcsum_ctx *c, uint8_t *h_umem, const struct xcsum_des
 		    bool gather = false);
 bool geometry_supported(Geometry g);
 hipError_t launch_csum(const CsumArgs &a, Geometry g, int cus, hipStream_t s);
+/* csum_kernel per feature set (xcsum_csum_f{0,1,2}.hip): plain, + VERIFY, + IPHDR */
+hipError_t launch_csum_f0(const CsumArgs &a, Geometry g, int cus, hipStream_t s);
+hipError_t launch_csum_f1(const CsumArgs &a, Geometry g, int cus, hipStream_t s);
+hipError_t launch_csum_f2(const CsumArgs &a, Geometry g, int cus, hipStream_t s);
 hipError_t launch_gen(uint8_t *d_umem, const struct xcsum_desc *d_desc, uint32_t n,
 		      uint32_t family, uint64_t seed, uint64_t first_index, int max_blocks,
 		      hipStream_t s);

@@ -137,11 +137,14 @@ def test_argument_validation_without_gpu():
 
 def test_geometry_list_matches_kernel_source():
     """X.GEOMETRIES (what the parity tests sweep) == the instantiations in
-    csrc/xcsum_kernels.hip: the XCSUM_GEOMETRIES table + the LDS and stream
-    dispatch."""
+    the XCSUM_GEOMETRIES table (csrc/xcsum_csum.h, instantiated per feature set
+    in xcsum_csum_f{0,1,2}.hip) + the LDS and stream dispatch of
+    csrc/xcsum_kernels.hip."""
     import re
-    src = open(os.path.join(ROOT, "libxudp_amd", "csrc", "xcsum_kernels.hip")).read()
-    table = src[src.index("#define XCSUM_GEOMETRIES"):]
+    csrc = os.path.join(ROOT, "libxudp_amd", "csrc")
+    src = open(os.path.join(csrc, "xcsum_kernels.hip")).read()
+    hdr = open(os.path.join(csrc, "xcsum_csum.h")).read()
+    table = hdr[hdr.index("#define XCSUM_GEOMETRIES"):]
     table = table[:table.index("\n\n")]
     reg = [tuple(map(int, m)) for m in re.findall(r"X\((\d+), (\d+), (\d+)\)", table)]
     lds = [tuple(map(int, m)) for m in re.findall(
