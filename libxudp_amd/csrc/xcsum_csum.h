@@ -447,6 +447,14 @@ static hipError_t launch_t(const CsumArgs &a, int cus, int bpc, hipStream_t s)
 	X(8, 1, 2) X(8, 2, 1) X(8, 1, 12) X(4, 2, 2) X(4, 4, 2) X(4, 1, 2) \
 	X(2, 1, 4) X(2, 2, 4) X(1, 1, 6) X(1, 1, 8) X(1, 2, 6)
 
+/* extra geometries for tuning sweeps only (make variant DEFS=-DXCSUM_SWEEP_GEOMS):
+ * plain instantiation, not in the tested table */
+#ifdef XCSUM_SWEEP_GEOMS
+#define XCSUM_SWEEP_GEOMETRIES(X) X(16, 3, 6) X(16, 4, 6) X(32, 2, 3) X(32, 3, 3) X(16, 3, 5) X(8, 4, 12)
+#else
+#define XCSUM_SWEEP_GEOMETRIES(X)
+#endif
+
 } /* namespace xcsum */
 
 #endif

@@ -450,6 +450,7 @@ bool geometry_supported(Geometry g)
 		return true;
 #define X(g_, u_, k_) if (g.G == g_ && g.U == u_ && g.K == k_) return true;
 	XCSUM_GEOMETRIES(X)
+	XCSUM_SWEEP_GEOMETRIES(X)
 #undef X
 	return false;
 }
