@@ -85,6 +85,7 @@ struct RxArgs {
 	struct xcsum_rx_msg *msgs;
 	uint32_t *count;               /* may be null */
 	uint32_t *part;                /* per-block counts (ctx scratch, RX_PART_MAX) */
+	Order ord;                     /* visiting order (set by launch_rx) */
 };
 
 /* per-block delivered counts of one receive launch: >= CUs x blocks per CU */

@@ -251,6 +251,30 @@ static __device__ __forceinline__ u32x3 rx_desc(const RxArgs &a, uint32_t q)
 	return *((gu32x3 *)(a.desc + (q < a.n ? q : a.n - 1)));
 }
 
+/* Visiting order of a receive batch (as resolve_order in xcsum_csum.h): the
+ * prepared region order only when the batch is sparse in the UMEM -- the
+ * first and last descriptors span more than twice the bytes of n frames of
+ * their mean length, as the frames of an AF_XDP RX ring are, one per 2-4 KB
+ * chunk -- else descriptor order.  Wave-uniform scalar loads. */
+typedef __attribute__((address_space(4))) const u32x3 cu32x3;
+
+static __device__ __forceinline__ void rx_resolve_order(RxArgs &a)
+{
+	if (!a.ord.sparse_only)
+		return;
+	bool sparse = false;
+	if (a.n >= 2) {
+		const u32x3 d0 = *((cu32x3 *)(a.desc));
+		const u32x3 dl = *((cu32x3 *)(a.desc + (a.n - 1)));
+		const uint64_t a0 = ((uint64_t)d0.y << 32) | d0.x;
+		const uint64_t al = ((uint64_t)dl.y << 32) | dl.x;
+		const uint64_t mean = ((uint64_t)d0.z + dl.z) / 2 + 1;
+		sparse = al > a0 && al + dl.z - a0 > 2ull * a.n * mean;
+	}
+	if (!sparse)
+		a.ord = order_identity(a.n);
+}
+
 static __device__ __forceinline__ RFrame rx_resolve(const RxArgs &a, u32x3 d, bool present)
 {
 	RFrame f;
@@ -541,7 +565,12 @@ __global__ void __launch_bounds__(256) rx_kernel(RxArgs a)
 	uint32_t delivered = 0;
 	if (lane == 0)
 		st[SW - 1] = 0u;
-	auto desc = [&](uint32_t q) { return rx_desc(a, q); };
+	rx_resolve_order(a);
+	/* q is a logical index: frame frame_of(q), present below a.n */
+	const uint32_t limit = a.ord.nlog;
+	auto phys = [&](uint32_t q) { return frame_of(a.ord, q); };
+	auto has = [&](uint32_t q) { return q < limit && phys(q) < a.n; };
+	auto desc = [&](uint32_t q) { return rx_desc(a, phys(q)); };
 
 	/* set A holds frames p + u*nseg, set B frames p + (U + u)*nseg */
 	u32x3 d[U];
@@ -552,7 +581,7 @@ __global__ void __launch_bounds__(256) rx_kernel(RxArgs a)
 		d[u] = desc(seg + u * nseg);
 #pragma unroll
 	for (int u = 0; u < U; u++) {
-		fa[u] = rx_resolve(a, d[u], seg + u * nseg < a.n);
+		fa[u] = rx_resolve(a, d[u], has(seg + u * nseg));
 		d[u] = desc(seg + (U + u) * nseg);
 	}
 	__builtin_amdgcn_sched_barrier(0);
@@ -560,10 +589,10 @@ __global__ void __launch_bounds__(256) rx_kernel(RxArgs a)
 	for (int u = 0; u < U; u++)
 		rx_issue<G, K>(a, fa[u], lane, va[u]);
 
-	for (uint32_t p = seg; p < a.n; p += 2 * U * nseg) {
+	for (uint32_t p = seg; p < limit; p += 2 * U * nseg) {
 #pragma unroll
 		for (int u = 0; u < U; u++) {
-			fb[u] = rx_resolve(a, d[u], p + (U + u) * nseg < a.n);
+			fb[u] = rx_resolve(a, d[u], has(p + (U + u) * nseg));
 			d[u] = desc(p + (2 * U + u) * nseg);
 		}
 		__builtin_amdgcn_sched_barrier(0);
@@ -576,12 +605,12 @@ __global__ void __launch_bounds__(256) rx_kernel(RxArgs a)
 		__builtin_amdgcn_sched_barrier(0);
 #pragma unroll
 		for (int u = 0; u < U; u++)
-			rx_frame<G, K>(a, st, span, fa[u], va[u], p + u * nseg, lane, verify, iphdr,
+			rx_frame<G, K>(a, st, span, fa[u], va[u], phys(p + u * nseg), lane, verify, iphdr,
 				       delivered);
 
 #pragma unroll
 		for (int u = 0; u < U; u++) {
-			fa[u] = rx_resolve(a, d[u], p + (2 * U + u) * nseg < a.n);
+			fa[u] = rx_resolve(a, d[u], has(p + (2 * U + u) * nseg));
 			d[u] = desc(p + (3 * U + u) * nseg);
 		}
 		__builtin_amdgcn_sched_barrier(0);
@@ -591,8 +620,8 @@ __global__ void __launch_bounds__(256) rx_kernel(RxArgs a)
 		__builtin_amdgcn_sched_barrier(0);
 #pragma unroll
 		for (int u = 0; u < U; u++)
-			rx_frame<G, K>(a, st, span, fb[u], vb[u], p + (U + u) * nseg, lane, verify, iphdr,
-				       delivered);
+			rx_frame<G, K>(a, st, span, fb[u], vb[u], phys(p + (U + u) * nseg), lane, verify,
+				       iphdr, delivered);
 	}
 	/* The delivered count: one plain store per block, summed by a second
 	 * one-block kernel.  Device-scope atomics to one address serialise
@@ -794,7 +823,11 @@ __global__ void __launch_bounds__(256) rx_wide_kernel(RxArgs a)
 	const uint32_t nw = gridDim.x * 4u;
 	const bool verify = (a.flags & XCSUM_F_VERIFY) != 0;
 	const bool iphdr = (a.flags & XCSUM_F_IPHDR) != 0;
-	const uint32_t nb = (a.n + 63u) / 64u;
+	/* batch b: logical frames 64b..64b+63, one 64-frame tile of the visiting
+	 * order (launch_rx prepares tiles of 2^6), so frames base(b) + wl */
+	rx_resolve_order(a);
+	const uint32_t nb = (a.ord.nlog + 63u) / 64u;
+	auto base = [&](uint32_t bb) { return frame_of(a.ord, bb * 64u); };
 	const uint8_t *zero = (const uint8_t *)g_rx_zero;
 	uint32_t delivered = 0;
 
@@ -824,14 +857,16 @@ __global__ void __launch_bounds__(256) rx_wide_kernel(RxArgs a)
 	};
 
 	uint32_t b = wid;
-	RFrame f = rx_resolve(a, rx_desc(a, b * 64u + wl), b * 64u + wl < a.n);
+	uint32_t fb = b < nb ? base(b) : a.n;   /* frame of lane 0 */
+	RFrame f = rx_resolve(a, rx_desc(a, fb + wl), fb + wl < a.n);
 	u32x4 hv[WHDR];
 	hdr_issue(f, hv);
 	for (; b < nb; b += nw) {
 		const uint32_t bn = b + nw;
-		const u32x3 dn = rx_desc(a, bn * 64u + wl);
+		const uint32_t fbn = bn < nb ? base(bn) : a.n;
+		const u32x3 dn = rx_desc(a, fbn + wl);
 		WParse P = rx_parse_lane(f, hv, hstage, threadIdx.x, verify);
-		const RFrame fn = rx_resolve(a, dn, bn * 64u + wl < a.n);
+		const RFrame fn = rx_resolve(a, dn, fbn + wl < a.n);
 		__builtin_amdgcn_sched_barrier(0);
 		const bool spans = __builtin_amdgcn_ballot_w64(P.want) != 0;
 		/* the next batch's headers: HDR_LEAD steps before this batch's
@@ -942,11 +977,11 @@ __global__ void __launch_bounds__(256) rx_wide_kernel(RxArgs a)
 			__builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
 			__builtin_amdgcn_wave_barrier();
 			__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-			u32x4 *m = (u32x4 *)(a.msgs + b * 64u);
+			u32x4 *m = (u32x4 *)(a.msgs + fb);
 #pragma unroll
 			for (uint32_t i = 0; i < 4; i++) {
 				const u32x4 v = *((const u32x4 *)(wst + 256u * i + 4u * wl));
-				if (b * 64u + 16u * i + (wl >> 2) < a.n)
+				if (fb + 16u * i + (wl >> 2) < a.n)
 					m[64u * i + wl] = v;
 			}
 			__builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -956,6 +991,7 @@ __global__ void __launch_bounds__(256) rx_wide_kernel(RxArgs a)
 				delivered++;
 		}
 		f = fn;
+		fb = fbn;
 	}
 	if (a.count) {
 		__shared__ uint32_t wsum[4];
@@ -1029,6 +1065,7 @@ hipError_t launch_rx(const RxArgs &a, uint32_t len_hint, int cus, hipStream_t s)
 {
 	if (a.n == 0)
 		return hipSuccess;
+	RxArgs b = a;
 	int G, K, U = 1, B = 0;
 	/* "G,K[,U[,B]]" for sweeps and tests; B = blocks per CU (0: occupancy) */
 	const char *e = getenv("XCSUM_RX_GEOMETRY");
@@ -1065,8 +1102,28 @@ hipError_t launch_rx(const RxArgs &a, uint32_t len_hint, int cus, hipStream_t s)
 		else { G = 64; K = 9; U = 0; }   /* lane-per-frame parse: config 5
 						  * 7.73 -> 6.93 ms (rxwide/) */
 	}
+	/* visiting order for frames spread over the UMEM (one per 2-4 KB
+	 * chunk, as an AF_XDP RX ring delivers them): 32 regions of 64-frame
+	 * tiles (the batch-per-wave kernel needs >= 64: a batch is one tile, so
+	 * its records stay contiguous); resolved in-kernel (rx_resolve_order),
+	 * packed batches keep descriptor order.  On 4096-B chunks
+	 * (tools/sweep_rx_order.sh, profiles/r02/rx_order/): config 2 VERIFY
+	 * 0.345 -> 0.321 ms, header-only 0.0755 -> 0.069, config 3 VERIFY
+	 * 0.070 -> 0.067; 8 or 128 regions and 16-frame tiles were slower.
+	 * XCSUM_RX_ORDER=0 turns it off, "R,T" sets it (A/B). */
+	const char *oe = getenv("XCSUM_RX_ORDER");
+	int rlog = 5, tlog = 6;
+	if (oe && sscanf(oe, "%d,%d", &rlog, &tlog) == 1 && rlog == 0) {
+		b.ord = order_identity(a.n);   /* "0": off */
+	} else {
+		/* "R,T": 2^R regions of 2^T-frame tiles (sweeps) */
+		if (U == 0 && tlog < 6)
+			tlog = 6;
+		b.ord = order_regions(a.n, rlog, tlog);
+		b.ord.sparse_only = 1u;
+	}
 #define X(g_, k_, u_) \
-	if (G == g_ && K == k_ && U == u_) return launch_rx_t<g_, k_, u_>(a, cus, B, s);
+	if (G == g_ && K == k_ && U == u_) return launch_rx_t<g_, k_, u_>(b, cus, B, s);
 	XCSUM_RX_GEOMETRIES(X)
 #undef X
 	return hipErrorInvalidValue;

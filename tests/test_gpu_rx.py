@@ -97,6 +97,48 @@ def test_rx_generated_vs_oracle(torch_cuda, engine, geometry):
             assert count == int((exp["status"] == X.RX_OK).sum())
 
 
+def umem_chunks(frames, rng, n):
+    """n frames one per chunk (xudp's UMEM: frame i in chunk i at a fixed
+    headroom plus a small jitter), the layout the region order is for"""
+    chunk = 4096
+    while chunk < max(len(f) for f in frames) + 512:
+        chunk *= 2
+    pick = [frames[i] for i in rng.integers(0, len(frames), n)]
+    offs = np.arange(n, dtype=np.uint64) * chunk + 256 + rng.integers(0, 8, n).astype(np.uint64)
+    umem = np.zeros(n * chunk + 64, dtype=np.uint8)
+    for o, f in zip(offs, pick):
+        umem[int(o):int(o) + len(f)] = np.frombuffer(f, dtype=np.uint8)
+    desc = np.zeros(n, dtype=X.DESC_DTYPE)
+    desc["addr"], desc["len"] = offs, [len(f) for f in pick]
+    return umem, desc
+
+
+@pytest.mark.parametrize("order", ["auto", "0"])
+@pytest.mark.parametrize("geometry", [None, "4,2,1", "16,3,1", "4,2,0", "32,3,0", "64,9,0"])
+def test_rx_sparse_umem_vs_oracle(torch_cuda, engine, geometry, order):
+    """Frames one per UMEM chunk (sparse: the kernels visit them in region
+    order, launch_rx) and a batch size that leaves the last tiles partly or
+    wholly past the end: the same records and count as the oracle, with the
+    order on and off (XCSUM_RX_ORDER=0)."""
+    frames = [f for f, _ in rx_frames.corpus(seed=11)]
+    rng = np.random.default_rng(12)
+    umem, desc = umem_chunks(frames, rng, 4099)
+    old = os.environ.pop("XCSUM_RX_ORDER", None)
+    if order != "auto":
+        os.environ["XCSUM_RX_ORDER"] = order
+    try:
+        for flags in FLAGS.values():
+            exp = oracle.rx_batch(umem, desc, flags)
+            recs, count = run_rx(torch_cuda, engine, umem, desc, flags, 1500, geometry)
+            bad = np.nonzero(recs.view(np.uint8).reshape(-1, 64) != exp.view(np.uint8).reshape(-1, 64))
+            assert len(bad[0]) == 0, (flags, sorted(set(bad[0].tolist()))[:10])
+            assert count == int((exp["status"] == X.RX_OK).sum())
+    finally:
+        os.environ.pop("XCSUM_RX_ORDER", None)
+        if old is not None:
+            os.environ["XCSUM_RX_ORDER"] = old
+
+
 def test_rx_empty_batch(torch_cuda, engine):
     dev = torch_cuda.device("cuda:0")
     d = torch_cuda.zeros(64, dtype=torch_cuda.uint8, device=dev)

@@ -37,6 +37,9 @@ def main():
     ap.add_argument("--reps", type=int, default=7, help="interleaved rounds")
     ap.add_argument("--no-count", action="store_true", help="pass d_count = NULL")
     ap.add_argument("--reverse", action="store_true", help="time the modes in reverse order")
+    ap.add_argument("--layout", default="packed", choices=["packed", "umem"],
+                    help="frames packed (default) or one per 4096-byte chunk as in xudp's "
+                         "UMEM (eth at chunk + 342 / + 322, SURVEY a14)")
     ap.add_argument("--only", default="", help="comma list of modes to run: plain, verify, "
                     "verify_iphdr, csum_verify, csum (default: all)")
     args = ap.parse_args()
@@ -48,7 +51,10 @@ def main():
         cfg = bench.CONFIGS[cid]
         n, fam = cfg["n"], cfg["family"]
         seed = bench.SEED_BASE ^ cid
-        desc, nbytes = X.gen_layout(n, fam, cfg["pmin"], cfg["pmax"], seed=seed)
+        kw = dict(stride=4096, offset=322 if fam == 6 else 342) if args.layout == "umem" else {}
+        if args.layout == "umem" and cfg["pmax"] > 3700:
+            continue   # jumbo frames do not fit a 4096-byte chunk
+        desc, nbytes = X.gen_layout(n, fam, cfg["pmin"], cfg["pmax"], seed=seed, **kw)
         d_desc = torch.from_numpy(desc.view(np.uint8)).to(dev)
         nrot = max(1, math.ceil((1 << 30) / nbytes))
         bufs = [torch.empty(nbytes + 64, dtype=torch.uint8, device=dev) for _ in range(nrot)]
@@ -97,6 +103,7 @@ def main():
             for fname, flags in (names[::-1] if args.reverse else names):
                 read = frame_bytes if flags else 64 * n
                 runs.append(({"kernel": "rx", "config": cid, "flags": fname, "geometry": gname,
+                              "layout": args.layout,
                               "moved": read + n * (16 + 64)}, rx_fn(flags, gname), flags))
         runs.append(({"kernel": "csum_verify", "config": cid, "flags": "verify",
                       "moved": frame_bytes + n * 18}, csum_fn(X.F_VERIFY), None))
