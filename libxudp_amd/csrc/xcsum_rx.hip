@@ -14,8 +14,8 @@
  * frame length: received frames may carry Ethernet padding), so loading the
  * span after parsing would put a dependent HBM round trip on every frame.
  * Instead the kernel loads the WHOLE frame speculatively from the descriptor
- * alone -- 16-byte chunks on a dword grid laid back from the frame end
- * rounded up to 4 bytes, reaching down to the EtherType at eth+12 -- with the
+ * alone -- the 16-byte aligned blocks from the one holding the EtherType at
+ * eth+12 to the one holding the frame's last byte -- with the
  * checksum kernel's two-stage software pipeline (frame i+1's chunks and frame
  * i+2's descriptor in flight while frame i is processed).  When frame i's
  * chunks land:
@@ -40,8 +40,10 @@
  * the header work one frame per lane, 64 frames per wave, and then sums the
  * spans G lanes per frame (see its comment).
  *
- * d_umem must be 4-byte aligned: the first chunk may start up to 3 bytes
- * before a frame whose address is not (it never leaves the frame's dword).
+ * d_umem must be 4-byte aligned (the ABI's rule).  The first chunk may start
+ * up to 15 bytes before eth+12 and the last end up to 15 bytes after the
+ * frame: neither leaves the 16-byte block of a frame byte, so neither can
+ * touch an unmapped page.
  */
 #include "xcsum_internal.h"
 #include "xcsum_device.h"
@@ -231,8 +233,8 @@ static __device__ Rec rx_slow(const uint8_t *pkt, uint32_t len, uint32_t lane, b
 
 constexpr uint32_t STAGE_CHUNKS = 6;   /* 96 bytes from the chunk holding eth+12 */
 
-/* A frame's chunk grid: dword grid laid back from E4 = (eth + len) rounded up
- * to 4, down to the chunk holding eth + 12.  Chunk c covers frame bytes
+/* A frame's chunk grid: the 16-byte aligned blocks from the one holding
+ * eth + 12 to the one holding the last byte.  Chunk c covers frame bytes
  * [g0 + 16c, g0 + 16c + 16) with g0 = 12 - h, h = offset of eth + 12 in chunk 0
  * (0..15), so frame byte x sits at stage byte x - 12 + h.  Everything but the
  * frame pointer is a 32-bit frame-relative offset (registers: two frames are
@@ -293,22 +295,23 @@ static __device__ __forceinline__ uint32_t rx_len(const RFrame &f)
 	return f.meta & 0x7fffffffu;
 }
 
-/* chunk count and h (registers are scarce: recomputed where needed) */
+/* chunk count and h (registers are scarce: recomputed where needed): the
+ * 16-byte blocks from the one holding eth + 12 to the one holding the
+ * frame's last byte.  Aligned chunks: the dword grid laid back from the
+ * frame end that this replaced made every load straddle two 16-byte blocks
+ * when the end was not 16-byte aligned, and cost 3-8 % at MTU
+ * (profiles/r02/rx/ab_grid16/). */
 static __device__ __forceinline__ uint32_t rx_nchunks(const RFrame &f)
 {
 	const uint32_t len = rx_len(f);
-	/* E4 - (eth + 12), with E4 = (eth + len + 3) & ~3 */
-	const uint32_t span = (((uint32_t)(uintptr_t)f.eth + len + 3u) & ~3u) -
-			      ((uint32_t)(uintptr_t)f.eth + 12u);
-	return (rx_present(f) && len >= 14) ? (span + 15u) >> 4 : 0u;
+	const uint32_t e = (uint32_t)(uintptr_t)f.eth;
+	const uint32_t span = ((e + len + 15u) & ~15u) - ((e + 12u) & ~15u);
+	return (rx_present(f) && len >= 14) ? span >> 4 : 0u;
 }
 
 static __device__ __forceinline__ uint32_t rx_h(const RFrame &f, uint32_t nchunks)
 {
-	const uint32_t len = rx_len(f);
-	const uint32_t span = (((uint32_t)(uintptr_t)f.eth + len + 3u) & ~3u) -
-			      ((uint32_t)(uintptr_t)f.eth + 12u);
-	return nchunks ? 16u * nchunks - span : 0u;
+	return nchunks ? ((uint32_t)(uintptr_t)f.eth + 12u) & 15u : 0u;
 }
 
 /* frame-relative offset of chunk c's first byte */
