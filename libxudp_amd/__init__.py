@@ -52,7 +52,10 @@ LDS_GEOMETRIES = [(16, 12, 6), (16, 13, 6), (16, 12, 3), (16, 14, 3)]
 # stream kernel (csum_stream_kernel<KC>): a wave per 64 packed frames, the
 # region they occupy streamed through a KC-KiB LDS stage: G = 64, U = 0, K = KC
 STREAM_GEOMETRIES = [(64, 0, 4), (64, 0, 8), (64, 0, 16)]
-GEOMETRIES = REG_GEOMETRIES + LDS_GEOMETRIES + STREAM_GEOMETRIES
+# segmented stream for packed large / mixed frames (A/B, not a default):
+# (64, frames per unit, rows in flight)
+SEG_GEOMETRIES = [(64, 64, 4), (64, 64, 8), (64, 16, 4)]
+GEOMETRIES = REG_GEOMETRIES + LDS_GEOMETRIES + STREAM_GEOMETRIES + SEG_GEOMETRIES
 
 F_BUILD_INPLACE = 0x20
 F_SRC_ALIGNED = 0x40

@@ -41,6 +41,20 @@ static __device__ __forceinline__ void resolve_order(CsumArgs &a)
 		a.ord = order_identity(a.n);
 }
 
+/* dense batch: the first and last descriptors span at most twice the bytes
+ * of n frames of their mean length (the converse of resolve_order) */
+static __device__ __forceinline__ bool dense_batch(const CsumArgs &a)
+{
+	if (a.n < 2)
+		return true;
+	const u32x4 d0 = *((cu32x4 *)(a.desc));
+	const u32x4 dl = *((cu32x4 *)(a.desc + (a.n - 1)));
+	const uint64_t a0 = ((uint64_t)d0.y << 32) | d0.x;
+	const uint64_t al = ((uint64_t)dl.y << 32) | dl.x;
+	const uint64_t mean = ((uint64_t)d0.z + dl.z) / 2 + 1;
+	return !(al > a0 && al + dl.z - a0 > 2ull * a.n * mean);
+}
+
 template <bool UNIFORM>
 static __device__ __forceinline__ u32x4 load_desc(const CsumArgs &a, uint32_t p)
 {

@@ -100,6 +100,10 @@ struct Geometry {
 	int B; /* 256-thread blocks per CU (0: occupancy limit) */
 };
 
+/* segmented-stream checksum kernel (csrc/xcsum_seg.hip): Geometry{64, F, D},
+ * F frames per unit, D rows of 1 KiB in flight per wave */
+#define XCSUM_SEG_GEOMETRIES(X) X(64, 4) X(64, 8) X(16, 4)
+hipError_t launch_seg(const CsumArgs &a, int F, int D, int cus, int bpc, hipStream_t s);
 Geometry pick_geometry(uint32_t len_hint);
 /* gather: stage each frame on its own (pinned host copy, frames packed)
  * instead of copying the UMEM range the chunk's frames span -- for frames

@@ -194,20 +194,6 @@ struct StreamSpan {
 	uint32_t present;   /* frame index < n */
 };
 
-/* dense batch: the first and last descriptors span at most twice the bytes
- * of n frames of their mean length (the converse of resolve_order) */
-static __device__ __forceinline__ bool dense_batch(const CsumArgs &a)
-{
-	if (a.n < 2)
-		return true;
-	const u32x4 d0 = *((cu32x4 *)(a.desc));
-	const u32x4 dl = *((cu32x4 *)(a.desc + (a.n - 1)));
-	const uint64_t a0 = ((uint64_t)d0.y << 32) | d0.x;
-	const uint64_t al = ((uint64_t)dl.y << 32) | dl.x;
-	const uint64_t mean = ((uint64_t)d0.z + dl.z) / 2 + 1;
-	return !(al > a0 && al + dl.z - a0 > 2ull * a.n * mean);
-}
-
 /* the 4 LDS bytes at byte offset o (any alignment), little-endian */
 static __device__ __forceinline__ uint32_t lds_bytes4(const uint8_t *st, uint32_t o)
 {
@@ -243,10 +229,10 @@ static __device__ __forceinline__ void stream_loop(const CsumArgs &a, u32x4 *sta
 		const uint64_t end = sp.eth + sp.len;
 		const uint64_t lo =
 			((uint64_t)__builtin_amdgcn_readlane((uint32_t)(sp.eth >> 32), 0) << 32) |
-			__builtin_amdgcn_readlane((uint32_t)sp.eth, 0);
+			(uint32_t)__builtin_amdgcn_readlane((uint32_t)sp.eth, 0);
 		const uint64_t hi =
 			((uint64_t)__builtin_amdgcn_readlane((uint32_t)(end >> 32), last) << 32) |
-			__builtin_amdgcn_readlane((uint32_t)end, last);
+			(uint32_t)__builtin_amdgcn_readlane((uint32_t)end, last);
 		base = lo & ~15ull;
 		const bool out = sp.present && (sp.eth < lo || end > hi);
 		nch = (__builtin_amdgcn_ballot_w64(out) || hi < lo || hi - base > (uint64_t)KC * 1024u)
@@ -444,6 +430,9 @@ bool geometry_supported(Geometry g)
 {
 	if (g.G == 64 && g.U == 0 && (g.K == 4 || g.K == 8 || g.K == 16))
 		return true;
+#define X(f_, d_) if (g.G == 64 && g.U == f_ && g.K == d_) return true;
+	XCSUM_SEG_GEOMETRIES(X)
+#undef X
 	if (g.G == 16 && ((g.U == 12 || g.U == 13) && g.K == 6))
 		return true;
 	if (g.G == 16 && ((g.U == 12 || g.U == 14) && g.K == 3))
@@ -467,6 +456,10 @@ hipError_t launch_csum(const CsumArgs &a, Geometry g, int cus, hipStream_t s)
 		if (g.K == 16) return launch_stream_t<16>(a, cus, g.B, s);
 		return hipErrorInvalidValue;
 	}
+	/* segmented stream: G = 64 lanes, U = frames per unit (8..64), K = rows
+	 * in flight (XCSUM_SEG_GEOMETRIES) */
+	if (g.G == 64 && g.U >= 8)
+		return launch_seg(a, g.U, g.K, cus, g.B, s);
 	CsumArgs b = a;
 	b.ord = order_identity(a.n);
 	if (g.G == 16 && g.U == 12 && g.K == 6) return launch_lds_t<6, 2>(b, cus, g.B, s);

@@ -138,7 +138,7 @@ def test_argument_validation_without_gpu():
 def test_geometry_list_matches_kernel_source():
     """X.GEOMETRIES (what the parity tests sweep) == the instantiations in
     the XCSUM_GEOMETRIES table (csrc/xcsum_csum.h, instantiated per feature set
-    in xcsum_csum_f{0,1,2}.hip) + the LDS and stream dispatch of
+    in xcsum_csum_f{0,1,2}.hip) + the LDS, stream and segmented-stream dispatch of
     csrc/xcsum_kernels.hip."""
     import re
     csrc = os.path.join(ROOT, "libxudp_amd", "csrc")
@@ -151,6 +151,11 @@ def test_geometry_list_matches_kernel_source():
         r"g\.G == (\d+) && g\.U == (\d+) && g\.K == (\d+)\) return launch_lds_t", src)]
     stream = [(64, 0, int(k)) for k in re.findall(
         r"if \(g\.K == (\d+)\) return launch_stream_t", src)]
+    internal = open(os.path.join(csrc, "xcsum_internal.h")).read()
+    segt = internal[internal.index("#define XCSUM_SEG_GEOMETRIES"):]
+    segt = segt[:segt.index("\n")]
+    seg = [(64, int(f), int(d)) for f, d in re.findall(r"X\((\d+), (\d+)\)", segt)]
+    assert sorted(seg) == sorted(X.SEG_GEOMETRIES)
     assert reg == X.REG_GEOMETRIES
     assert sorted(lds) == sorted(X.LDS_GEOMETRIES)
     assert sorted(stream) == sorted(X.STREAM_GEOMETRIES)

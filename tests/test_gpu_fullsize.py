@@ -111,6 +111,27 @@ def test_config5_digest_8m_mixed(torch_cuda, engine, digests):
     assert sha(np.concatenate(parts)) == dg["sha256_out"]
 
 
+def test_config5_every_jumbo_geometry_same_digest(torch_cuda, engine, digests):
+    """Config 5 through the segmented stream (every D) and the frame-group
+    kernel it replaced as the default: the reference's digest each time;
+    then INPLACE and a VERIFY pass over the written frames."""
+    cfg, desc, d_desc, d_umem = device_batch(torch_cuda, engine, 5)
+    for g in X.SEG_GEOMETRIES + [(64, 1, 9)]:
+        engine.set_geometry(*g)
+        try:
+            got = run(torch_cuda, engine, d_umem, d_desc, len(desc), cfg["mode"])
+        finally:
+            engine.set_geometry(0)
+        assert sha(got) == digests["config5"]["sha256_out"], g
+    engine.set_geometry(*X.SEG_GEOMETRIES[-1])
+    try:
+        run(torch_cuda, engine, d_umem, d_desc, len(desc), X.MODE_V4_RFC, X.F_INPLACE)
+        ok = run(torch_cuda, engine, d_umem, d_desc, len(desc), X.MODE_V4_RFC, X.F_VERIFY)
+    finally:
+        engine.set_geometry(0)
+    assert (ok == 0).all()
+
+
 @pytest.mark.parametrize("cid,mode", [(2, X.MODE_V4_RFC), (4, X.MODE_V6)])
 def test_verify_after_inplace_write(torch_cuda, engine, cid, mode):
     """RFC property: once udp->check holds the checksum, the one's complement

@@ -1,0 +1,69 @@
+"""GPU: frames at UMEM offsets across 2 GiB and 4 GiB (a 4.3 GB device
+buffer).  The kernels carry UMEM offsets in 64 bits but move them between
+lanes as 32-bit halves (v_readlane, ds_bpermute); a sign-extended low half
+once broke every offset with bit 31 set (found by the config-5 digest, 37 GB
+of UMEM).  Each kernel family sees packed batches straddling both
+boundaries, checked against the oracle on the same frames at offset 0."""
+import numpy as np
+import pytest
+
+import libxudp_amd as X
+import oracle
+
+pytestmark = pytest.mark.gpu
+
+OFFSETS = [(1 << 31) - 5000, (1 << 32) - 3000]
+GEOMS = [None, (16, 2, 6), (64, 1, 9), (4, 1, 2)] + X.STREAM_GEOMETRIES[1:2] + X.SEG_GEOMETRIES
+
+
+@pytest.fixture(scope="module")
+def big(torch_cuda):
+    buf = torch_cuda.zeros((1 << 32) + (64 << 20), dtype=torch_cuda.uint8, device="cuda:0")
+    yield buf
+    del buf
+    torch_cuda.cuda.empty_cache()
+
+
+def place(torch, big, umem, desc, off):
+    big[off:off + len(umem)] = torch.from_numpy(umem).to(big.device)
+    d = desc.copy()
+    d["addr"] += off
+    return torch.from_numpy(d.view(np.uint8)).to(big.device)
+
+
+@pytest.mark.parametrize("geom", GEOMS)
+@pytest.mark.parametrize("sizes", [(0, 64), (1400, 1500), (0, 9000)])
+def test_checksum_across_2g_and_4g(torch_cuda, engine, big, geom, sizes):
+    umem, desc = X.gen_frames_host(700, 4, sizes[0], sizes[1], seed=sizes[1])
+    exp = oracle.batch(umem, desc, X.MODE_V4_LEGACY)
+    if geom is not None:
+        engine.set_geometry(*geom)
+    try:
+        for off in OFFSETS:
+            d_desc = place(torch_cuda, big, umem, desc, off)
+            out = torch_cuda.zeros(len(desc), dtype=torch_cuda.int16, device="cuda:0")
+            engine.batch_device(big, d_desc, len(desc), out, X.MODE_V4_LEGACY, 0,
+                                int(desc["len"].mean()))
+            torch_cuda.cuda.synchronize()
+            assert np.array_equal(out.cpu().numpy().view(np.uint16), exp), (geom, off)
+    finally:
+        engine.set_geometry(0)
+
+
+@pytest.mark.parametrize("geometry", [None, "4,2,1", "32,3,0", "64,9,0"])
+def test_receive_across_2g_and_4g(torch_cuda, engine, big, geometry, monkeypatch):
+    umem, desc = X.gen_frames_host(700, 6, 0, 3000, seed=3)
+    exp = oracle.rx_batch(umem, desc, X.F_VERIFY)
+    if geometry:
+        monkeypatch.setenv("XCSUM_RX_GEOMETRY", geometry)
+    for off in OFFSETS:
+        d_desc = place(torch_cuda, big, umem, desc, off)
+        msgs = torch_cuda.zeros(len(desc) * 64, dtype=torch_cuda.uint8, device="cuda:0")
+        engine.rx_device(big, d_desc, len(desc), msgs, None, X.F_VERIFY, 1500)
+        torch_cuda.cuda.synchronize()
+        got = msgs.cpu().numpy().view(X.RX_MSG_DTYPE)
+        # records hold UMEM offsets: compare with the expected ones moved by off
+        e = exp.copy()
+        e["frame"] += off
+        e["body"][e["body"] != 0] += off
+        assert np.array_equal(got.view(np.uint8), e.view(np.uint8)), (geometry, off)

@@ -19,7 +19,7 @@ pytestmark = pytest.mark.gpu
 GEOMETRIES = X.GEOMETRIES
 # the default pick plus the LDS-staged variant: the feature tests below run
 # under each, so both kernels see INPLACE/IPHDR/VERIFY, ragged and maximum sizes
-FEATURE_GEOMS = [None] + X.LDS_GEOMETRIES + X.STREAM_GEOMETRIES
+FEATURE_GEOMS = [None] + X.LDS_GEOMETRIES + X.STREAM_GEOMETRIES + X.SEG_GEOMETRIES
 
 
 @contextlib.contextmanager

@@ -18,8 +18,8 @@ import os
 import re
 import statistics
 
-# the checksum kernels: csum_kernel<G,U,K,IPH> and csum_stream_kernel<KC>
-KERNEL = re.compile(r"csum_(stream_)?kernel")
+# the checksum kernels: csum_kernel<G,U,K,FEAT>, csum_stream_kernel<KC>, csum_seg_kernel<D>
+KERNEL = re.compile(r"csum_(stream_|seg_)?kernel")
 
 
 names = set()
