@@ -67,3 +67,44 @@ def test_receive_across_2g_and_4g(torch_cuda, engine, big, geometry, monkeypatch
         e["frame"] += off
         e["body"][e["body"] != 0] += off
         assert np.array_equal(got.view(np.uint8), e.view(np.uint8)), (geometry, off)
+
+
+@pytest.mark.parametrize("inplace", [False, True])
+def test_build_across_2g_and_4g(torch_cuda, engine, big, inplace):
+    """xcsum_build_device into 4096-byte slots around 2 GiB and 4 GiB."""
+    torch = torch_cuda
+    FRAME, DATA_OFF = 4096, 384
+    rng = np.random.default_rng(21)
+    slots = np.concatenate([np.arange((1 << 19) - 12, (1 << 19) + 12),
+                            np.arange((1 << 20) - 12, (1 << 20) + 12)]).astype(np.uint32)
+    n = len(slots)
+    r = dict(smac=bytes(range(6)), dmac=bytes(range(6, 12)), saddr=bytes([10, 0, 0, 1]),
+             daddr=bytes([10, 0, 0, 2]), sport=1234, dport=5678)
+    route = X.make_route(4, r["smac"], r["dmac"], r["saddr"], r["sport"], r["daddr"], r["dport"])
+    pays = [rng.integers(0, 256, int(L), dtype=np.uint8) for L in rng.integers(0, 3000, n)]
+    msgs = np.zeros(n, dtype=X.MSG_DTYPE)
+    msgs["len"] = [len(p) for p in pays]
+    msgs["slot"] = slots
+    if inplace:
+        for s, p in zip(slots, pays):
+            o = int(s) * FRAME + DATA_OFF
+            big[o:o + len(p)] = torch.from_numpy(p).to(big.device)
+        d_src = torch.zeros(16, dtype=torch.uint8, device="cuda:0")
+    else:
+        src = np.concatenate(pays + [np.zeros(16, np.uint8)])
+        msgs["src"] = np.concatenate([[0], np.cumsum([len(p) for p in pays])[:-1]])
+        d_src = torch.from_numpy(src).to("cuda:0")
+    d_msgs = torch.from_numpy(msgs.view(np.uint8)).to("cuda:0")
+    d_desc = torch.zeros(n * 16, dtype=torch.uint8, device="cuda:0")
+    d_out = torch.zeros(n, dtype=torch.int16, device="cuda:0")
+    engine.build_device(route, d_src, d_msgs, n, big, FRAME, DATA_OFF, d_desc, d_out,
+                        X.F_BUILD_INPLACE if inplace else 0, 1500)
+    torch.cuda.synchronize()
+    desc = d_desc.cpu().numpy().view(X.DESC_DTYPE)
+    for i, p in enumerate(pays):
+        exp = oracle.build_frame(p.tobytes(), 4, r["smac"], r["dmac"], r["saddr"], r["sport"],
+                                 r["daddr"], r["dport"], False)
+        eth = int(slots[i]) * FRAME + DATA_OFF - 42
+        assert int(desc["addr"][i]) == eth and int(desc["len"][i]) == len(exp)
+        got = big[eth:eth + len(exp)].cpu().numpy()
+        assert np.array_equal(got, exp), (i, int(slots[i]))
