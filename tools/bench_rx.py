@@ -129,6 +129,12 @@ def main():
                 torch.cuda.synchronize()
                 times[i].append(e0.elapsed_time(e1) / K * 1e-3)
         os.environ.pop("XCSUM_RX_GEOMETRY", None)
+        # clocks while kernels run: the boxes differ on this kernel far more
+        # than on the checksum kernel, and SCLK is the first suspect
+        for k in range(3 * K):
+            runs[0][1](k)
+        clocks = bench.gpu_clocks(dev)
+        torch.cuda.synchronize()
         cv = [i for i, r in enumerate(runs) if r[0]["kernel"] == "csum_verify"]
         t_csum = float(np.median(times[cv[0]])) if cv else float("nan")
         for (rec, fn, flags), ts in zip(runs, times):
@@ -151,7 +157,7 @@ def main():
                         "GBps_moved": round(moved / t / 1e9, 1),
                         "pct_hbm_peak": round(100 * moved / t / 8e12, 1),
                         "vs_csum_verify": round(t / t_csum, 3), "launches_per_round": K,
-                        "rounds": args.reps})
+                        "rounds": args.reps, "clocks_under_load": clocks})
             print(json.dumps(rec), flush=True)
         del bufs, d_msgs
         torch.cuda.empty_cache()
