@@ -115,3 +115,31 @@ def test_fuzz_receive_vs_oracle(torch_cuda, engine, seed):
     assert len(bad) == 0, f"seed {seed}: geometry {geometry} flags {flags:#x} hint {hint}: " \
                           f"records {bad[:8].tolist()}"
     assert count == int((exp["status"] == X.RX_OK).sum())
+
+
+@pytest.mark.parametrize("seed", range(24))
+def test_fuzz_host_path_vs_device(torch_cuda, engine, seed):
+    """xcsum_batch_host (staged copies, or zero-copy from a registered UMEM)
+    on random batches: the same results as the oracle, and with INPLACE the
+    same frame bytes as the device path writes."""
+    rng = np.random.default_rng(3000 + seed)
+    umem, desc = random_batch(rng)
+    mode = MODES[int(rng.integers(len(MODES)))]
+    flags = int(rng.choice([0, X.F_INPLACE, X.F_INPLACE | X.F_IPHDR, X.F_VERIFY,
+                            X.F_VERIFY | X.F_IPHDR]))
+    zerocopy = rng.random() < 0.5
+    exp = oracle.batch(umem, desc, mode, flags & ~X.F_INPLACE)
+    _, exp_after = run_device(torch_cuda, engine, umem, desc, mode, flags)
+    host = umem.copy()
+    out = np.full(len(desc), 0x5a5a, dtype=np.uint16)
+    if zerocopy:
+        engine.register_umem(host)
+    try:
+        engine.batch_host(host, desc, out, mode, flags | (X.F_ZEROCOPY if zerocopy else 0))
+    finally:
+        if zerocopy:
+            engine.unregister_umem(host)
+    bad = np.nonzero(out != exp)[0]
+    assert len(bad) == 0, f"seed {seed}: mode {mode} flags {flags:#x} zerocopy {zerocopy}: " \
+                          f"frames {bad[:8].tolist()}"
+    assert np.array_equal(host, exp_after), f"seed {seed}: in-place bytes differ"
