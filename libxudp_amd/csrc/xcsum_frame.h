@@ -257,6 +257,12 @@ static __device__ __forceinline__ void store_u16(uint8_t *p, uint16_t v)
 	}
 }
 
+/* XCSUM_EDGE_T=1 builds a variant whose first chunk row of each frame is
+ * loaded with the default (temporal) policy at G = 64 (A/B only) */
+#ifndef XCSUM_EDGE_T
+#define XCSUM_EDGE_T 0
+#endif
+
 template <int G, int U, int K>
 static __device__ __forceinline__ void issue(const Frame (&f)[U], uint32_t lane,
 					     u32x4 (&v)[U][K])
@@ -267,7 +273,11 @@ static __device__ __forceinline__ void issue(const Frame (&f)[U], uint32_t lane,
 #pragma unroll
 		for (int k = 0; k < K; k++) {
 			uint32_t c = lane + k * G;
-			v[u][k] = load_chunk(c < f[u].nchunks ? f[u].base + 16u * c : zero);
+			const uint8_t *p = c < f[u].nchunks ? f[u].base + 16u * c : zero;
+			if (XCSUM_EDGE_T && G == 64 && k == 0)
+				v[u][k] = *((gu32x4 *)p);
+			else
+				v[u][k] = load_chunk(p);
 		}
 }
 

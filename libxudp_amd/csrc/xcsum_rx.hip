@@ -806,8 +806,15 @@ static __device__ __forceinline__ uint32_t rx_step_sum(const uint32_t *tab, cons
 	return seg_sum<G>(sum);
 }
 
+/* XCSUM_RX_WIDE_WPE=N builds a variant capped for N waves per SIMD (A/B) */
+#if defined(XCSUM_RX_WIDE_WPE) && XCSUM_RX_WIDE_WPE > 0
+#define RX_WIDE_ATTR __attribute__((amdgpu_waves_per_eu(XCSUM_RX_WIDE_WPE)))
+#else
+#define RX_WIDE_ATTR
+#endif
+
 template <int G, int K>
-__global__ void __launch_bounds__(256) rx_wide_kernel(RxArgs a)
+__global__ void __launch_bounds__(256) RX_WIDE_ATTR rx_wide_kernel(RxArgs a)
 {
 	constexpr uint32_t FPS = 64 / G;        /* frames per step */
 	constexpr uint32_t STEPS = G;           /* 64 frames per batch */

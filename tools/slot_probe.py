@@ -5,6 +5,7 @@ checksum kernel?  Reads only the spans, 1M slots, with (a) packed spans,
 (b) the fixed xudp offset, (c) offsets rotated across the slot, (d) 2048-B
 slots.  One JSON line per case.  Bounds checked on the host: every read ends
 inside the buffer."""
+import argparse
 import ctypes
 import json
 import os
@@ -15,6 +16,10 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 
 
 def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--small", action="store_true",
+                    help="config 3's 80-B spans (64-B payloads) instead of config 2's")
+    args = ap.parse_args()
     L = ctypes.CDLL(os.path.join(HERE, "libhbmprobe.so"))
     L.probe_slot_read.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32,
                                   ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
@@ -24,7 +29,9 @@ def main():
     dev = torch.device("cuda:0")
     cus = torch.cuda.get_device_properties(dev).multi_processor_count
     nslots = 1 << 20
-    span16 = 1488 // 16 + 1                   # 94 x 16 B: a config-2 span
+    # a config-2 span (94 x 16 B) or a config-3 one: 80 B at eth+26 = F+368,
+    # two 64-B lines per 4096-B slot
+    span16 = 5 if args.small else 1488 // 16 + 1
     buf = torch.zeros((nslots * 4096 + 4096,), dtype=torch.uint8, device=dev)
     out = torch.empty(cus * 16 * 256, dtype=torch.int32, device=dev)
     s = torch.cuda.current_stream(dev)
@@ -35,8 +42,13 @@ def main():
              ("4096_fixed_scattered_slots", 4096, 368, 0, 0, 0x9E3779B1, 0),
              ("4096_fixed_scattered_groups16", 4096, 368, 0, 0, 0x9E3779B1, 4),
              ("4096_fixed_scattered_groups256", 4096, 368, 0, 0, 0x9E3779B1, 8),
-             ("xudp_2048_fixed_off_368", 2048, 368, 0, 0, 0, 0),
-             # 16-byte loads at 8/4/2-byte aligned addresses (packed 1520-B slots)
+             ("xudp_2048_fixed_off_368", 2048, 368, 0, 0, 0, 0)]
+    if args.small:
+        cases += [("4096_fixed_scattered_groups64", 4096, 368, 0, 0, 0x9E3779B1, 6),
+                  ("1024_fixed_off_368", 1024, 368, 0, 0, 0, 0),
+                  ("512_fixed_off_368", 512, 368, 0, 0, 0, 0)]
+    else:
+        cases += [  # 16-byte loads at 8/4/2-byte aligned addresses (packed 1520-B slots)
              ("packed1520_align16", 1520, 0, 0, 0, 0, 0),
              ("packed1520_align8", 1520, 8, 0, 0, 0, 0),
              ("packed1520_align4", 1520, 4, 0, 0, 0, 0),
@@ -44,7 +56,9 @@ def main():
              ("2048_rotated_off", 2048, 0, 7, (2048 - span16 * 16) // 16, 0, 0)]
     for name, slot, off0, rot, nrot, pm, ps in cases:
         assert (nslots - 1) * slot + off0 + max(nrot - 1, 0) * 16 + span16 * 16 <= buf.numel()
-        for per_cu in (4, 8):
+        lines = span16 * 16 if slot == span16 * 16 else \
+            64 * ((off0 % 64 + span16 * 16 + 63) // 64)
+        for per_cu in ((4, 8, 16) if args.small else (4, 8)):
             ts = []
             for _ in range(12):
                 a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -55,9 +69,11 @@ def main():
                 torch.cuda.synchronize()
                 ts.append(a.elapsed_time(b))
             t = sorted(ts)[len(ts) // 2]
-            print(json.dumps({"case": name, "slot_bytes": slot, "blocks_per_cu": per_cu,
-                              "ms": round(t, 4),
-                              "GBps": round(nslots * span16 * 16 / (t * 1e-3) / 1e9, 1)}),
+            print(json.dumps({"case": name, "slot_bytes": slot, "span_bytes": span16 * 16,
+                              "blocks_per_cu": per_cu, "ms": round(t, 4),
+                              "GBps": round(nslots * span16 * 16 / (t * 1e-3) / 1e9, 1),
+                              # 64-byte lines the spans touch (= HBM bytes)
+                              "line_GBps": round(nslots * lines / (t * 1e-3) / 1e9, 1)}),
                   flush=True)
 
 
