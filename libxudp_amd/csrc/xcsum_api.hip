@@ -107,6 +107,9 @@ extern "C" int xcsum_ctx_create(int device, xcsum_ctx **out)
 		c->h_rx_msgs[s] = nullptr;
 		c->h_stage[s] = nullptr;
 		c->h_dstage[s] = nullptr;
+		c->v_stage[s] = nullptr;
+		c->v_dstage[s] = nullptr;
+		c->v_out[s] = nullptr;
 	}
 	c->frame_cap = 0;
 	c->desc_cap = 0;
@@ -132,6 +135,9 @@ static void free_staging(xcsum_ctx *c)
 		if (c->h_dstage[s]) (void)hipHostFree(c->h_dstage[s]);
 		c->h_stage[s] = nullptr;
 		c->h_dstage[s] = nullptr;
+		c->v_stage[s] = nullptr;
+		c->v_dstage[s] = nullptr;
+		c->v_out[s] = nullptr;
 		c->d_rx_msgs[s] = nullptr;
 		c->h_rx_msgs[s] = nullptr;
 		c->streams[s] = nullptr;
@@ -426,6 +432,12 @@ static const Region *find_region(const xcsum_ctx *c, const uint8_t *lo, const ui
 
 /* ---- host-resident batches ----------------------------------------------- */
 
+/* Gathered batches of at most this many staged bytes skip the copies (the
+ * kernel works on the pinned stage in place); 0 disables */
+#ifndef XCSUM_DIRECT_MAX
+#define XCSUM_DIRECT_MAX 0
+#endif
+
 static int ensure_staging(xcsum_ctx *c)
 {
 	if (c->frame_cap)
@@ -539,6 +551,13 @@ int batch_host_impl(xcsum_ctx *c, uint8_t *h_umem, const struct xcsum_desc *h_de
 			    hipHostMalloc(&c->h_dstage[s], c->desc_cap * sizeof(struct xcsum_desc), 0) !=
 				    hipSuccess)
 				return -XCSUM_ERR_NOMEM;
+			if (XCSUM_DIRECT_MAX && !c->v_stage[s] &&
+			    (hipHostGetDevicePointer((void **)&c->v_stage[s], c->h_stage[s], 0) != hipSuccess ||
+			     hipHostGetDevicePointer((void **)&c->v_dstage[s], c->h_dstage[s], 0) != hipSuccess ||
+			     hipHostGetDevicePointer((void **)&c->v_out[s], c->h_out[s], 0) != hipSuccess)) {
+				c->v_stage[s] = nullptr;
+				return -XCSUM_ERR_HIP;
+			}
 		}
 	}
 
@@ -587,6 +606,7 @@ int batch_host_impl(xcsum_ctx *c, uint8_t *h_umem, const struct xcsum_desc *h_de
 			pend[slot].busy = false;
 		}
 		hipStream_t st = c->streams[slot];
+		bool direct = false;
 		CsumArgs a;
 		a.desc = c->d_desc[slot];
 		a.n = cnt;
@@ -611,11 +631,23 @@ int batch_host_impl(xcsum_ctx *c, uint8_t *h_umem, const struct xcsum_desc *h_de
 				c->h_dstage[slot][k] = xcsum_desc{off, d.len, 0};
 				pos = off + d.len;
 			}
-			HIPCHK(hipMemcpyAsync(c->d_frames[slot], c->h_stage[slot], pos,
-					      hipMemcpyHostToDevice, st));
-			a.umem = c->d_frames[slot];
 			a.bias = 0;
 			a.flags = flags & (XCSUM_F_IPHDR | XCSUM_F_V4_RFC | XCSUM_F_VERIFY);
+			if (XCSUM_DIRECT_MAX && pos <= XCSUM_DIRECT_MAX) {
+				/* small batch: no copies -- the kernel reads the pinned
+				 * stage over PCIe and writes the pinned result slot; the
+				 * call's latency is one launch, not three transfers and
+				 * a launch */
+				direct = true;
+				a.umem = c->v_stage[slot];
+				a.desc = c->v_dstage[slot];
+				a.out = c->v_out[slot];
+				a.out_ip = want_ip ? c->v_out[slot] + cnt : nullptr;
+			} else {
+				HIPCHK(hipMemcpyAsync(c->d_frames[slot], c->h_stage[slot], pos,
+						      hipMemcpyHostToDevice, st));
+				a.umem = c->d_frames[slot];
+			}
 		} else {
 			/* 16-byte aligned copy of [lo, hi) keeps every frame's address
 			 * parity and 16-byte phase identical to the host UMEM */
@@ -627,13 +659,15 @@ int batch_host_impl(xcsum_ctx *c, uint8_t *h_umem, const struct xcsum_desc *h_de
 			/* the device copy is scratch: in-place writes happen on the host */
 			a.flags = flags & (XCSUM_F_IPHDR | XCSUM_F_V4_RFC | XCSUM_F_VERIFY);
 		}
-		HIPCHK(hipMemcpyAsync(c->d_desc[slot], gather ? c->h_dstage[slot] : h_desc + i,
-				      cnt * sizeof(struct xcsum_desc), hipMemcpyHostToDevice, st));
+		if (!direct)
+			HIPCHK(hipMemcpyAsync(c->d_desc[slot], gather ? c->h_dstage[slot] : h_desc + i,
+					      cnt * sizeof(struct xcsum_desc), hipMemcpyHostToDevice, st));
 		uint32_t avg = (uint32_t)((gather ? gpos : hi - lo) / cnt);
 		HIPCHK(launch_csum(a, geometry_for(c, avg, a.flags), c->cus, st));
-		HIPCHK(hipMemcpyAsync(c->h_out[slot], c->d_out[slot],
-				      (want_ip ? 2 : 1) * cnt * sizeof(uint16_t),
-				      hipMemcpyDeviceToHost, st));
+		if (!direct)
+			HIPCHK(hipMemcpyAsync(c->h_out[slot], c->d_out[slot],
+					      (want_ip ? 2 : 1) * cnt * sizeof(uint16_t),
+					      hipMemcpyDeviceToHost, st));
 		HIPCHK(hipEventRecord(c->done[slot], st));
 		pend[slot].first = i;
 		pend[slot].count = cnt;

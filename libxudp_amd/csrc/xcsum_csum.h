@@ -227,12 +227,12 @@ static __device__ __forceinline__ void finalize(const CsumArgs &a, const Frame &
 			if ((a.flags & XCSUM_F_IPHDR) && f.mode != 2) {
 				uint16_t ipr = ip_header_csum<FEAT == 2>(f, true);
 				if (a.out_ip)
-					a.out_ip[p] = ipr;
+					st_res(a.out_ip + p, ipr);
 				if (wire == 0)
 					wire = ipr;  /* 0 only if both verify */
 			}
 			if (a.out)
-				a.out[p] = wire;
+				st_res(a.out + p, wire);
 			return;
 		}
 		if (f.mode == 0) {
@@ -253,7 +253,7 @@ static __device__ __forceinline__ void finalize(const CsumArgs &a, const Frame &
 			if (a.flags & XCSUM_F_INPLACE)
 				store_u16(f.eth + 24, ipc);
 			if (a.out_ip)
-				a.out_ip[p] = ipc;
+				st_res(a.out_ip + p, ipc);
 		}
 	} else {
 		if (f.mode != -3)        /* -3: UDP length does not fit (VERIFY) */
@@ -262,9 +262,9 @@ static __device__ __forceinline__ void finalize(const CsumArgs &a, const Frame &
 			wire = 0xffffu;  /* a malformed frame never verifies */
 	}
 	if (a.out)
-		a.out[p] = wire;
+		st_res(a.out + p, wire);
 	if (a.out_ip && !((a.flags & XCSUM_F_IPHDR) && f.mode >= 0 && f.mode != 2))
-		a.out_ip[p] = 0;
+		st_res(a.out_ip + p, (uint16_t)0);
 }
 
 /* accumulate, reduce and finalize the U frames of one iteration */

@@ -247,13 +247,28 @@ struct Grid {
 	static constexpr bool DW = XCSUM_GRID_DW || (!(G == 16 && K >= 6) && !(G == 8 && K >= 12));
 };
 
+/* XCSUM_NT_STORE=1 builds a variant whose result and in-place stores are
+ * nontemporal (A/B only) */
+#ifndef XCSUM_NT_STORE
+#define XCSUM_NT_STORE 0
+#endif
+
+template <typename T>
+static __device__ __forceinline__ void st_res(T *p, T v)
+{
+	if (XCSUM_NT_STORE)
+		__builtin_nontemporal_store(v, p);
+	else
+		*p = v;
+}
+
 static __device__ __forceinline__ void store_u16(uint8_t *p, uint16_t v)
 {
 	if (((uintptr_t)p & 1) == 0) {
-		*reinterpret_cast<uint16_t *>(p) = v;
+		st_res(reinterpret_cast<uint16_t *>(p), v);
 	} else {
-		p[0] = (uint8_t)v;
-		p[1] = (uint8_t)(v >> 8);
+		st_res(p, (uint8_t)v);
+		st_res(p + 1, (uint8_t)(v >> 8));
 	}
 }
 

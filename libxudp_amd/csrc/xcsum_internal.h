@@ -153,6 +153,12 @@ struct Ctx {
 	struct xcsum_rx_msg *h_rx_msgs[NSLOT];  /* pinned */
 	uint8_t *h_stage[NSLOT];       /* gathered frames (pinned, lazy) */
 	struct xcsum_desc *h_dstage[NSLOT];     /* their descriptors (pinned, lazy) */
+	/* device addresses of the pinned stage, its descriptors and the result
+	 * slot: small gathered batches are read and answered in place by the
+	 * kernel, no copies (batch_host_impl) */
+	uint8_t *v_stage[NSLOT];
+	struct xcsum_desc *v_dstage[NSLOT];
+	uint16_t *v_out[NSLOT];
 	size_t frame_cap;              /* bytes per slot */
 	uint32_t desc_cap;             /* frames per slot */
 };

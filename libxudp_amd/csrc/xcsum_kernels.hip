@@ -360,13 +360,18 @@ static __device__ __forceinline__ void stream_loop(const CsumArgs &a, u32x4 *sta
 #define STREAM_ATTR
 #endif
 
+/* frame-group geometry (G, 1, 2) of the sparse fallback (A/B knob) */
+#ifndef XCSUM_STREAM_SPARSE_G
+#define XCSUM_STREAM_SPARSE_G 4
+#endif
+
 template <int KC>
 __global__ void __launch_bounds__(256) STREAM_ATTR csum_stream_kernel(CsumArgs a)
 {
 	extern __shared__ u32x4 stream_stage[];   /* [4 waves][KC * 64] chunks */
 	if (!dense_batch(a)) {
 		/* sparse batch: the frame-group kernel, region order as usual */
-		csum_body<4, 1, 2, 2>(a);
+		csum_body<XCSUM_STREAM_SPARSE_G, 1, 2, 2>(a);
 		return;
 	}
 	stream_loop<KC>(a, stream_stage + (threadIdx.x >> 6) * (KC * 64));

@@ -28,10 +28,12 @@
  * PCIe); IPv4 (udp->check 0 as packet.c:125), IPv4 with the opt-in RFC UDP
  * checksum, IPv6 (udp_csum6); and the batch-host hook with in-place writes.
  *
- * usage: umem_ring [--bench]     exit 0 ok, 1 failure, 77 no GPU
- *   --bench: 1M MTU frames per variant in batches of 4096, payloads written
- *   on a frame's first use only, every 64th frame checked by the NIC thread
- *   (all are checked for order): the producer loop's own rate
+ * usage: umem_ring [--bench [B1,B2,...]]     exit 0 ok, 1 failure, 77 no GPU
+ *   --bench: MTU frames per variant in batches of B (default 4096; 1M frames
+ *   for B >= 1024, fewer for smaller batches), payloads written on a frame's
+ *   first use only, every 64th frame checked by the NIC thread (all are
+ *   checked for order): the producer loop's own rate.  Small B shows the
+ *   fixed cost of one call (libxudp's tx_batch_num is 100, xudp.c:74).
  */
 #define _GNU_SOURCE
 #include <arpa/inet.h>
@@ -301,6 +303,16 @@ static int run_variant(xcsum_ctx *ctx, struct run *r, uint32_t batch, double *se
 int main(int argc, char **argv)
 {
 	const int bench = argc > 1 && strcmp(argv[1], "--bench") == 0;
+	uint32_t batches[16] = {4096u};
+	int nbatch = 1;
+	if (bench && argc > 2) {
+		nbatch = 0;
+		for (char *t = strtok(argv[2], ","); t && nbatch < 16; t = strtok(NULL, ","))
+			if (atoi(t) > 0)
+				batches[nbatch++] = (uint32_t)atoi(t);
+		if (!nbatch)
+			batches[nbatch++] = 4096u;
+	}
 	xcsum_ctx *ctx = NULL;
 	int rc = xcsum_ctx_create(-1, &ctx);
 	if (rc == -XCSUM_ERR_NODEV) {
@@ -339,7 +351,9 @@ int main(int argc, char **argv)
 		const struct variant *v = &vars[k];
 		if (v->registered)
 			CHECK(xcsum_register_umem(ctx, umem, bytes) == 0, "%s: register", v->name);
-		for (int pass = bench; pass < (bench ? 2 : 1); pass++) {
+		for (int pass = bench; pass < (bench ? 1 + nbatch : 1); pass++) {
+			/* tx_batch_num is 100 (xudp.c:74); the bench batches as asked */
+			const uint32_t batch = pass ? batches[pass - 1] : 100u;
 			memset(r, 0, sizeof(*r));
 			r->v = v;
 			r->umem = umem;
@@ -347,12 +361,11 @@ int main(int argc, char **argv)
 			/* correctness: ragged sizes; bench: MTU payloads */
 			r->pmin = pass ? 1472u - (v->family == 6 ? 20u : 0u) : 0u;
 			r->pmax = pass ? r->pmin : 1438u;
-			r->total = pass ? 1048576u : 40000u;
+			r->total = !pass ? 40000u : batch >= 1024u ? 1048576u
+				 : batch >= 64u ? 262144u : 16384u * batch;
 			r->verify_every = pass ? 64u : 1u;
 			r->fill_once = pass;
 			double secs = 0, csecs = 0;
-			/* tx_batch_num is 100 (xudp.c:74); the bench batches 4096 */
-			const uint32_t batch = pass ? 4096u : 100u;
 			int e = run_variant(ctx, r, batch, &secs, &csecs);
 			CHECK(e == 0, "%s: run failed", v->name);
 			CHECK(r->seen == r->total, "%s: NIC saw %llu of %llu frames", v->name,
@@ -366,10 +379,10 @@ int main(int argc, char **argv)
 				printf("{\"variant\": \"%s\", \"frames\": %llu, \"batch\": %u, "
 				       "\"frame_bytes\": %.0f, \"wall_s\": %.4f, \"mpps\": %.3f, "
 				       "\"frames_GBps\": %.3f, \"checksum_call_s\": %.4f, "
-				       "\"checksum_call_GBps\": %.3f}\n",
+				       "\"checksum_call_GBps\": %.3f, \"us_per_call\": %.2f}\n",
 				       v->name, (unsigned long long)r->total, batch, fb, secs,
 				       r->total / secs / 1e6, r->total * fb / secs / 1e9, csecs,
-				       r->total * fb / csecs / 1e9);
+				       r->total * fb / csecs / 1e9, csecs * 1e6 * batch / r->total);
 		}
 		if (v->registered)
 			CHECK(xcsum_unregister_umem(ctx, umem) == 0, "%s: unregister", v->name);
