@@ -461,6 +461,12 @@ static hipError_t wait_slot(hipEvent_t e)
 	return hipEventSynchronize(e);
 }
 
+/* The pinned stage, its descriptors and the result slots are read and
+ * written by kernels directly on the copy-free path: allocate them coherent
+ * (uncached on the GPU side), so that a slot reused by the next call never
+ * serves lines a previous kernel cached, whatever HIP_HOST_COHERENT says. */
+#define PINNED_FLAGS hipHostMallocCoherent
+
 static int ensure_staging(xcsum_ctx *c)
 {
 	if (c->frame_cap)
@@ -473,7 +479,7 @@ static int ensure_staging(xcsum_ctx *c)
 		    hipMalloc(&c->d_frames[s], frame_cap + 64) != hipSuccess ||
 		    hipMalloc(&c->d_desc[s], desc_cap * sizeof(struct xcsum_desc)) != hipSuccess ||
 		    hipMalloc(&c->d_out[s], 2 * desc_cap * sizeof(uint16_t)) != hipSuccess ||
-		    hipHostMalloc(&c->h_out[s], 2 * desc_cap * sizeof(uint16_t), 0) != hipSuccess) {
+		    hipHostMalloc(&c->h_out[s], 2 * desc_cap * sizeof(uint16_t), PINNED_FLAGS) != hipSuccess) {
 			free_staging(c);
 			return -XCSUM_ERR_NOMEM;
 		}
@@ -568,10 +574,10 @@ int batch_host_impl(xcsum_ctx *c, uint8_t *h_umem, const struct xcsum_desc *h_de
 		gather = false;
 	if (gather) {
 		for (int s = 0; s < Ctx::NSLOT; s++) {
-			if (!c->h_stage[s] && hipHostMalloc(&c->h_stage[s], c->frame_cap, 0) != hipSuccess)
+			if (!c->h_stage[s] && hipHostMalloc(&c->h_stage[s], c->frame_cap, PINNED_FLAGS) != hipSuccess)
 				return -XCSUM_ERR_NOMEM;
 			if (!c->h_dstage[s] &&
-			    hipHostMalloc(&c->h_dstage[s], c->desc_cap * sizeof(struct xcsum_desc), 0) !=
+			    hipHostMalloc(&c->h_dstage[s], c->desc_cap * sizeof(struct xcsum_desc), PINNED_FLAGS) !=
 				    hipSuccess)
 				return -XCSUM_ERR_NOMEM;
 			if (XCSUM_DIRECT_MAX && !c->v_stage[s] &&
