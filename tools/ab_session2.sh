@@ -1,0 +1,104 @@
+#!/bin/bash
+# The GPU calls of round 2's second session, one step per call:
+#   gpurun -- bash tools/ab_session2.sh <step>        (logs in gpurun_out/<step>/)
+# Results are indexed in profiles/README.md ("Round 2, second session").
+# Steps that compare builds need the variant libraries first, e.g.
+#   make -C libxudp_amd variant NAME=ntrec DEFS=-DXCSUM_RX_NTREC=1
+# (the knobs each step compared are named in profiles/README.md).
+set -e
+export TMPDIR=/tmp
+case "$1" in
+s3)
+
+  tools/gpu_run.sh s3/pytest_gpu 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread
+  tools/gpu_run.sh s3/smoke 200 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')"
+  tools/gpu_run.sh s3/bench 300 python bench.py --gpus 1 --steps 20 --warmup 5
+  tools/gpu_run.sh s3/slot_small 200 python tools/slot_probe.py --small
+  for c in 4 5; do
+    tools/gpu_run.sh s3/fetch$c 200 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/s3/fetch$c -o run -- python3 bench.py --config $c --steps 10 --warmup 2 --no-cpu-baseline --no-graph --ramp-ms 0 --reps 1 --no-ceiling
+    tools/gpu_run.sh s3/write$c 200 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/s3/write$c -o run -- python3 bench.py --config $c --steps 10 --warmup 2 --no-cpu-baseline --no-graph --ramp-ms 0 --reps 1 --no-ceiling
+  done
+  tools/gpu_run.sh s3/sweep5_bpc 300 python tools/sweep.py --config 5 --geoms "64,1,9" --bpc 1,2,3,4 --orders=-1,0 --rounds 3 --launches 10
+  ;;
+s4)
+  # round-2 session-2 A/B call: config 5 first-row temporal loads / all temporal,
+  # receive kernel capped at 3 waves/SIMD, config 3 in xudp's slot layout sweep
+  mkdir -p gpurun_out/s4
+  for r in 1 2; do
+    for v in cur edget nt0; do
+      L=libxudp_amd/libxcsum.so; [ $v = cur ] || L=libxudp_amd/variants/$v/libxcsum.so
+      XCSUM_LIB=$L tools/gpu_run.sh s4/c5_${v}_$r 200 python bench.py --config 5 --steps 10 --warmup 2 --reps 3 --no-cpu-baseline --no-ceiling
+    done
+  done
+  for v in edget nt0; do
+    XCSUM_LIB=libxudp_amd/variants/$v/libxcsum.so tools/gpu_run.sh s4/fetch5_$v 200 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/s4/fetch5_$v -o run -- python3 bench.py --config 5 --steps 10 --warmup 2 --no-cpu-baseline --no-graph --ramp-ms 0 --reps 1 --no-ceiling
+  done
+  ROUNDS=2 tools/ab_rx_libs.sh gpurun_out/s4/rx 2,4 auto rxw3
+  tools/gpu_run.sh s4/sweep3_umem 300 python tools/sweep.py --config 3 --layout umem --geoms "4,1,2;8,1,2;4,2,2;2,1,4" --bpc 0,2,4,8 --orders="-1,0;0,0;3,4;7,4" --rounds 3 --launches 20
+  ;;
+s5)
+  # A/B: sparse fallback of the stream kernel at G = 8 (config 3 in xudp's
+  # slots), nontemporal receive-record stores
+  mkdir -p gpurun_out/s5
+  for r in 1 2; do
+    for v in cur sg8; do
+      L=libxudp_amd/libxcsum.so; [ $v = cur ] || L=libxudp_amd/variants/$v/libxcsum.so
+      XCSUM_LIB=$L tools/gpu_run.sh s5/c3u_${v}_$r 200 python bench.py --config 3 --layout umem --steps 100 --warmup 5 --reps 3 --no-cpu-baseline --no-ceiling
+      XCSUM_LIB=$L tools/gpu_run.sh s5/c3p_${v}_$r 200 python bench.py --config 3 --steps 100 --warmup 5 --reps 3 --no-cpu-baseline --no-ceiling
+    done
+  done
+  ROUNDS=2 tools/ab_rx_libs.sh gpurun_out/s5/rx 2,4,5 auto ntrec
+  ;;
+s6)
+  # full GPU suite on nontemporal receive records; A/B nontemporal result /
+  # in-place stores in the checksum kernels (flags none / INPLACE / INPLACE+IPHDR)
+  mkdir -p gpurun_out/s6
+  tools/gpu_run.sh s6/pytest_gpu 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread
+  tools/gpu_run.sh s6/bench_rx 300 python tools/bench_rx.py --configs 2,4,3,5
+  for r in 1 2; do
+    for v in cur ntst; do
+      L=libxudp_amd/libxcsum.so; [ $v = cur ] || L=libxudp_amd/variants/$v/libxcsum.so
+      for fl in none inplace inplace,iphdr verify; do
+        XCSUM_LIB=$L tools/gpu_run.sh s6/c2_${v}_${fl/,/_}_$r 200 python tools/sweep.py --config 2 --geoms 16,2,6 --bpc 0 --orders=-1,0 --flags $fl --rounds 3 --launches 20
+      done
+      XCSUM_LIB=$L tools/gpu_run.sh s6/c2u_${v}_inplace_iphdr_$r 200 python tools/sweep.py --config 2 --layout umem --geoms 16,2,6 --bpc 0 --orders=-1,0 --flags inplace,iphdr --rounds 3 --launches 20
+      XCSUM_LIB=$L tools/gpu_run.sh s6/c3_${v}_$r 200 python tools/sweep.py --config 3 --geoms 64,0,8 --bpc 0 --orders=-1,0 --rounds 3 --launches 40
+      XCSUM_LIB=$L tools/gpu_run.sh s6/c5_${v}_$r 200 python tools/sweep.py --config 5 --geoms 64,1,9 --bpc 0 --orders=-1,0 --rounds 2 --launches 10
+    done
+  done
+  ;;
+s7)
+  # copy-free small-batch host path (XCSUM_DIRECT_MAX) vs current: correctness
+  # (TX ring harness, host-path GPU tests) and per-call cost by batch size
+  mkdir -p gpurun_out/s7
+  V=libxudp_amd/variants/direct
+  LD_LIBRARY_PATH=$V tools/gpu_run.sh s7/ring_direct_check 200 tests/c/umem_ring
+  XCSUM_LIB=$V/libxcsum.so tools/gpu_run.sh s7/pytest_host_direct 300 python -u -m pytest tests/test_gpu_host_path.py tests/test_gpu_config1.py tests/test_gpu_fuzz.py -m gpu -x -q --timeout 120 --timeout-method thread
+  for r in 1 2; do
+    tools/gpu_run.sh s7/ring_cur_$r 300 tests/c/umem_ring --bench 1,16,100,1024,4096
+    LD_LIBRARY_PATH=$V tools/gpu_run.sh s7/ring_direct_$r 300 tests/c/umem_ring --bench 1,16,100,1024,4096
+  done
+  ;;
+s8)
+  # host path per-call cost: copy-free small batches, and spin-wait on the slot event
+  mkdir -p gpurun_out/s8
+  for r in 1 2 3; do
+    for v in cur direct dspin; do
+      L=; [ $v = cur ] || L=libxudp_amd/variants/$v
+      LD_LIBRARY_PATH=$L tools/gpu_run.sh s8/ring_${v}_$r 300 tests/c/umem_ring --bench 1,16,100,1024
+    done
+  done
+  ;;
+s10)
+  # full GPU suite + TX ring harness + end-to-end bench on the final host path
+  mkdir -p gpurun_out/s10
+  tools/gpu_run.sh s10/pytest_gpu 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread
+  tools/gpu_run.sh s10/ring_check 200 tests/c/umem_ring
+  tools/gpu_run.sh s10/ring_bench 300 tests/c/umem_ring --bench 1,16,100,1024,4096
+  tools/gpu_run.sh s10/e2e 300 python tools/bench_e2e.py
+  ;;
+*)
+  echo "usage: $0 s3|s4|s5|s6|s7|s8|s10" >&2
+  exit 2
+  ;;
+esac

@@ -24,3 +24,7 @@ for c in 2 3; do
   tools/gpu_run.sh $out/write$c 300 rocprofv3 --pmc WRITE_SIZE --output-format csv \
       -d gpurun_out/$out/write$c -o run -- python3 bench.py --config $c --steps 10 --warmup 2 --no-cpu-baseline --no-graph --ramp-ms 0 --reps 1 --no-ceiling
 done
+# receive kernels: every mode on configs 2, 4, 3, 5, and rocprofv3 stats of config 2
+tools/gpu_run.sh $out/bench_rx 300 python tools/bench_rx.py --configs 2,4,3,5
+tools/gpu_run.sh $out/rx_stats2 300 rocprofv3 --kernel-trace --stats --output-format csv \
+    -d gpurun_out/$out/rx_stats2 -o run -- python3 tools/bench_rx.py --configs 2 --reps 5
