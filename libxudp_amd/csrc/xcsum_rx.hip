@@ -565,18 +565,24 @@ static __device__ __forceinline__ void rx_frame(const RxArgs &a, uint32_t *st, c
  * needs the in-flight loads to have landed and would drain the pipeline
  * every iteration (vmcnt(0) at the loop latch, seen in the ISA).
  */
+/* per-frame header stage of the group kernel: STAGE_CHUNKS chunks + one
+ * dword of slack per G-lane group */
+template <int G>
+struct GroupStage {
+	static constexpr uint32_t SW = STAGE_CHUNKS * 4 + 4;   /* dwords per group */
+	static constexpr uint32_t DWORDS = (256 / G) * SW;
+};
+
+/* stage: GroupStage<G>::DWORDS of LDS, 16-byte aligned; span: the mask
+ * table, initialised (span_init + block barrier) by the caller */
 template <int G, int K, int U>
-__global__ void __launch_bounds__(256) rx_kernel(RxArgs a)
+static __device__ __forceinline__ void rx_group_body(RxArgs a, uint32_t *stage,
+						     const uint32_t *span)
 {
-	/* per-frame header stage: STAGE_CHUNKS chunks + one dword of slack */
-	constexpr uint32_t SW = STAGE_CHUNKS * 4 + 4;   /* dwords per group */
-	__shared__ __attribute__((aligned(16))) uint32_t stage[(256 / G) * SW];
+	constexpr uint32_t SW = GroupStage<G>::SW;
 	const uint32_t lane = threadIdx.x & (G - 1);
 	const uint32_t grp = threadIdx.x / G;
 	uint32_t *st = stage + grp * SW;
-	__shared__ __attribute__((aligned(16))) uint32_t span[SPAN_DWORDS];
-	span_init(span);
-	__syncthreads();
 	uint32_t seg = (blockIdx.x * 256u + threadIdx.x) / G;
 	const uint32_t nseg = gridDim.x * (256u / G);
 	if (G == 64)
@@ -658,6 +664,16 @@ __global__ void __launch_bounds__(256) rx_kernel(RxArgs a)
 	}
 }
 
+template <int G, int K, int U>
+__global__ void __launch_bounds__(256) rx_kernel(RxArgs a)
+{
+	__shared__ __attribute__((aligned(16))) uint32_t stage[GroupStage<G>::DWORDS];
+	__shared__ __attribute__((aligned(16))) uint32_t span[SPAN_DWORDS];
+	span_init(span);
+	__syncthreads();
+	rx_group_body<G, K, U>(a, stage, span);
+}
+
 /* ---- lane-per-frame parse (geometry U = 0) ---------------------------------
  * rx_kernel pays the header work (parse, masks, record) once per G-lane group,
  * i.e. once per 64/G frames per wave instruction.  Here a wave takes 64
@@ -690,10 +706,12 @@ constexpr uint32_t WSTAGE = 4 * STAGE_CHUNKS + 4;
  * LDS stages. */
 constexpr int WHDR = 8;
 
+static __device__ __forceinline__ WParse rx_parse_hdr(const RFrame &f, const uint32_t (&hdr)[13],
+						      bool verify);
+
 static __device__ __forceinline__ WParse rx_parse_lane(const RFrame &f, const u32x4 (&hv)[WHDR],
 						       uint32_t *hstage, uint32_t wl, bool verify)
 {
-	const uint32_t len = rx_len(f);
 	const uint32_t nc = rx_nchunks(f);
 	const uint32_t fh = rx_h(f, nc);
 	uint32_t *wst = hstage + (wl & ~63u) * WSTAGE;        /* the wave's stages */
@@ -720,12 +738,21 @@ static __device__ __forceinline__ WParse rx_parse_lane(const RFrame &f, const u3
 #pragma unroll
 	for (int i = 0; i < 13; i++)
 		hdr[i] = __builtin_amdgcn_alignbyte(d[i + 1], d[i], fh & 3u);
+	return rx_parse_hdr(f, hdr, verify);
+}
+
+/* packet_parse(), as rx_frame, from hdr[i] = frame bytes [12 + 4i, 16 + 4i)
+ * (bytes past the frame's length may be anything: every field read from
+ * them is behind a length test) */
+static __device__ __forceinline__ WParse rx_parse_hdr(const RFrame &f, const uint32_t (&hdr)[13],
+						      bool verify)
+{
+	const uint32_t len = rx_len(f);
 	auto f0 = [&](int x) { return hdr[(x - 12) >> 2]; };
 	auto f2 = [&](int x) {
 		const int i = (x - 12) >> 2;
 		return __builtin_amdgcn_alignbyte(hdr[i + 1], hdr[i], 2u);
 	};
-	/* packet_parse(), as rx_frame */
 	const uint32_t w12 = f0(12), w20 = f0(20), w26 = f2(26), w30 = f2(30);
 	const uint32_t p0 = w12 & 0xffu, p1 = (w12 >> 8) & 0xffu;
 	const uint32_t ihl = (w12 >> 16) & 0xfu;
@@ -832,8 +859,11 @@ static __device__ __forceinline__ uint32_t rx_step_sum(const uint32_t *tab, cons
 #define RX_WIDE_ATTR
 #endif
 
+/* hstage: 256 * WSTAGE dwords of LDS, 16-byte aligned; span: the mask table,
+ * initialised (span_init + block barrier) by the caller */
 template <int G, int K>
-__global__ void __launch_bounds__(256) RX_WIDE_ATTR rx_wide_kernel(RxArgs a)
+static __device__ __forceinline__ void rx_wide_body(RxArgs a, uint32_t *hstage,
+						    const uint32_t *span)
 {
 	constexpr uint32_t FPS = 64 / G;        /* frames per step */
 	constexpr uint32_t STEPS = G;           /* 64 frames per batch */
@@ -841,10 +871,6 @@ __global__ void __launch_bounds__(256) RX_WIDE_ATTR rx_wide_kernel(RxArgs a)
 #define XCSUM_RX_WIDE_HDR_LEAD 4   /* 4 steps: config 2 -2.3%, config 5 -3.1% vs 0 (rx_wide/rxlead) */
 #endif
 	constexpr uint32_t HDR_LEAD = XCSUM_RX_WIDE_HDR_LEAD;   /* even */
-	__shared__ __attribute__((aligned(16))) uint32_t span[SPAN_DWORDS];
-	__shared__ __attribute__((aligned(16))) uint32_t hstage[256 * WSTAGE];
-	span_init(span);
-	__syncthreads();
 	const uint32_t wl = threadIdx.x & 63u;  /* lane = frame of the batch */
 	const uint32_t lane = wl & (G - 1);     /* lane in the step's group */
 	const uint32_t grp = wl / G;
@@ -1033,6 +1059,245 @@ __global__ void __launch_bounds__(256) RX_WIDE_ATTR rx_wide_kernel(RxArgs a)
 	}
 }
 
+template <int G, int K>
+__global__ void __launch_bounds__(256) RX_WIDE_ATTR rx_wide_kernel(RxArgs a)
+{
+	__shared__ __attribute__((aligned(16))) uint32_t span[SPAN_DWORDS];
+	__shared__ __attribute__((aligned(16))) uint32_t hstage[256 * WSTAGE];
+	span_init(span);
+	__syncthreads();
+	rx_wide_body<G, K>(a, hstage, span);
+}
+
+/* ---- stream receive kernel (geometry U = 3): packed small frames ---------
+ * The receive side of csum_stream_kernel.  A wave takes 64 consecutive
+ * descriptors (lane = frame) and reads the region the 64 frames occupy --
+ * [first frame, last frame's end) -- as KC coalesced 1 KiB loads into its LDS
+ * stage, with no per-frame chunk grid.  Every lane then parses its frame
+ * (rx_parse_hdr), sums its span for VERIFY and builds its record from that
+ * copy; the 64 records go out through the same stage, 1 KiB per nontemporal
+ * store instruction.  The next region's loads (and the descriptors after
+ * it) are in flight while one region is processed.
+ * A wave whose frames do not fit the stage (a long frame, descriptors out of
+ * UMEM order) takes every frame through rx_slow, the general path; a sparse
+ * batch (one frame per UMEM chunk, as an RX ring delivers them) runs the
+ * group kernel (4,2,1) in region order, decided once per launch. */
+constexpr uint32_t RXS_SLACK = 8;   /* chunks past the region: a short last
+				       frame's header reads stay in the stage */
+
+template <int KC>
+__global__ void __launch_bounds__(256) rx_stream_kernel(RxArgs a)
+{
+	constexpr uint32_t SC = KC * 64 + RXS_SLACK;   /* stage chunks per wave */
+	static_assert(KC >= 4, "the 64 records (4 KiB) go out through the stage");
+	static_assert(4 * SC * 4 >= GroupStage<4>::DWORDS && 4 * SC * 4 >= 256 * WSTAGE,
+		      "the fallbacks' stages fit");
+	__shared__ __attribute__((aligned(16))) u32x4 rstage[4 * SC];
+	__shared__ __attribute__((aligned(16))) uint32_t span[SPAN_DWORDS];
+	span_init(span);
+	__syncthreads();
+	rx_resolve_order(a);
+	if (a.ord.rshift != 0) {
+		/* sparse batch, in region order (rx_resolve_order): what the
+		 * small-frame defaults were before this kernel -- frame groups
+		 * (4,2,1) with VERIFY, the lane-per-frame parse (4,2,0) without */
+		if (a.flags & XCSUM_F_VERIFY)
+			rx_group_body<4, 2, 1>(a, (uint32_t *)rstage, span);
+		else
+			rx_wide_body<4, 2>(a, (uint32_t *)rstage, span);
+		return;
+	}
+	const uint32_t lane = threadIdx.x & 63u;
+	u32x4 *stage = rstage + (threadIdx.x >> 6) * SC;
+	const uint8_t *st8 = (const uint8_t *)stage;
+	const uint32_t nw = gridDim.x * 4u;
+	const bool verify = (a.flags & XCSUM_F_VERIFY) != 0;
+	const bool iphdr = (a.flags & XCSUM_F_IPHDR) != 0;
+	const uint8_t *zero = (const uint8_t *)g_rx_zero;
+	uint32_t delivered = 0;
+	uint32_t w = __builtin_amdgcn_readfirstlane(blockIdx.x * 4u + (threadIdx.x >> 6));
+
+	auto frame_at = [&](uint32_t wi, u32x3 d) {
+		return rx_resolve(a, d, 64ull * wi + lane < a.n);
+	};
+	auto desc_at = [&](uint32_t wi) {
+		const uint64_t p = 64ull * wi + lane;
+		return rx_desc(a, p < a.n ? (uint32_t)p : a.n - 1u);
+	};
+	/* the region: the first lane's frame start to the last present lane's
+	 * end (two readlanes); every present frame must lie inside it (one
+	 * ballot) and it must fit the stage, else nch = ~0u (walk) */
+	auto region = [&](uint32_t wi, const RFrame &f, uintptr_t &base, uint32_t &nch) {
+		const uint64_t rem = a.n - 64ull * wi;
+		const uint32_t last = rem > 64 ? 63u : (uint32_t)rem - 1u;
+		const uint64_t e = (uint64_t)(uintptr_t)f.eth;
+		const uint64_t end = e + rx_len(f);
+		const uint64_t lo =
+			((uint64_t)__builtin_amdgcn_readlane((uint32_t)(e >> 32), 0) << 32) |
+			(uint32_t)__builtin_amdgcn_readlane((uint32_t)e, 0);
+		const uint64_t hi =
+			((uint64_t)__builtin_amdgcn_readlane((uint32_t)(end >> 32), last) << 32) |
+			(uint32_t)__builtin_amdgcn_readlane((uint32_t)end, last);
+		base = (uintptr_t)(lo & ~15ull);
+		const bool out = rx_present(f) && (e < lo || end > hi);
+		nch = (__builtin_amdgcn_ballot_w64(out) || hi < lo ||
+		       hi - base > (uint64_t)KC * 1024u) ? ~0u : (uint32_t)((hi - base + 15) >> 4);
+	};
+	auto issue_region = [&](uintptr_t base, uint32_t nch, u32x4 (&v)[KC]) {
+#pragma unroll
+		for (int k = 0; k < KC; k++) {
+			const uint32_t c = (uint32_t)k * 64u + lane;
+			v[k] = __builtin_nontemporal_load(
+				(gu32x4 *)(nch != ~0u && c < nch ? (const uint8_t *)base + 16u * c : zero));
+		}
+	};
+	auto wave_sync = [] {
+		__builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+		__builtin_amdgcn_wave_barrier();
+		__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+	};
+
+	RFrame fc = frame_at(w, desc_at(w));
+	uintptr_t bc = 0;
+	uint32_t nc = ~0u;
+	u32x4 v[KC];
+	if (64ull * w < a.n) {
+		region(w, fc, bc, nc);
+		issue_region(bc, nc, v);
+	}
+	u32x3 dn = desc_at(w + nw);
+	for (; 64ull * w < a.n; w += nw) {
+		/* this region -> LDS (waits for its loads only) */
+#pragma unroll
+		for (int k = 0; k < KC; k++)
+			stage[k * 64 + lane] = v[k];
+		const RFrame cur = fc;
+		const uintptr_t cbase = bc;
+		const uint32_t cnch = nc;
+		/* the next region's loads go out before this one is processed */
+		if (64ull * (w + nw) < a.n) {
+			fc = frame_at(w + nw, dn);
+			region(w + nw, fc, bc, nc);
+			__builtin_amdgcn_sched_barrier(0);
+			issue_region(bc, nc, v);
+			dn = desc_at(w + 2 * nw);
+		}
+		__builtin_amdgcn_sched_barrier(0);
+		wave_sync();
+
+		/* parse from the stage (lane = frame) */
+		const uint32_t oe = (uint32_t)((uintptr_t)cur.eth - cbase);  /* frame in the stage */
+		WParse P;
+		if (cnch != ~0u) {
+			const uint32_t o = oe + 12u;
+			const uint32_t *dw = (const uint32_t *)(st8 + (o & ~3u));
+			uint32_t d[14], hdr[13];
+#pragma unroll
+			for (int i = 0; i < 14; i++)
+				d[i] = dw[i];
+#pragma unroll
+			for (int i = 0; i < 13; i++)
+				hdr[i] = __builtin_amdgcn_alignbyte(d[i + 1], d[i], o & 3u);
+			P = rx_parse_hdr(cur, hdr, verify);
+		} else {
+			/* does not fit the stage: every frame the general way */
+			P.r = Rec{XCSUM_RX_PARSE, 0u, 0u, 0u, 0u};
+			P.saddr = P.daddr = u32x4{0u, 0u, 0u, 0u};
+			P.wck = P.hsum = 0u;
+			P.hi = 0;
+			P.v4 = false;
+			P.want = P.good = false;
+			P.slow = rx_present(cur);
+		}
+
+		/* verify: the span [addresses, udp + ulen) summed from the stage */
+		if (__builtin_amdgcn_ballot_w64(P.want)) {
+			bool good = P.good;
+			if (good) {
+				const uint32_t lo = oe + (P.v4 ? 26u : 22u), hi = oe + (uint32_t)P.hi;
+				uint32_t E = 0, O = 0;
+				for (uint32_t c = lo >> 4; c < (hi + 15u) >> 4; c++) {
+					u32x4 x = stage[c];
+					const int cb = (int)(16u * c);
+					if (cb < (int)lo || cb + 16 > (int)hi)
+						x = keep_span(span, x, (int)lo - cb, (int)hi - cb);
+					accum(x, E, O);
+				}
+				/* the stage base is 16-byte aligned: oe has the frame's
+				 * address parity */
+				const uint32_t s = ((oe & 1u) ? (O << 8) + E : (E << 8) + O) + 17u + P.r.ulen;
+				good = (P.wck >> 16) == 0 ? P.r.family == 4 : fold16(s) == 0xffffu;
+			}
+			if (iphdr && P.r.family == 4)
+				good = good && fold16(P.hsum) == 0xffffu;
+			if (P.want && !good)
+				P.r.status = XCSUM_RX_CSUM;
+		}
+
+		/* the general case, one frame at a time by the whole wave */
+		uint64_t sm = __builtin_amdgcn_ballot_w64(P.slow);
+		while (sm) {
+			const uint32_t j = __builtin_ctzll(sm);
+			sm &= sm - 1;
+			const uint64_t e = (uint64_t)(uintptr_t)cur.eth;
+			const uint8_t *eth = (const uint8_t *)(uintptr_t)(
+				((uint64_t)__builtin_amdgcn_readlane((int)(e >> 32), (int)j) << 32) |
+				(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)e, (int)j));
+			const uint32_t len = (uint32_t)__builtin_amdgcn_readlane((int)rx_len(cur), (int)j);
+			const Rec rs = rx_slow<64>(eth, len, lane, true, verify, iphdr);
+			if (lane == j) {
+				P.r = rs;
+				auto ld4 = [&](uint32_t o) {
+					return (uint32_t)eth[o] | ((uint32_t)eth[o + 1] << 8) |
+					       ((uint32_t)eth[o + 2] << 16) | ((uint32_t)eth[o + 3] << 24);
+				};
+				if (rs.family == 4) {
+					P.saddr = u32x4{ld4(26), 0u, 0u, 0u};
+					P.daddr = u32x4{ld4(30), 0u, 0u, 0u};
+				} else if (rs.status != XCSUM_RX_PARSE) {
+					P.saddr = u32x4{ld4(22), ld4(26), ld4(30), ld4(34)};
+					P.daddr = u32x4{ld4(38), ld4(42), ld4(46), ld4(50)};
+				}
+			}
+		}
+
+		/* the records through the stage (every read of the region is done) */
+		const Rec &r = P.r;
+		const bool pok = r.status != XCSUM_RX_PARSE;
+		const uint64_t addr = (uint64_t)(cur.eth - a.umem);
+		const uint64_t body = pok ? addr + r.l4 + 8 : 0;
+		const u32x4 zero4 = {0u, 0u, 0u, 0u};
+		wave_sync();
+		u32x4 *rs = stage + 4u * lane;
+		rs[0] = u32x4{(uint32_t)addr, (uint32_t)(addr >> 32), (uint32_t)body,
+			      (uint32_t)(body >> 32)};
+		rs[1] = u32x4{pok ? r.ulen - 8u : 0u,
+			      r.status | (r.family << 8) | ((pok ? r.l4 : 0u) << 16), r.ports, 0u};
+		rs[2] = pok ? P.saddr : zero4;
+		rs[3] = pok ? P.daddr : zero4;
+		wave_sync();
+		u32x4 *m = (u32x4 *)(a.msgs + 64ull * w);
+#pragma unroll
+		for (uint32_t i = 0; i < 4; i++) {
+			const u32x4 x = stage[64u * i + lane];
+			if (64ull * w + 16u * i + (lane >> 2) < a.n)
+				store_rec(&m[64u * i + lane], x);
+		}
+		wave_sync();   /* the next region overwrites the stage */
+		if (rx_present(cur) && r.status == XCSUM_RX_OK)
+			delivered++;
+	}
+	if (a.count) {
+		__shared__ uint32_t wsum[4];
+		const uint32_t tot = seg_sum<64>(delivered);
+		if ((threadIdx.x & 63) == 0)
+			wsum[threadIdx.x >> 6] = tot;
+		__syncthreads();
+		if (threadIdx.x == 0)
+			a.part[blockIdx.x] = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+	}
+}
+
 __global__ void __launch_bounds__(256) rx_count_kernel(const uint32_t *part, uint32_t nblocks,
 						      uint32_t *count)
 {
@@ -1057,14 +1322,16 @@ static hipError_t launch_rx_t(const RxArgs &a, int cus, int bpc, hipStream_t s)
 		hipError_t e;
 		if constexpr (U == 0)
 			e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, rx_wide_kernel<G, K>, 256, 0);
+		else if constexpr (U == 3)
+			e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, rx_stream_kernel<K>, 256, 0);
 		else
 			e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, rx_kernel<G, K, U>, 256, 0);
 		if (e != hipSuccess || nb <= 0)
 			nb = 4;
 		return nb;
 	});
-	/* U == 0: lane-per-frame parse, a wave per 64 frames */
-	uint64_t blocks = U == 0 ? ((uint64_t)a.n + 255) / 256
+	/* U == 0 / 3: lane-per-frame parse / stream, a wave per 64 frames */
+	uint64_t blocks = (U == 0 || U == 3) ? ((uint64_t)a.n + 255) / 256
 				 : (((uint64_t)a.n + (U ? U : 1) - 1) / (U ? U : 1) * G + 255) / 256;
 	const uint64_t cap = (uint64_t)cus * ((bpc > 0 && bpc < occ) ? bpc : occ);
 	if (blocks > cap)
@@ -1077,6 +1344,8 @@ static hipError_t launch_rx_t(const RxArgs &a, int cus, int bpc, hipStream_t s)
 	                           * someone's hipEventQuery) before checking ours */
 	if constexpr (U == 0)
 		hipLaunchKernelGGL((rx_wide_kernel<G, K>), dim3((unsigned)blocks), dim3(256), 0, s, a);
+	else if constexpr (U == 3)
+		hipLaunchKernelGGL((rx_stream_kernel<K>), dim3((unsigned)blocks), dim3(256), 0, s, a);
 	else
 		hipLaunchKernelGGL((rx_kernel<G, K, U>), dim3((unsigned)blocks), dim3(256), 0, s, a);
 	if (a.count)
@@ -1088,7 +1357,8 @@ static hipError_t launch_rx_t(const RxArgs &a, int cus, int bpc, hipStream_t s)
 #define XCSUM_RX_GEOMETRIES(X) \
 	X(2, 4, 1) X(2, 4, 2) X(4, 2, 1) X(4, 2, 2) X(8, 1, 2) X(8, 2, 1) \
 	X(16, 2, 1) X(16, 3, 1) X(16, 6, 1) X(16, 6, 2) X(64, 9, 1) \
-	X(4, 2, 0) X(8, 2, 0) X(16, 3, 0) X(16, 6, 0) X(32, 3, 0) X(64, 2, 0) X(64, 9, 0)
+	X(4, 2, 0) X(8, 2, 0) X(16, 3, 0) X(16, 6, 0) X(32, 3, 0) X(64, 2, 0) X(64, 9, 0) \
+	X(64, 8, 3)
 
 hipError_t launch_rx(const RxArgs &a, uint32_t len_hint, int cus, hipStream_t s)
 {
@@ -1118,9 +1388,13 @@ hipError_t launch_rx(const RxArgs &a, uint32_t len_hint, int cus, hipStream_t s)
 			 * 0.039 ms, config 2 0.060 -> 0.057, config 3 0.040 ->
 			 * 0.0375 (rx_wide/rxwide6, reclds, rxsmall) */
 			if (chunks > 16) { G = 32; K = 3; U = 0; }
-			else { G = 4; K = 2; U = 0; }
+			else if (chunks > 8) { G = 4; K = 2; U = 0; }
+			else { G = 64; K = 8; U = 3; }   /* stream: config 3 0.0363 ->
+							    0.0341 ms (session2/rx_stream) */
 		}
-		else if (chunks <= 8) { G = 4; K = 2; }
+		else if (chunks <= 8) { G = 64; K = 8; U = 3; }   /* stream: config 3 VERIFY
+								     0.0415 -> 0.0352 ms, group
+								     (4,2,1) before */
 		else if (chunks <= 16) { G = 8; K = 2; }
 		else if (chunks <= 32) { G = 16; K = 2; }
 		else if (chunks <= 48) { G = 16; K = 3; }

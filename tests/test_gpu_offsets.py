@@ -50,7 +50,7 @@ def test_checksum_across_2g_and_4g(torch_cuda, engine, big, geom, sizes):
         engine.set_geometry(0)
 
 
-@pytest.mark.parametrize("geometry", [None, "4,2,1", "32,3,0", "64,9,0"])
+@pytest.mark.parametrize("geometry", [None, "4,2,1", "32,3,0", "64,9,0", "64,8,3"])
 def test_receive_across_2g_and_4g(torch_cuda, engine, big, geometry, monkeypatch):
     umem, desc = X.gen_frames_host(700, 6, 0, 3000, seed=3)
     exp = oracle.rx_batch(umem, desc, X.F_VERIFY)

@@ -53,7 +53,7 @@ def run_rx(torch, eng, umem, desc, flags, len_hint=0, geometry=None):
 
 
 GEOMETRIES = ["2,4,1", "2,4,2", "4,2,1", "4,2,2", "8,1,2", "8,2,1", "16,2,1", "16,3,1", "16,6,1", "16,6,2", "64,9,1",
-              "4,2,0", "8,2,0", "16,3,0", "16,6,0", "32,3,0", "64,2,0", "64,9,0"]
+              "4,2,0", "8,2,0", "16,3,0", "16,6,0", "32,3,0", "64,2,0", "64,9,0", "64,8,3"]
 
 
 def test_rx_geometry_list_matches_kernel():
@@ -97,6 +97,30 @@ def test_rx_generated_vs_oracle(torch_cuda, engine, geometry):
             assert count == int((exp["status"] == X.RX_OK).sum())
 
 
+@pytest.mark.parametrize("geometry", [None, "64,8,3"])
+def test_rx_stream_small_frames_vs_oracle(torch_cuda, engine, geometry):
+    """Packed small frames, the stream receive kernel's fast path (one 8 KiB
+    region per 64 frames): every corpus frame of at most 128 bytes (padding,
+    options, ihl < 5, extension headers, stats requests, corrupted, truncated,
+    junk), under four seeds, at irregular offsets, and a batch size that ends
+    mid-wave."""
+    frames = []
+    for seed in (1, 2, 3, 4):
+        frames += [f for f, _ in rx_frames.corpus(seed=seed) if len(f) <= 128]
+    rng = np.random.default_rng(8)
+    frames = [frames[i] for i in rng.permutation(len(frames))] * 20
+    frames = frames[:len(frames) - 37]
+    umem, offs, lens = rx_frames.layout(frames, rng)
+    desc = np.zeros(len(frames), dtype=X.DESC_DTYPE)
+    desc["addr"], desc["len"] = offs, lens
+    for flags in FLAGS.values():
+        exp = oracle.rx_batch(umem, desc, flags)
+        recs, count = run_rx(torch_cuda, engine, umem, desc, flags, 100, geometry)
+        bad = np.nonzero(recs.view(np.uint8).reshape(-1, 64) != exp.view(np.uint8).reshape(-1, 64))
+        assert len(bad[0]) == 0, (flags, sorted(set(bad[0].tolist()))[:10])
+        assert count == int((exp["status"] == X.RX_OK).sum())
+
+
 def umem_chunks(frames, rng, n):
     """n frames one per chunk (xudp's UMEM: frame i in chunk i at a fixed
     headroom plus a small jitter), the layout the region order is for"""
@@ -114,7 +138,7 @@ def umem_chunks(frames, rng, n):
 
 
 @pytest.mark.parametrize("order", ["auto", "0"])
-@pytest.mark.parametrize("geometry", [None, "4,2,1", "16,3,1", "4,2,0", "32,3,0", "64,9,0"])
+@pytest.mark.parametrize("geometry", [None, "4,2,1", "16,3,1", "4,2,0", "32,3,0", "64,9,0", "64,8,3"])
 def test_rx_sparse_umem_vs_oracle(torch_cuda, engine, geometry, order):
     """Frames one per UMEM chunk (sparse: the kernels visit them in region
     order, launch_rx) and a batch size that leaves the last tiles partly or

@@ -97,8 +97,23 @@ s10)
   tools/gpu_run.sh s10/ring_bench 300 tests/c/umem_ring --bench 1,16,100,1024,4096
   tools/gpu_run.sh s10/e2e 300 python tools/bench_e2e.py
   ;;
+s11)
+  # stream receive kernel (64,8,3) for packed small frames: receive tests, then
+  # every receive mode on config 3 against the group / wide kernels
+  tools/gpu_run.sh s11/pytest_rx 600 python -u -m pytest tests/test_gpu_rx.py tests/test_gpu_offsets.py -m gpu -x -q --timeout 120 --timeout-method thread
+  tools/gpu_run.sh s11/bench_rx3 300 python tools/bench_rx.py --configs 3 --geoms "auto;4,2,1;4,2,0;64,8,3"
+  tools/gpu_run.sh s11/bench_rx3_umem 300 python tools/bench_rx.py --configs 3 --layout umem --geoms "auto;64,8,3"
+  ;;
+s12)
+  # the stream receive kernel as the small-frame default (plain and VERIFY;
+  # sparse batches fall back to (4,2,0) / (4,2,1)): whole suite, every mode
+  tools/gpu_run.sh s12/pytest_gpu 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread
+  tools/gpu_run.sh s12/bench_rx 300 python tools/bench_rx.py --configs 2,4,3,5
+  tools/gpu_run.sh s12/bench_rx3_umem 300 python tools/bench_rx.py --configs 3 --layout umem --geoms "auto;4,2,0;4,2,1"
+  tools/gpu_run.sh s12/e2e 300 python tools/bench_e2e.py
+  ;;
 *)
-  echo "usage: $0 s3|s4|s5|s6|s7|s8|s10" >&2
+  echo "usage: $0 s3|s4|s5|s6|s7|s8|s10|s11|s12" >&2
   exit 2
   ;;
 esac
