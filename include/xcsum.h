@@ -222,9 +222,12 @@ int xcsum_rx_device(xcsum_ctx *ctx, const uint8_t *d_umem, const struct xcsum_de
 /* Same for received frames in the host UMEM (the AF_XDP RX ring's frames):
  * frames are staged to the device with chunked, double-buffered
  * hipMemcpyAsync, or with XCSUM_F_ZEROCOPY read in place over PCIe from a
- * registered UMEM; the 64-byte records come back into h_msgs.  *h_count (may
- * be NULL) = number of XCSUM_RX_OK records.  flags: XCSUM_F_VERIFY,
- * XCSUM_F_IPHDR, XCSUM_F_ZEROCOPY.  Synchronous. */
+ * registered UMEM; the 64-byte records come back into h_msgs.  A sparse
+ * batch in a pageable UMEM (one frame per UMEM chunk, as the RX ring hands
+ * them over) is gathered frame by frame instead of copying the range with
+ * its gaps.  Records hold UMEM offsets either way.  *h_count (may be NULL)
+ * = number of XCSUM_RX_OK records.  flags: XCSUM_F_VERIFY, XCSUM_F_IPHDR,
+ * XCSUM_F_ZEROCOPY.  Synchronous. */
 int xcsum_rx_host(xcsum_ctx *ctx, const uint8_t *h_umem, const struct xcsum_desc *h_desc,
 		  uint32_t n, struct xcsum_rx_msg *h_msgs, uint32_t *h_count, uint32_t flags);
 

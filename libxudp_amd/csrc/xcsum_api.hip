@@ -110,6 +110,7 @@ extern "C" int xcsum_ctx_create(int device, xcsum_ctx **out)
 		c->v_stage[s] = nullptr;
 		c->v_dstage[s] = nullptr;
 		c->v_out[s] = nullptr;
+		c->v_rx_msgs[s] = nullptr;
 	}
 	c->frame_cap = 0;
 	c->desc_cap = 0;
@@ -138,6 +139,7 @@ static void free_staging(xcsum_ctx *c)
 		c->v_stage[s] = nullptr;
 		c->v_dstage[s] = nullptr;
 		c->v_out[s] = nullptr;
+		c->v_rx_msgs[s] = nullptr;
 		c->d_rx_msgs[s] = nullptr;
 		c->h_rx_msgs[s] = nullptr;
 		c->streams[s] = nullptr;
@@ -443,6 +445,8 @@ static const Region *find_region(const xcsum_ctx *c, const uint8_t *lo, const ui
 #ifndef XCSUM_DIRECT_MAX
 #define XCSUM_DIRECT_MAX (256u << 10)
 #endif
+static constexpr uint64_t DIRECT_MAX = XCSUM_DIRECT_MAX;
+static constexpr bool DIRECT_ON = DIRECT_MAX != 0;
 
 /* XCSUM_SPIN_WAIT=1: wait for a slot by polling its event (A/B only;
  * measured no faster than hipEventSynchronize) */
@@ -489,6 +493,56 @@ static int ensure_staging(xcsum_ctx *c)
 	return 0;
 }
 
+/* Pinned stage for gathered frames and their descriptors, and the device
+ * addresses the copy-free path hands the kernel (stage, descriptors, result
+ * slot).  After ensure_staging. */
+static int ensure_gather(xcsum_ctx *c)
+{
+	for (int s = 0; s < Ctx::NSLOT; s++) {
+		if (!c->h_stage[s] && hipHostMalloc(&c->h_stage[s], c->frame_cap, PINNED_FLAGS) != hipSuccess)
+			return -XCSUM_ERR_NOMEM;
+		if (!c->h_dstage[s] &&
+		    hipHostMalloc(&c->h_dstage[s], c->desc_cap * sizeof(struct xcsum_desc), PINNED_FLAGS) !=
+			    hipSuccess)
+			return -XCSUM_ERR_NOMEM;
+		if (DIRECT_ON && !c->v_stage[s] &&
+		    (hipHostGetDevicePointer((void **)&c->v_stage[s], c->h_stage[s], 0) != hipSuccess ||
+		     hipHostGetDevicePointer((void **)&c->v_dstage[s], c->h_dstage[s], 0) != hipSuccess ||
+		     hipHostGetDevicePointer((void **)&c->v_out[s], c->h_out[s], 0) != hipSuccess)) {
+			c->v_stage[s] = nullptr;
+			return -XCSUM_ERR_HIP;
+		}
+	}
+	return 0;
+}
+
+/* Gather a host batch frame by frame (one host memcpy per frame into the
+ * pinned stage) instead of copying the UMEM range it spans, when the frames
+ * fill less than 1/8 of that range and the UMEM is pageable.  A registered
+ * UMEM keeps the range copy (pure DMA, no host memcpy).  Measured on xudp's
+ * 4096-byte chunks, pageable (tools/bench_e2e.py --layout umem,
+ * profiles/r02/session2/rx_gather/): 64-byte frames 23.3 -> 6.9 ms per
+ * 256K-frame receive batch; MTU frames 22.7 -> 33.6 ms (the single-thread
+ * memcpy of 1.5 KB frames loses to the runtime's pipelined pageable copy of
+ * the whole range), hence the 1/8.  XCSUM_RX_GATHER=0 builds the range copy
+ * everywhere (A/B only). */
+#ifndef XCSUM_RX_GATHER
+#define XCSUM_RX_GATHER 1
+#endif
+static bool gather_pays(const xcsum_ctx *c, const uint8_t *h_umem, uint64_t lo, uint64_t hi,
+			uint64_t frame_bytes)
+{
+	return XCSUM_RX_GATHER && hi - lo > 8 * frame_bytes + 4096 &&
+	       !find_region(c, h_umem + lo, h_umem + hi);
+}
+
+/* staged offset of a gathered frame: packed, each at its UMEM 16-byte phase
+ * (the kernel sees the same address parity and alignment) */
+static inline uint64_t stage_off(uint64_t pos, uint64_t addr)
+{
+	return ((pos + 15) & ~(uint64_t)15) + (addr & 15);
+}
+
 /* udp->check / iph->check offsets of a frame for the resolved family */
 static int host_family(const uint8_t *eth, uint32_t mode)
 {
@@ -503,6 +557,7 @@ static int host_family(const uint8_t *eth, uint32_t mode)
 struct Pending {
 	uint32_t first, count;
 	bool busy;
+	bool gathered;   /* receive: records hold staged offsets, to be fixed up */
 };
 
 /* results of one finished chunk -> caller arrays / host frames */
@@ -572,23 +627,8 @@ int batch_host_impl(xcsum_ctx *c, uint8_t *h_umem, const struct xcsum_desc *h_de
 
 	if (zc)
 		gather = false;
-	if (gather) {
-		for (int s = 0; s < Ctx::NSLOT; s++) {
-			if (!c->h_stage[s] && hipHostMalloc(&c->h_stage[s], c->frame_cap, PINNED_FLAGS) != hipSuccess)
-				return -XCSUM_ERR_NOMEM;
-			if (!c->h_dstage[s] &&
-			    hipHostMalloc(&c->h_dstage[s], c->desc_cap * sizeof(struct xcsum_desc), PINNED_FLAGS) !=
-				    hipSuccess)
-				return -XCSUM_ERR_NOMEM;
-			if (XCSUM_DIRECT_MAX && !c->v_stage[s] &&
-			    (hipHostGetDevicePointer((void **)&c->v_stage[s], c->h_stage[s], 0) != hipSuccess ||
-			     hipHostGetDevicePointer((void **)&c->v_dstage[s], c->h_dstage[s], 0) != hipSuccess ||
-			     hipHostGetDevicePointer((void **)&c->v_out[s], c->h_out[s], 0) != hipSuccess)) {
-				c->v_stage[s] = nullptr;
-				return -XCSUM_ERR_HIP;
-			}
-		}
-	}
+	if (gather && (rc = ensure_gather(c)))
+		return rc;
 
 	/* zero-copy + INPLACE: the kernel already wrote the host frames */
 	const uint32_t rflags = zc ? (flags & ~XCSUM_F_INPLACE) : flags;
@@ -598,11 +638,6 @@ int batch_host_impl(xcsum_ctx *c, uint8_t *h_umem, const struct xcsum_desc *h_de
 
 	uint32_t i = 0;
 	int slot = 0;
-	/* staged offset of a gathered frame: packed, each at its UMEM 16-byte
-	 * phase (the kernel sees the same address parity and alignment) */
-	auto stage_off = [](uint64_t pos, uint64_t addr) {
-		return ((pos + 15) & ~(uint64_t)15) + (addr & 15);
-	};
 	while (i < n) {
 		/* grow a chunk: <= desc_cap frames, UMEM range (or gathered bytes)
 		 * <= frame_cap */
@@ -662,7 +697,7 @@ int batch_host_impl(xcsum_ctx *c, uint8_t *h_umem, const struct xcsum_desc *h_de
 			}
 			a.bias = 0;
 			a.flags = flags & (XCSUM_F_IPHDR | XCSUM_F_V4_RFC | XCSUM_F_VERIFY);
-			if (XCSUM_DIRECT_MAX && pos <= XCSUM_DIRECT_MAX) {
+			if (DIRECT_ON && pos <= DIRECT_MAX) {
 				/* small batch: no copies -- the kernel reads the pinned
 				 * stage over PCIe and writes the pinned result slot; the
 				 * call's latency is one launch, not three transfers and
@@ -720,14 +755,36 @@ int batch_host_impl(xcsum_ctx *c, uint8_t *h_umem, const struct xcsum_desc *h_de
 extern "C" int xcsum_batch_host(xcsum_ctx *c, uint8_t *h_umem, const struct xcsum_desc *h_desc,
 				uint32_t n, uint16_t *h_out, uint32_t mode, uint32_t flags)
 {
-	return batch_host_impl(c, h_umem, h_desc, n, h_out, nullptr, mode, flags);
+	/* small frames spread over a pageable UMEM: gathered (gather_pays) */
+	bool gather = false;
+	if (c && h_umem && h_desc && n && !(flags & XCSUM_F_ZEROCOPY)) {
+		uint64_t lo = UINT64_MAX, hi = 0, sum = 0;
+		for (uint32_t i = 0; i < n; i++) {
+			if (h_desc[i].addr < lo) lo = h_desc[i].addr;
+			if (h_desc[i].addr + h_desc[i].len > hi) hi = h_desc[i].addr + h_desc[i].len;
+			sum += h_desc[i].len;
+		}
+		gather = gather_pays(c, h_umem, lo, hi, sum);
+	}
+	return batch_host_impl(c, h_umem, h_desc, n, h_out, nullptr, mode, flags, gather);
 }
 
 /* Receive batch on host-resident frames: the chunking of batch_host_impl
- * (<= desc_cap frames, <= frame_cap bytes of UMEM per chunk, two slots in
- * flight), the receive kernel per chunk, records back through pinned
- * staging.  Record addresses are UMEM offsets, as from xcsum_rx_device: the
- * staged copy's base is handed to the kernel biased by the chunk's offset. */
+ * (<= desc_cap frames, <= frame_cap bytes per chunk, two slots in flight),
+ * the receive kernel per chunk, records back through pinned staging.  Record
+ * addresses are UMEM offsets, as from xcsum_rx_device.
+ * Three ways to the frames:
+ *   - zero-copy (XCSUM_F_ZEROCOPY, registered UMEM): read in place;
+ *   - a dense batch: one copy of the UMEM range per chunk, the kernel's base
+ *     biased by the chunk's offset so addresses stay UMEM offsets;
+ *   - a sparse batch in a pageable UMEM (the frames cover less than half
+ *     the range they span, as an RX ring's frames do, one per 2-4 KB UMEM
+ *     chunk): gathered frame by frame into the pinned stage, so only frame
+ *     bytes are copied (a pageable range copy memcpy's the gaps too); up to
+ *     XCSUM_DIRECT_MAX staged bytes the kernel reads the stage and writes the
+ *     pinned records in place (no copies).  The kernel then sees staged
+ *     offsets: `frame` and `body` are moved back to UMEM offsets on the host
+ *     as the records are collected. */
 extern "C" int xcsum_rx_host(xcsum_ctx *c, const uint8_t *h_umem, const struct xcsum_desc *h_desc,
 			     uint32_t n, struct xcsum_rx_msg *h_msgs, uint32_t *h_count,
 			     uint32_t flags)
@@ -749,31 +806,49 @@ extern "C" int xcsum_rx_host(xcsum_ctx *c, const uint8_t *h_umem, const struct x
 		    hipMalloc(&c->d_rx_msgs[s], c->desc_cap * sizeof(struct xcsum_rx_msg)) != hipSuccess)
 			return -XCSUM_ERR_NOMEM;
 		if (!c->h_rx_msgs[s] &&
-		    hipHostMalloc(&c->h_rx_msgs[s], c->desc_cap * sizeof(struct xcsum_rx_msg), 0) !=
-			    hipSuccess)
+		    hipHostMalloc(&c->h_rx_msgs[s], c->desc_cap * sizeof(struct xcsum_rx_msg),
+				  PINNED_FLAGS) != hipSuccess)
 			return -XCSUM_ERR_NOMEM;
+		if (DIRECT_ON && !c->v_rx_msgs[s] &&
+		    hipHostGetDevicePointer((void **)&c->v_rx_msgs[s], c->h_rx_msgs[s], 0) != hipSuccess) {
+			c->v_rx_msgs[s] = nullptr;
+			return -XCSUM_ERR_HIP;
+		}
+	}
+	uint64_t blo = UINT64_MAX, bhi = 0, bsum = 0;
+	for (uint32_t i = 0; i < n; i++) {
+		if (h_desc[i].addr < blo) blo = h_desc[i].addr;
+		if (h_desc[i].addr + h_desc[i].len > bhi) bhi = h_desc[i].addr + h_desc[i].len;
+		bsum += h_desc[i].len;
 	}
 	const Region *zc = nullptr;
 	if (flags & XCSUM_F_ZEROCOPY) {
-		uint64_t lo = UINT64_MAX, hi = 0;
-		for (uint32_t i = 0; i < n; i++) {
-			if (h_desc[i].addr < lo) lo = h_desc[i].addr;
-			if (h_desc[i].addr + h_desc[i].len > hi) hi = h_desc[i].addr + h_desc[i].len;
-		}
-		zc = find_region(c, h_umem + lo, h_umem + hi);
+		zc = find_region(c, h_umem + blo, h_umem + bhi);
 		if (!zc || ((uintptr_t)zc->dev & 3u) != ((uintptr_t)zc->host & 3u))
 			return -XCSUM_ERR_NOT_REGISTERED;
 	}
+	const bool gather = !zc && gather_pays(c, h_umem, blo, bhi, bsum);
+	if (gather && (rc = ensure_gather(c)))
+		return rc;
 	Pending pend[Ctx::NSLOT];
 	for (int s = 0; s < Ctx::NSLOT; s++)
 		pend[s].busy = false;
 	uint32_t delivered = 0;
 	auto finish = [&](int s) -> int {
 		HIPCHK(wait_slot(c->done[s]));
-		memcpy(h_msgs + pend[s].first, c->h_rx_msgs[s],
-		       (size_t)pend[s].count * sizeof(struct xcsum_rx_msg));
-		for (uint32_t k = 0; k < pend[s].count; k++)
-			delivered += c->h_rx_msgs[s][k].status == XCSUM_RX_OK;
+		struct xcsum_rx_msg *m = h_msgs + pend[s].first;
+		memcpy(m, c->h_rx_msgs[s], (size_t)pend[s].count * sizeof(struct xcsum_rx_msg));
+		for (uint32_t k = 0; k < pend[s].count; k++) {
+			delivered += m[k].status == XCSUM_RX_OK;
+			if (pend[s].gathered) {
+				/* staged offset -> UMEM offset */
+				const uint64_t st = c->h_dstage[s][k].addr;
+				const uint64_t ua = h_desc[pend[s].first + k].addr;
+				m[k].frame = ua;
+				if (m[k].body)
+					m[k].body = m[k].body - st + ua;
+			}
+		}
 		pend[s].busy = false;
 		return 0;
 	};
@@ -781,10 +856,19 @@ extern "C" int xcsum_rx_host(xcsum_ctx *c, const uint8_t *h_umem, const struct x
 	int slot = 0;
 	while (i < n) {
 		uint64_t lo = h_desc[i].addr, hi = h_desc[i].addr + h_desc[i].len;
-		if (!zc && hi - lo > c->frame_cap)
-			return -XCSUM_ERR_INVAL;
 		uint32_t cnt = 1;
-		while (i + cnt < n && cnt < c->desc_cap) {
+		uint64_t gpos = stage_off(0, lo) + h_desc[i].len;   /* gathered bytes so far */
+		if (gather ? gpos > c->frame_cap : (!zc && hi - lo > c->frame_cap))
+			return -XCSUM_ERR_INVAL;
+		while (gather && i + cnt < n && cnt < c->desc_cap) {
+			const struct xcsum_desc &d = h_desc[i + cnt];
+			const uint64_t e = stage_off(gpos, d.addr) + d.len;
+			if (e > c->frame_cap)
+				break;
+			gpos = e;
+			cnt++;
+		}
+		while (!gather && i + cnt < n && cnt < c->desc_cap) {
 			const struct xcsum_desc &d = h_desc[i + cnt];
 			uint64_t nlo = d.addr < lo ? d.addr : lo;
 			uint64_t nhi = d.addr + d.len > hi ? d.addr + d.len : hi;
@@ -797,9 +881,31 @@ extern "C" int xcsum_rx_host(xcsum_ctx *c, const uint8_t *h_umem, const struct x
 		if (pend[slot].busy && (rc = finish(slot)))
 			return rc;
 		hipStream_t st = c->streams[slot];
+		bool direct = false;
 		RxArgs a;
+		a.desc = c->d_desc[slot];
+		a.msgs = c->d_rx_msgs[slot];
 		if (zc) {
 			a.umem = zc->dev + (h_umem - zc->host);
+		} else if (gather) {
+			uint64_t pos = 0;
+			for (uint32_t k = 0; k < cnt; k++) {
+				const struct xcsum_desc &d = h_desc[i + k];
+				const uint64_t off = stage_off(pos, d.addr);
+				memcpy(c->h_stage[slot] + off, h_umem + d.addr, d.len);
+				c->h_dstage[slot][k] = xcsum_desc{off, d.len, 0};
+				pos = off + d.len;
+			}
+			if (DIRECT_ON && pos <= DIRECT_MAX) {
+				direct = true;
+				a.umem = c->v_stage[slot];
+				a.desc = c->v_dstage[slot];
+				a.msgs = c->v_rx_msgs[slot];
+			} else {
+				HIPCHK(hipMemcpyAsync(c->d_frames[slot], c->h_stage[slot], pos,
+						      hipMemcpyHostToDevice, st));
+				a.umem = c->d_frames[slot];
+			}
 		} else {
 			/* 16-byte aligned copy of [lo, hi): every frame keeps its
 			 * address phase; the kernel sees umem + addr inside it */
@@ -808,22 +914,23 @@ extern "C" int xcsum_rx_host(xcsum_ctx *c, const uint8_t *h_umem, const struct x
 					      hipMemcpyHostToDevice, st));
 			a.umem = (const uint8_t *)((uintptr_t)c->d_frames[slot] - (uintptr_t)alo);
 		}
-		HIPCHK(hipMemcpyAsync(c->d_desc[slot], h_desc + i, cnt * sizeof(struct xcsum_desc),
-				      hipMemcpyHostToDevice, st));
-		a.desc = c->d_desc[slot];
+		if (!direct)
+			HIPCHK(hipMemcpyAsync(c->d_desc[slot], gather ? c->h_dstage[slot] : h_desc + i,
+					      cnt * sizeof(struct xcsum_desc), hipMemcpyHostToDevice, st));
 		a.n = cnt;
 		a.flags = flags & (XCSUM_F_VERIFY | XCSUM_F_IPHDR);
-		a.msgs = c->d_rx_msgs[slot];
 		a.count = nullptr;
 		a.part = c->d_rx_part;
-		HIPCHK(launch_rx(a, (uint32_t)((hi - lo) / cnt), c->cus, st));
-		HIPCHK(hipMemcpyAsync(c->h_rx_msgs[slot], c->d_rx_msgs[slot],
-				      (size_t)cnt * sizeof(struct xcsum_rx_msg), hipMemcpyDeviceToHost,
-				      st));
+		HIPCHK(launch_rx(a, (uint32_t)((gather ? gpos : hi - lo) / cnt), c->cus, st));
+		if (!direct)
+			HIPCHK(hipMemcpyAsync(c->h_rx_msgs[slot], c->d_rx_msgs[slot],
+					      (size_t)cnt * sizeof(struct xcsum_rx_msg),
+					      hipMemcpyDeviceToHost, st));
 		HIPCHK(hipEventRecord(c->done[slot], st));
 		pend[slot].first = i;
 		pend[slot].count = cnt;
 		pend[slot].busy = true;
+		pend[slot].gathered = gather;
 		i += cnt;
 		slot = (slot + 1) % Ctx::NSLOT;
 	}

@@ -151,6 +151,7 @@ struct Ctx {
 	uint16_t *h_out[NSLOT];        /* pinned */
 	struct xcsum_rx_msg *d_rx_msgs[NSLOT];  /* receive records (lazy) */
 	struct xcsum_rx_msg *h_rx_msgs[NSLOT];  /* pinned */
+	struct xcsum_rx_msg *v_rx_msgs[NSLOT];  /* their device address */
 	uint8_t *h_stage[NSLOT];       /* gathered frames (pinned, lazy) */
 	struct xcsum_desc *h_dstage[NSLOT];     /* their descriptors (pinned, lazy) */
 	/* device addresses of the pinned stage, its descriptors and the result

@@ -112,8 +112,27 @@ s12)
   tools/gpu_run.sh s12/bench_rx3_umem 300 python tools/bench_rx.py --configs 3 --layout umem --geoms "auto;4,2,0;4,2,1"
   tools/gpu_run.sh s12/e2e 300 python tools/bench_e2e.py
   ;;
+s13)
+  # receive host path: sparse batches in a pageable UMEM gathered frame by
+  # frame (XCSUM_RX_GATHER) vs the range copy, MTU and 64-byte frames
+  tools/gpu_run.sh s13/pytest_rx 600 python -u -m pytest tests/test_gpu_rx.py -m gpu -x -q --timeout 120 --timeout-method thread
+  for v in cur nogather; do
+    L=libxudp_amd/libxcsum.so; [ $v = cur ] || L=libxudp_amd/variants/$v/libxcsum.so
+    for c in 2 3; do
+      XCSUM_LIB=$L tools/gpu_run.sh s13/e2e_umem_c${c}_$v 300 python tools/bench_e2e.py --config $c --layout umem --reps 3
+    done
+  done
+  ;;
+s14)
+  # gather only where frames fill < 1/8 of the range (and the TX host batch
+  # too): host-path and receive tests, e2e on xudp's chunks, MTU and 64 B
+  tools/gpu_run.sh s14/pytest 600 python -u -m pytest tests/test_gpu_rx.py tests/test_gpu_host_path.py tests/test_gpu_host_direct.py -m gpu -x -q --timeout 120 --timeout-method thread
+  for c in 2 3; do
+    tools/gpu_run.sh s14/e2e_umem_c$c 300 python tools/bench_e2e.py --config $c --layout umem --reps 3
+  done
+  ;;
 *)
-  echo "usage: $0 s3|s4|s5|s6|s7|s8|s10|s11|s12" >&2
+  echo "usage: $0 s3|s4|s5|s6|s7|s8|s10|s11|s12|s13|s14" >&2
   exit 2
   ;;
 esac

@@ -8,7 +8,10 @@ hipMemcpyAsync H2D -> kernel -> 2-byte results D2H, for
 and each of them with XCSUM_F_INPLACE (udp->check written into the host
 frames); then the receive side, xcsum_rx_host with VERIFY on the same frames
 (checksums written in first), in the same three variants.  Also the raw
-pinned H2D copy rate for context.  One JSON line per variant.  Usage: python tools/bench_e2e.py [--config 2] [--reps 5]"""
+pinned H2D copy rate for context.  One JSON line per variant.
+--layout umem puts one frame per 4096-byte chunk (xudp's UMEM, SURVEY a14;
+256K frames, 1 GiB), the layout an AF_XDP RX ring hands over.
+Usage: python tools/bench_e2e.py [--config 2] [--reps 5] [--layout umem]"""
 import argparse
 import json
 import os
@@ -28,12 +31,17 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", type=int, default=2)
     ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--layout", default="packed", choices=["packed", "umem"])
     args = ap.parse_args()
     import torch
     cfg = dict(bench.CONFIGS[args.config], id=args.config)
     n = min(cfg["n"], 1 << 20)
+    lay = {}
+    if args.layout == "umem":
+        n = min(n, 1 << 18)
+        lay = dict(stride=4096, offset=322 if cfg["family"] == 6 else 342)
     umem, desc = X.gen_frames_host(n, cfg["family"], cfg["pmin"], cfg["pmax"],
-                                   seed=bench.SEED_BASE ^ args.config)
+                                   seed=bench.SEED_BASE ^ args.config, **lay)
     alg = X.alg_bytes(desc, cfg["family"])
     out = np.zeros(n, dtype=np.uint16)
     eng = X.Engine(0)
@@ -72,9 +80,10 @@ def main():
                 eng.unregister_umem(umem)
             if inplace:  # restore check fields for the next variant
                 umem2, _ = X.gen_frames_host(n, cfg["family"], cfg["pmin"], cfg["pmax"],
-                                             seed=bench.SEED_BASE ^ args.config)
+                                             seed=bench.SEED_BASE ^ args.config, **lay)
                 umem[:] = umem2
             print(json.dumps({"variant": variant, "inplace": inplace, "frames": n,
+                              "layout": args.layout,
                               "ms": round(dt * 1e3, 3),
                               "GiBps_alg": round(alg / dt / 2**30, 1),
                               "GBps_frames": round(umem.nbytes / dt / 1e9, 1),
@@ -100,6 +109,7 @@ def main():
         if variant != "pageable":
             eng.unregister_umem(umem)
         print(json.dumps({"variant": "rx_" + variant, "verify": True, "frames": n,
+                          "layout": args.layout, "frame_bytes": int(desc["len"].sum()),
                           "ms": round(dt * 1e3, 3),
                           "GBps_frames": round(umem.nbytes / dt / 1e9, 1),
                           "mpps": round(n / dt / 1e6, 1), "parity": ok}), flush=True)
