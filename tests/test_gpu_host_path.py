@@ -91,20 +91,29 @@ def test_host_batch_umem_mirror_layout(engine):
     assert np.array_equal(got, oracle.batch(umem, desc, X.MODE_V4_LEGACY))
 
 
+@pytest.mark.parametrize("register", [False, True])
 @pytest.mark.parametrize("n", [100, 5000, 70000])
 @pytest.mark.parametrize("fam", [4, 6])
-def test_host_batch_small_frames_in_slots(engine, n, fam):
-    """Small frames one per 4096-byte chunk of a pageable UMEM: gathered frame
+def test_host_batch_small_frames_in_slots(engine, n, fam, register):
+    """Small frames one per 4096-byte chunk: in a pageable UMEM gathered frame
     by frame (xcsum_batch_host, gather_pays; copy-free up to 256 KiB, staged
-    copies above, two chunks at 70,000 frames), plain and in place."""
+    copies above, two chunks at 70,000 frames), in a registered one read in
+    place without XCSUM_F_ZEROCOPY (zerocopy_pays); plain and in place."""
     umem, desc = X.gen_frames_host(n, fam, 0, 100, seed=31 + n, stride=4096,
                                    offset=322 if fam == 6 else 342)
     mode = X.MODE_V6 if fam == 6 else X.MODE_V4_RFC
     exp = oracle.batch(umem, desc, mode)
-    assert np.array_equal(host_batch(engine, umem, desc, mode), exp)
     flags = X.F_INPLACE | (X.F_IPHDR if fam == 4 else 0)
     before = umem.copy()
-    assert np.array_equal(host_batch(engine, umem, desc, mode, flags), exp)
+    if register:
+        engine.register_umem(umem)
+    try:
+        assert np.array_equal(host_batch(engine, umem, desc, mode), exp)
+        assert np.array_equal(umem, before)
+        assert np.array_equal(host_batch(engine, umem, desc, mode, flags), exp)
+    finally:
+        if register:
+            engine.unregister_umem(umem)
     a = desc["addr"].astype(np.int64)
     chk = 60 if fam == 6 else 40
     got = umem[a[:, None] + np.array([chk, chk + 1])].copy().view("<u2").ravel()

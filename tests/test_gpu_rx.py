@@ -240,22 +240,31 @@ def test_rx_host_vs_oracle(torch_cuda, engine, zerocopy):
             engine.unregister_umem(umem)
 
 
+@pytest.mark.parametrize("register", [False, True])
 @pytest.mark.parametrize("n", [100, 5000, 70000])
-def test_rx_host_sparse_umem_vs_oracle(engine, n):
+def test_rx_host_sparse_umem_vs_oracle(engine, n, register):
     """xcsum_rx_host on frames one per UMEM chunk, as an RX ring hands them
-    over: gathered frame by frame into the pinned stage (copy-free up to 256
-    KiB of frames, staged copies above, two chunks at 70,000 frames); the
-    records still hold UMEM offsets."""
+    over: from a pageable UMEM gathered frame by frame into the pinned stage
+    (copy-free up to 256 KiB of frames, staged copies above, two chunks at
+    70,000 frames), from a registered one read in place (zerocopy_pays); the
+    records hold UMEM offsets either way."""
     frames = [f for f, _ in rx_frames.corpus(seed=13)]
     rng = np.random.default_rng(14)
     umem, desc = umem_chunks(frames, rng, n)
-    for flags in FLAGS.values():
-        msgs = np.full(n * 64, 0xA5, dtype=np.uint8).view(X.RX_MSG_DTYPE)
-        count = engine.rx_host(umem, desc, msgs, flags)
-        exp = oracle.rx_batch(umem, desc, flags)
-        bad = np.nonzero(msgs.view(np.uint8).reshape(-1, 64) != exp.view(np.uint8).reshape(-1, 64))
-        assert len(bad[0]) == 0, (flags, sorted(set(bad[0].tolist()))[:10])
-        assert count == int((exp["status"] == X.RX_OK).sum())
+    if register:
+        engine.register_umem(umem)
+    try:
+        for flags in FLAGS.values():
+            msgs = np.full(n * 64, 0xA5, dtype=np.uint8).view(X.RX_MSG_DTYPE)
+            count = engine.rx_host(umem, desc, msgs, flags)
+            exp = oracle.rx_batch(umem, desc, flags)
+            bad = np.nonzero(msgs.view(np.uint8).reshape(-1, 64) !=
+                             exp.view(np.uint8).reshape(-1, 64))
+            assert len(bad[0]) == 0, (flags, sorted(set(bad[0].tolist()))[:10])
+            assert count == int((exp["status"] == X.RX_OK).sum())
+    finally:
+        if register:
+            engine.unregister_umem(umem)
 
 
 def test_rx_host_errors(engine):

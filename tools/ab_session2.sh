@@ -131,8 +131,22 @@ s14)
     tools/gpu_run.sh s14/e2e_umem_c$c 300 python tools/bench_e2e.py --config $c --layout umem --reps 3
   done
   ;;
+s15)
+  # whole GPU suite, smoke and the driver's bench command on the session's final code
+  tools/gpu_run.sh s15/pytest_gpu 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread
+  tools/gpu_run.sh s15/smoke 200 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')"
+  tools/gpu_run.sh s15/bench 300 python bench.py --gpus 1 --steps 20 --warmup 5
+  tools/gpu_run.sh s15/ring_bench 300 tests/c/umem_ring --bench 1,16,100,1024,4096
+  ;;
+s16)
+  # sparse batches in a registered UMEM read in place without XCSUM_F_ZEROCOPY
+  tools/gpu_run.sh s16/pytest 600 python -u -m pytest tests/test_gpu_rx.py tests/test_gpu_host_path.py tests/test_gpu_host_direct.py tests/test_capi.py -m gpu -x -q --timeout 120 --timeout-method thread
+  for c in 2 3; do
+    tools/gpu_run.sh s16/e2e_umem_c$c 300 python tools/bench_e2e.py --config $c --layout umem --reps 3
+  done
+  ;;
 *)
-  echo "usage: $0 s3|s4|s5|s6|s7|s8|s10|s11|s12|s13|s14" >&2
+  echo "usage: $0 s3|s4|s5|s6|s7|s8|s10|s11|s12|s13|s14|s15|s16" >&2
   exit 2
   ;;
 esac
