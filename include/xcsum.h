@@ -223,9 +223,9 @@ int xcsum_rx_device(xcsum_ctx *ctx, const uint8_t *d_umem, const struct xcsum_de
  * frames are staged to the device with chunked, double-buffered
  * hipMemcpyAsync, or with XCSUM_F_ZEROCOPY read in place over PCIe from a
  * registered UMEM; the 64-byte records come back into h_msgs.  A sparse
- * batch of small frames (one frame per UMEM chunk, as the RX ring hands
- * them over) is gathered frame by frame from a pageable UMEM and read in
- * place from a registered one, instead of copying the range with its gaps.
+ * batch (one frame per UMEM chunk, as the RX ring hands them over) is read
+ * in place from a registered UMEM, and its small frames are gathered frame
+ * by frame from a pageable one, instead of copying the range with its gaps.
  * Records hold UMEM offsets either way.  *h_count (may be NULL)
  * = number of XCSUM_RX_OK records.  flags: XCSUM_F_VERIFY, XCSUM_F_IPHDR,
  * XCSUM_F_ZEROCOPY.  Synchronous. */
@@ -238,11 +238,11 @@ int xcsum_rx_host(xcsum_ctx *ctx, const uint8_t *h_umem, const struct xcsum_desc
  * registered) -> kernel -> the 2-byte results back; with XCSUM_F_INPLACE the
  * results are also written into the host frames' udp->check (and iph->check
  * with XCSUM_F_IPHDR).  With XCSUM_F_ZEROCOPY and a registered UMEM the
- * kernel reads the frames in place over PCIe instead.  Small frames spread
- * over the UMEM (filling under 1/8 of the range they span, e.g. one per
- * 4096-byte chunk) are gathered frame by frame from a pageable UMEM, and
- * read in place from a registered one even without XCSUM_F_ZEROCOPY; the
- * results do not depend on the transport. */
+ * kernel reads the frames in place over PCIe instead.  Frames spread over
+ * the UMEM (one per 4096-byte chunk, as xudp lays them out) are read in
+ * place from a registered UMEM even without XCSUM_F_ZEROCOPY, and small ones
+ * are gathered frame by frame from a pageable UMEM; the results do not
+ * depend on the transport. */
 int xcsum_batch_host(xcsum_ctx *ctx, uint8_t *h_umem, const struct xcsum_desc *h_desc,
 		     uint32_t n, uint16_t *h_out, uint32_t mode, uint32_t flags);
 

@@ -536,12 +536,14 @@ static bool gather_pays(const xcsum_ctx *c, const uint8_t *h_umem, uint64_t lo, 
 	       !find_region(c, h_umem + lo, h_umem + hi);
 }
 
-/* The same sparse batch in a registered UMEM is read in place (zero-copy)
- * even without XCSUM_F_ZEROCOPY: the range copy moves 4 KB of PCIe per
- * 106-byte frame.  Results are the same bytes either way.  256K 64-byte
- * frames in 4096-byte chunks: 20 ms copied, 1.3 ms in place (checksum),
- * 22.5 / 3.1 ms (receive) (profiles/r02/session2/rx_gather/).  Returns the
- * region, or null. */
+/* A sparse batch in a registered UMEM (the frames fill less than half of
+ * the range they span) is read in place (zero-copy) even without
+ * XCSUM_F_ZEROCOPY: the range copy moves the gaps over PCIe too.  Results
+ * are the same bytes either way.  256K frames in 4096-byte chunks
+ * (profiles/r02/session2/rx_gather/): 64-byte frames 20 ms copied, 1.5 ms in
+ * place (checksum), 22.5 / 2.9 ms (receive); MTU frames 19.6 / 7.6-8.5 ms,
+ * 22.6 / 9.5 ms.  Dense batches keep the copy (packed MTU frames: 31.9 ms
+ * copied, 39.2 ms in place).  Returns the region, or null. */
 static const Region *zerocopy_pays(const xcsum_ctx *c, const uint8_t *h_umem,
 				   const struct xcsum_desc *h_desc, uint32_t n)
 {
@@ -551,7 +553,7 @@ static const Region *zerocopy_pays(const xcsum_ctx *c, const uint8_t *h_umem,
 		if (h_desc[i].addr + h_desc[i].len > hi) hi = h_desc[i].addr + h_desc[i].len;
 		sum += h_desc[i].len;
 	}
-	if (!XCSUM_RX_GATHER || n == 0 || hi - lo <= 8 * sum + 4096)
+	if (!XCSUM_RX_GATHER || n == 0 || hi - lo <= 2 * sum + 4096)
 		return nullptr;
 	return find_region(c, h_umem + lo, h_umem + hi);
 }

@@ -145,8 +145,18 @@ s16)
     tools/gpu_run.sh s16/e2e_umem_c$c 300 python tools/bench_e2e.py --config $c --layout umem --reps 3
   done
   ;;
+s17)
+  # any sparse batch in a registered UMEM read in place (2x rule): whole
+  # suite, TX ring harness by batch size, end to end on xudp's chunks
+  tools/gpu_run.sh s17/pytest_gpu 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread
+  tools/gpu_run.sh s17/ring_bench 300 tests/c/umem_ring --bench 1,16,100,1024,4096
+  for c in 2 3 4; do
+    tools/gpu_run.sh s17/e2e_umem_c$c 300 python tools/bench_e2e.py --config $c --layout umem --reps 3
+  done
+  tools/gpu_run.sh s17/e2e_packed_c2 300 python tools/bench_e2e.py --config 2 --reps 3
+  ;;
 *)
-  echo "usage: $0 s3|s4|s5|s6|s7|s8|s10|s11|s12|s13|s14|s15|s16" >&2
+  echo "usage: $0 s3|s4|s5|s6|s7|s8|s10|s11|s12|s13|s14|s15|s16|s17" >&2
   exit 2
   ;;
 esac
