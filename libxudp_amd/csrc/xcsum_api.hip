@@ -187,16 +187,38 @@ extern "C" int xcsum_ctx_take_errors(xcsum_ctx *c, uint64_t *count)
 	return 0;
 }
 
-static void set_order(const xcsum_ctx *c, CsumArgs &a)
+/* Visiting order of a checksum launch.  Forced (xcsum_ctx_set_order), or
+ * automatic: 32 regions of 16-frame tiles if the kernel finds the batch
+ * sparse in the UMEM (profiles/r01/order_*.log), else the dense order of
+ * the geometry, measured in round 2 (profiles/r02/session2/order_dense/):
+ * MTU frames (16,2,6) 8 regions of 16-frame tiles, in the bench config 2
+ * 0.2408 -> 0.2338 ms and config 4 0.2415 -> 0.2344 ms (16 regions: 0.2349
+ * / 0.2342, 4 regions 0.2375 / 0.2417); mixed sizes (64,1,9) 16 regions of
+ * 4-frame tiles, config 5 6.01 -> 5.86 ms.  Frames spread over 8-32 places
+ * of the batch keep more HBM channels busy than one contiguous window.
+ * (Round 1 measured forced region orders 1-4 % slower on packed frames,
+ * with the kernel of that time.)  Other geometries keep descriptor order
+ * for dense batches. */
+/* XCSUM_DENSE_ORDER=0 builds descriptor order for dense batches (A/B only) */
+#ifndef XCSUM_DENSE_ORDER
+#define XCSUM_DENSE_ORDER 1
+#endif
+
+static void set_order(const xcsum_ctx *c, CsumArgs &a, const Geometry &g)
 {
 	if (c->order_rlog >= 0) {
 		a.ord = order_regions(a.n, c->order_rlog, c->order_tlog);
+		a.dense = a.ord;
 		return;
 	}
-	/* automatic: 32 regions of 16-frame tiles if the kernel finds the batch
-	 * sparse in the UMEM, else descriptor order (profiles/r01/order_*.log) */
 	a.ord = order_regions(a.n, 5, 4);
 	a.ord.sparse_only = a.ord.rshift != 0;
+	if (XCSUM_DENSE_ORDER && g.G == 16 && g.U == 2 && g.K == 6)
+		a.dense = order_regions(a.n, 3, 4);
+	else if (XCSUM_DENSE_ORDER && g.G == 64 && g.U == 1)
+		a.dense = order_regions(a.n, 4, 2);
+	else
+		a.dense = order_identity(a.n);
 }
 
 static Geometry geometry_for(const xcsum_ctx *c, uint32_t len_hint, uint32_t flags)
@@ -270,8 +292,9 @@ extern "C" int xcsum_batch_device(xcsum_ctx *c, uint8_t *d_umem, const struct xc
 		a.flags &= ~XCSUM_F_INPLACE; /* verifying never writes frames */
 	a.bias = 0;
 	a.err = c->d_err;
-	set_order(c, a);
-	HIPCHK(launch_csum(a, geometry_for(c, len_hint, a.flags), c->cus, (hipStream_t)stream));
+	const Geometry g = geometry_for(c, len_hint, a.flags);
+	set_order(c, a, g);
+	HIPCHK(launch_csum(a, g, c->cus, (hipStream_t)stream));
 	return 0;
 }
 
@@ -699,6 +722,7 @@ int batch_host_impl(xcsum_ctx *c, uint8_t *h_umem, const struct xcsum_desc *h_de
 		a.desc = c->d_desc[slot];
 		a.n = cnt;
 		a.ord = order_identity(cnt);
+		a.dense = a.ord;
 		a.out = c->d_out[slot];
 		a.out_ip = want_ip ? c->d_out[slot] + cnt : nullptr;
 		a.mode = mode;

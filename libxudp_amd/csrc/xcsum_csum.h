@@ -17,13 +17,14 @@ namespace xcsum {
  * (s_load_dwordx4, counted on lgkmcnt): the compiler moves uniform values to
  * SGPRs right after a vector load, which would make every prefetched
  * descriptor wait stall on the in-order vmcnt of the chunk loads. */
-/* Automatic order (ord.sparse_only): keep the prepared region order only when
- * the batch is sparse in the UMEM -- the first and last descriptors span more
- * than twice the bytes of n frames of their mean length.  xudp's TX UMEM (one
- * ~1.5 KB frame per 4096-B chunk, every frame at the same in-chunk offset)
- * is the case: visited in descriptor order, the frames in flight hit a
- * narrow set of HBM channels (tools/slot_probe.py).  Wave-uniform scalar
- * loads; the result never depends on the order. */
+/* Automatic order (ord.sparse_only): keep the prepared region order when the
+ * batch is sparse in the UMEM -- the first and last descriptors span more
+ * than twice the bytes of n frames of their mean length -- else take the
+ * dense batch's order (a.dense).  xudp's TX UMEM (one ~1.5 KB frame per
+ * 4096-B chunk, every frame at the same in-chunk offset) is the sparse case:
+ * visited in descriptor order, the frames in flight hit a narrow set of HBM
+ * channels (tools/slot_probe.py).  Wave-uniform scalar loads; the result
+ * never depends on the order. */
 static __device__ __forceinline__ void resolve_order(CsumArgs &a)
 {
 	if (!a.ord.sparse_only)
@@ -38,7 +39,7 @@ static __device__ __forceinline__ void resolve_order(CsumArgs &a)
 		sparse = al > a0 && al + dl.z - a0 > 2ull * a.n * mean;
 	}
 	if (!sparse)
-		a.ord = order_identity(a.n);
+		a.ord = a.dense;
 }
 
 /* dense batch: the first and last descriptors span at most twice the bytes

@@ -59,6 +59,8 @@ struct CsumArgs {
 	uint64_t bias;
 	unsigned long long *err;       /* device counter of malformed frames */
 	Order ord;
+	Order dense;                   /* ord.sparse_only: the order a dense batch
+					  gets instead (resolve_order) */
 };
 
 /* Frame-build kernel arguments (xcsum_build.hip). */
@@ -86,6 +88,7 @@ struct RxArgs {
 	uint32_t *count;               /* may be null */
 	uint32_t *part;                /* per-block counts (ctx scratch, RX_PART_MAX) */
 	Order ord;                     /* visiting order (set by launch_rx) */
+	Order dense;                   /* ord.sparse_only: a dense batch's order */
 };
 
 /* per-block delivered counts of one receive launch: >= CUs x blocks per CU */

@@ -467,6 +467,7 @@ hipError_t launch_csum(const CsumArgs &a, Geometry g, int cus, hipStream_t s)
 		return launch_seg(a, g.U, g.K, cus, g.B, s);
 	CsumArgs b = a;
 	b.ord = order_identity(a.n);
+	b.dense = b.ord;
 	if (g.G == 16 && g.U == 12 && g.K == 6) return launch_lds_t<6, 2>(b, cus, g.B, s);
 	if (g.G == 16 && g.U == 13 && g.K == 6) return launch_lds_t<6, 3>(b, cus, g.B, s);
 	if (g.G == 16 && g.U == 14 && g.K == 3) return launch_lds_t<3, 4>(b, cus, g.B, s);

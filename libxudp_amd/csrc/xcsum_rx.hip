@@ -292,7 +292,7 @@ static __device__ __forceinline__ void rx_resolve_order(RxArgs &a)
 		sparse = al > a0 && al + dl.z - a0 > 2ull * a.n * mean;
 	}
 	if (!sparse)
-		a.ord = order_identity(a.n);
+		a.ord = a.dense;
 }
 
 static __device__ __forceinline__ RFrame rx_resolve(const RxArgs &a, u32x3 d, bool present)
@@ -1416,6 +1416,7 @@ hipError_t launch_rx(const RxArgs &a, uint32_t len_hint, int cus, hipStream_t s)
 	 * XCSUM_RX_ORDER=0 turns it off, "R,T" sets it (A/B). */
 	const char *oe = getenv("XCSUM_RX_ORDER");
 	int rlog = 5, tlog = 6;
+	b.dense = order_identity(a.n);
 	if (oe && sscanf(oe, "%d,%d", &rlog, &tlog) == 1 && rlog == 0) {
 		b.ord = order_identity(a.n);   /* "0": off */
 	} else {
@@ -1424,6 +1425,15 @@ hipError_t launch_rx(const RxArgs &a, uint32_t len_hint, int cus, hipStream_t s)
 			tlog = 6;
 		b.ord = order_regions(a.n, rlog, tlog);
 		b.ord.sparse_only = 1u;
+		/* dense batches: XCSUM_RX_DENSE="R,T" (A/B; the stream kernel,
+		 * U = 3, needs descriptor order for them) */
+		const char *de = getenv("XCSUM_RX_DENSE");
+		int dr = 0, dt = 6;
+		if (U != 3 && de && sscanf(de, "%d,%d", &dr, &dt) >= 1 && dr > 0) {
+			if (U == 0 && dt < 6)
+				dt = 6;
+			b.dense = order_regions(a.n, dr, dt);
+		}
 	}
 #define X(g_, k_, u_) \
 	if (G == g_ && K == k_ && U == u_) return launch_rx_t<g_, k_, u_>(b, cus, B, s);

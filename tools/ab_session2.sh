@@ -155,8 +155,64 @@ s17)
   done
   tools/gpu_run.sh s17/e2e_packed_c2 300 python tools/bench_e2e.py --config 2 --reps 3
   ;;
+s18)
+  # config 5: visiting orders (2^R regions of 2^T-frame tiles) against the
+  # plain cyclic assignment: blocked (one region per wave) to interleaved
+  tools/gpu_run.sh s18/sweep5_orders 300 python tools/sweep.py --config 5 --geoms 64,1,9 --bpc 0 --orders="0,0;11,0;10,0;8,0;5,0;11,2;5,2;3,4" --rounds 2 --launches 8
+  ;;
+s19)
+  # config 5 orders, finer; and the MTU configs (2, 4) under the same orders
+  tools/gpu_run.sh s19/sweep5_orders 400 python tools/sweep.py --config 5 --geoms 64,1,9 --bpc 0 --orders="0,0;5,2;5,1;5,3;4,2;6,2;7,2;3,2;5,0" --rounds 3 --launches 8
+  tools/gpu_run.sh s19/sweep2_orders 300 python tools/sweep.py --config 2 --geoms 16,2,6 --bpc 0 --orders="0,0;5,2;5,4;3,4" --rounds 3 --launches 20
+  ;;
+s20)
+  # packed MTU configs: orders swept finer, then the bench itself (graph
+  # replay) with XCSUM_ORDER forced vs automatic, interleaved processes
+  tools/gpu_run.sh s20/sweep2_orders 400 python tools/sweep.py --config 2 --geoms 16,2,6 --bpc 0 --orders="0,0;3,4;2,4;3,3;3,5;4,4;2,5;3,6;1,4" --rounds 3 --launches 20
+  tools/gpu_run.sh s20/sweep4_orders 300 python tools/sweep.py --config 4 --geoms 16,2,6 --bpc 0 --orders="0,0;3,4;2,4;4,4;3,5" --rounds 3 --launches 20
+  for r in 1 2; do
+    for o in auto 3,4 2,4; do
+      if [ $o = auto ]; then E=; else E="XCSUM_ORDER=$o"; fi
+      env $E tools/gpu_run.sh s20/bench_c2_${o/,/_}_$r 200 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-ceiling
+    done
+  done
+  ;;
+s21)
+  # dense-batch visiting order per geometry (XCSUM_DENSE_ORDER): suite, then
+  # the bench per config and flag sweeps against the descriptor-order build
+  tools/gpu_run.sh s21/pytest_gpu 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread
+  for r in 1 2; do
+    for v in cur nodense; do
+      L=libxudp_amd/libxcsum.so; [ $v = cur ] || L=libxudp_amd/variants/$v/libxcsum.so
+      for c in 2 4 5; do
+        XCSUM_LIB=$L tools/gpu_run.sh s21/bench_c${c}_${v}_$r 200 python bench.py --config $c --steps 20 --warmup 5 --no-cpu-baseline --no-ceiling
+      done
+      XCSUM_LIB=$L tools/gpu_run.sh s21/flags_c2_${v}_$r 200 python tools/sweep.py --config 2 --geoms 16,2,6 --bpc 0 --orders=-1,0 --flags inplace,iphdr --rounds 2 --launches 20
+      XCSUM_LIB=$L tools/gpu_run.sh s21/verify_c2_${v}_$r 200 python tools/sweep.py --config 2 --geoms 16,2,6 --bpc 0 --orders=-1,0 --flags verify --rounds 2 --launches 20
+    done
+  done
+  ;;
+s22)
+  # dense order for MTU frames: 8 vs 16 regions of 16-frame tiles, in the bench
+  for r in 1 2 3; do
+    for o in 3,4 4,4 2,4; do
+      for c in 2 4; do
+        XCSUM_ORDER=$o tools/gpu_run.sh s22/bench_c${c}_${o/,/_}_$r 200 python bench.py --config $c --steps 20 --warmup 5 --no-cpu-baseline --no-ceiling
+      done
+    done
+  done
+  ;;
+s23)
+  # the receive kernels under dense-batch region orders (XCSUM_RX_DENSE)
+  for r in 1 2; do
+    for o in none 3,6 4,6 5,6; do
+      if [ $o = none ]; then E=; else E="XCSUM_RX_DENSE=$o"; fi
+      env $E tools/gpu_run.sh s23/rx_${o/,/_}_$r 300 python tools/bench_rx.py --configs 2,4,5 --only verify,csum_verify
+    done
+  done
+  ;;
 *)
-  echo "usage: $0 s3|s4|s5|s6|s7|s8|s10|s11|s12|s13|s14|s15|s16|s17" >&2
+  echo "usage: $0 s3|s4|s5|s6|s7|s8|s10|s11|s12|s13|s14|s15|s16|s17|s18|s19|s20|s21|s22|s23" >&2
   exit 2
   ;;
 esac
