@@ -194,7 +194,9 @@ extern "C" int xcsum_ctx_take_errors(xcsum_ctx *c, uint64_t *count)
  * MTU frames (16,2,6) 8 regions of 16-frame tiles, in the bench config 2
  * 0.2408 -> 0.2338 ms and config 4 0.2415 -> 0.2344 ms (16 regions: 0.2349
  * / 0.2342, 4 regions 0.2375 / 0.2417); mixed sizes (64,1,9) 16 regions of
- * 4-frame tiles, config 5 6.01 -> 5.86 ms.  Frames spread over 8-32 places
+ * 4-frame tiles, config 5 6.01 -> 5.86 ms; 400-760-byte frames (16,1,2) /
+ * (16,1,3) 32 regions of 16-frame tiles, -5 %; 150-byte frames (8,1,2)
+ * lose under it and keep descriptor order.  Frames spread over 8-32 places
  * of the batch keep more HBM channels busy than one contiguous window.
  * (Round 1 measured forced region orders 1-4 % slower on packed frames,
  * with the kernel of that time.)  Other geometries keep descriptor order
@@ -215,6 +217,10 @@ static void set_order(const xcsum_ctx *c, CsumArgs &a, const Geometry &g)
 	a.ord.sparse_only = a.ord.rshift != 0;
 	if (XCSUM_DENSE_ORDER && g.G == 16 && g.U == 2 && g.K == 6)
 		a.dense = order_regions(a.n, 3, 4);
+	else if (XCSUM_DENSE_ORDER && g.G == 16 && g.U == 1 && (g.K == 2 || g.K == 3))
+		a.dense = order_regions(a.n, 5, 4);   /* 400 / 700-byte payloads:
+							 0.0888 -> 0.0842 ms,
+							 0.1408 -> 0.1343 ms (s24) */
 	else if (XCSUM_DENSE_ORDER && g.G == 64 && g.U == 1)
 		a.dense = order_regions(a.n, 4, 2);
 	else

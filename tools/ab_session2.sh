@@ -211,8 +211,18 @@ s23)
     done
   done
   ;;
+s24)
+  # final tree: whole suite, smoke, driver bench; dense orders for the
+  # mid-size geometries (payloads 150 / 400 / 700 B: (8,1,2), (16,1,2), (16,1,3))
+  tools/gpu_run.sh s24/pytest_gpu 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread
+  tools/gpu_run.sh s24/smoke 200 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')"
+  tools/gpu_run.sh s24/bench 300 python bench.py --gpus 1 --steps 20 --warmup 5
+  for p in 150 400 700; do
+    tools/gpu_run.sh s24/sweep_p$p 300 python tools/sweep.py --config 2 --payload $p,$p --geoms auto --bpc 0 --orders="-1,0;3,4;4,4;4,2;5,4" --rounds 3 --launches 20
+  done
+  ;;
 *)
-  echo "usage: $0 s3|s4|s5|s6|s7|s8|s10|s11|s12|s13|s14|s15|s16|s17|s18|s19|s20|s21|s22|s23" >&2
+  echo "usage: $0 s3|s4|s5|s6|s7|s8|s10|s11|s12|s13|s14|s15|s16|s17|s18|s19|s20|s21|s22|s23|s24" >&2
   exit 2
   ;;
 esac

@@ -33,12 +33,15 @@ def main():
                          "-1,0 = automatic)")
     ap.add_argument("--layout", default="packed", choices=["packed", "umem"])
     ap.add_argument("--flags", default="", help="comma list of inplace,iphdr,verify,rfc")
+    ap.add_argument("--payload", default="", help="MIN,MAX payload bytes instead of the config's")
     args = ap.parse_args()
     fl = {"inplace": X.F_INPLACE, "iphdr": X.F_IPHDR, "verify": X.F_VERIFY}
     flags = sum(fl[f] for f in args.flags.split(",") if f in fl)
     import torch
     dev = torch.device("cuda:0")
     cfg = dict(bench.CONFIGS[args.config], id=args.config, layout=args.layout)
+    if args.payload:
+        cfg["pmin"], cfg["pmax"] = (int(v) for v in args.payload.split(","))
     eng = X.Engine(0)
     s = torch.cuda.current_stream(dev)
     desc, d_desc, bufs, out, first, count = bench.build_batch(cfg, 0, 1, torch, dev, eng,
@@ -47,32 +50,36 @@ def main():
     mode = cfg["mode"]
     if "rfc" in args.flags.split(",") and cfg["family"] == 4:
         mode = X.MODE_V4_RFC
-    geoms = GEOMS if not args.geoms else [tuple(int(v) for v in g.split(","))
+    # "auto": the library's own pick from the batch's mean frame length
+    geoms = GEOMS if not args.geoms else [(0, 0, 0) if g == "auto" else
+                                          tuple(int(v) for v in g.split(","))
                                           for g in args.geoms.split(";")]
+    len_hint = int(desc["len"].mean()) if len(desc) else 0
     bpcs = [int(b) for b in args.bpc.split(",")]
     orders = [tuple(int(v) for v in o.split(",")) for o in args.orders.split(";")]
     geoms = [(g, b, o) for g in geoms for b in bpcs for o in orders]
     times = {g: [] for g in geoms}
     for r in range(args.rounds):
         for g, b, o in geoms:
-            eng.set_geometry(*g)
+            eng.set_geometry(*g) if g[0] else eng.set_geometry(0)
             eng.set_launch(b)
             eng.set_order(*o)
             for k in range(3):
                 eng.batch_device(bufs[k % len(bufs)], d_desc, count, out, mode, flags,
-                                 stream=s.cuda_stream)
+                                 len_hint, stream=s.cuda_stream)
             evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
                    for _ in range(args.launches)]
             for k in range(args.launches):
                 evs[k][0].record(s)
                 eng.batch_device(bufs[k % len(bufs)], d_desc, count, out, mode, flags,
-                                 stream=s.cuda_stream)
+                                 len_hint, stream=s.cuda_stream)
                 evs[k][1].record(s)
             torch.cuda.synchronize()
             times[(g, b, o)] += [e0.elapsed_time(e1) for e0, e1 in evs]
     for g, b, o in geoms:
         t = np.array(times[(g, b, o)])
-        print(json.dumps({"config": args.config, "layout": args.layout, "flags": args.flags,
+        print(json.dumps({"config": args.config, "payload": [cfg["pmin"], cfg["pmax"]],
+                          "layout": args.layout, "flags": args.flags,
                           "geometry": g, "bpc": b,
                           "order": o, "median_ms": round(float(
             np.median(t)), 4), "min_ms": round(float(t.min()), 4), "GBps_median": round(
