@@ -221,8 +221,16 @@ s24)
     tools/gpu_run.sh s24/sweep_p$p 300 python tools/sweep.py --config 2 --payload $p,$p --geoms auto --bpc 0 --orders="-1,0;3,4;4,4;4,2;5,4" --rounds 3 --launches 20
   done
   ;;
+s25)
+  # the final tree: whole suite and smoke; the mid-size payloads again under the new default
+  tools/gpu_run.sh s25/pytest_gpu 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread
+  tools/gpu_run.sh s25/smoke 200 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')"
+  for p in 400 700; do
+    tools/gpu_run.sh s25/sweep_p$p 300 python tools/sweep.py --config 2 --payload $p,$p --geoms auto --bpc 0 --orders="-1,0;0,0" --rounds 3 --launches 20
+  done
+  ;;
 *)
-  echo "usage: $0 s3|s4|s5|s6|s7|s8|s10|s11|s12|s13|s14|s15|s16|s17|s18|s19|s20|s21|s22|s23|s24" >&2
+  echo "usage: $0 s3|s4|s5|s6|s7|s8|s10|s11|s12|s13|s14|s15|s16|s17|s18|s19|s20|s21|s22|s23|s24|s25" >&2
   exit 2
   ;;
 esac
