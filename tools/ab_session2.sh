@@ -229,8 +229,15 @@ s25)
     tools/gpu_run.sh s25/sweep_p$p 300 python tools/sweep.py --config 2 --payload $p,$p --geoms auto --bpc 0 --orders="-1,0;0,0" --rounds 3 --launches 20
   done
   ;;
+s26)
+  # sparse batches (xudp's 4096-byte slots): the region order re-swept with
+  # round 2's kernels, MTU IPv4 / IPv6 and the in-place header build flags
+  tools/gpu_run.sh s26/sweep2u 300 python tools/sweep.py --config 2 --layout umem --geoms auto --bpc 0 --orders="-1,0;4,4;3,4;6,4;5,3;5,5;4,3;6,3" --rounds 3 --launches 20
+  tools/gpu_run.sh s26/sweep4u 300 python tools/sweep.py --config 4 --layout umem --geoms auto --bpc 0 --orders="-1,0;4,4;6,4;5,3;5,5" --rounds 3 --launches 20
+  tools/gpu_run.sh s26/sweep2u_ip 300 python tools/sweep.py --config 2 --layout umem --geoms auto --bpc 0 --orders="-1,0;4,4;6,4;5,3;5,5" --flags inplace,iphdr --rounds 3 --launches 20
+  ;;
 *)
-  echo "usage: $0 s3|s4|s5|s6|s7|s8|s10|s11|s12|s13|s14|s15|s16|s17|s18|s19|s20|s21|s22|s23|s24|s25" >&2
+  echo "usage: $0 s3|s4|s5|s6|s7|s8|s10|s11|s12|s13|s14|s15|s16|s17|s18|s19|s20|s21|s22|s23|s24|s25|s26" >&2
   exit 2
   ;;
 esac
