@@ -201,6 +201,19 @@ static __device__ __forceinline__ uint32_t lds_bytes4(const uint8_t *st, uint32_
 	return __builtin_amdgcn_alignbyte(w[1], w[0], o & 3u);
 }
 
+/* The 64-frame groups of a batch are visited in 2^XCSUM_STREAM_RLOG regions
+ * of 2^XCSUM_STREAM_TLOG-group tiles (RLOG 0: descriptor order), as the
+ * frame-group kernels visit dense batches (xcsum_api.hip, set_order).
+ * Config 3 in the bench, two processes each (profiles/r02/session2/
+ * stream_order/): 16 regions of single groups 0.0231 -> 0.0227 ms; 8
+ * regions of 4-group tiles 0.0230; 32 regions of 4-group tiles 0.0235. */
+#ifndef XCSUM_STREAM_RLOG
+#define XCSUM_STREAM_RLOG 4
+#endif
+#ifndef XCSUM_STREAM_TLOG
+#define XCSUM_STREAM_TLOG 0
+#endif
+
 template <int KC>
 static __device__ __forceinline__ void stream_loop(const CsumArgs &a, u32x4 *stage)
 {
@@ -208,11 +221,16 @@ static __device__ __forceinline__ void stream_loop(const CsumArgs &a, u32x4 *sta
 	const uint32_t nw = gridDim.x * 4;
 	const uint8_t *zero = (const uint8_t *)g_zero_chunk;
 	const uint8_t *st8 = (const uint8_t *)stage;
+	const uint32_t ngroups = (uint32_t)(((uint64_t)a.n + 63) >> 6);
+	const Order go = XCSUM_STREAM_RLOG ? order_regions(ngroups, XCSUM_STREAM_RLOG, XCSUM_STREAM_TLOG)
+					   : order_identity(ngroups);
+	/* logical wave-iteration -> group of 64 frames (>= ngroups: none) */
+	auto grp = [&](uint32_t wi) { return wi < go.nlog ? frame_of(go, wi) : ngroups; };
 	uint32_t w = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
 
 	auto span_of = [&](uint32_t wi, u32x4 d) {
 		StreamSpan sp;
-		const uint32_t p = 64u * wi + lane;
+		const uint64_t p = 64ull * grp(wi) + lane;
 		sp.present = p < a.n;
 		sp.eth = ((((uint64_t)d.y << 32) | d.x) - a.bias);
 		sp.len = d.z;
@@ -224,7 +242,12 @@ static __device__ __forceinline__ void stream_loop(const CsumArgs &a, u32x4 *sta
 	 * (two readlanes -- a packed batch is in UMEM order); every frame must
 	 * then lie inside them (one ballot), else the wave walks its frames. */
 	auto region = [&](uint32_t wi, const StreamSpan &sp, uint64_t &base, uint32_t &nch) {
-		const uint64_t rem = a.n - 64ull * wi;
+		if (grp(wi) >= ngroups) {   /* a padding slot of the order: no frames */
+			base = 0;
+			nch = 0;
+			return;
+		}
+		const uint64_t rem = a.n - 64ull * grp(wi);
 		const uint32_t last = rem > 64 ? 63u : (uint32_t)rem - 1u;
 		const uint64_t end = sp.eth + sp.len;
 		const uint64_t lo =
@@ -246,11 +269,11 @@ static __device__ __forceinline__ void stream_loop(const CsumArgs &a, u32x4 *sta
 		}
 	};
 	auto load_d = [&](uint32_t wi) {
-		const uint32_t p = 64u * wi + lane;
+		const uint64_t p = 64ull * grp(wi) + lane;
 		return *((gu32x4 *)(a.desc + (p < a.n ? p : a.n - 1)));
 	};
 
-	if (64ull * w >= a.n)
+	if (w >= go.nlog)
 		return;
 	u32x4 d = load_d(w);
 	StreamSpan sc = span_of(w, d);
@@ -260,7 +283,7 @@ static __device__ __forceinline__ void stream_loop(const CsumArgs &a, u32x4 *sta
 	u32x4 v[KC];
 	issue_region(bc, nc, v);
 	d = load_d(w + nw);
-	for (; 64ull * w < a.n; w += nw) {
+	for (; w < go.nlog; w += nw) {
 		/* this iteration's region -> LDS (waits for its loads only: the
 		 * descriptors issued after them may still be in flight) */
 #pragma unroll
@@ -270,7 +293,7 @@ static __device__ __forceinline__ void stream_loop(const CsumArgs &a, u32x4 *sta
 		const uint64_t cbase = bc;
 		const uint32_t cnch = nc;
 		/* next iteration: its region's loads go out before this one is summed */
-		if (64ull * (w + nw) < a.n) {
+		if (w + nw < go.nlog) {
 			sc = span_of(w + nw, d);
 			region(w + nw, sc, bc, nc);
 			__builtin_amdgcn_sched_barrier(0);
@@ -285,9 +308,10 @@ static __device__ __forceinline__ void stream_loop(const CsumArgs &a, u32x4 *sta
 		if (cnch == ~0u) {
 			/* does not fit the stage: the whole wave walks each frame */
 			for (uint32_t i = 0; i < 64; i++) {
-				const uint32_t p = 64u * w + i;
-				if (p >= a.n)
+				const uint64_t p64 = 64ull * grp(w) + i;
+				if (p64 >= a.n)
 					break;
+				const uint32_t p = (uint32_t)p64;
 				const u32x4 di = *((cu32x4 *)(a.desc + p));
 				const Frame f = resolve<false, 2>(a, di, true);
 				uint32_t E = 0, O = 0;
@@ -344,7 +368,7 @@ static __device__ __forceinline__ void stream_loop(const CsumArgs &a, u32x4 *sta
 				}
 			}
 			const uint32_t s = f.odd ? (O << 8) + E : (E << 8) + O;
-			finalize<2>(a, f, 64u * w + lane, s);
+			finalize<2>(a, f, 64u * grp(w) + lane, s);
 		}
 		/* the stage is rewritten next iteration: all reads done first */
 		__builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");

@@ -236,8 +236,37 @@ s26)
   tools/gpu_run.sh s26/sweep4u 300 python tools/sweep.py --config 4 --layout umem --geoms auto --bpc 0 --orders="-1,0;4,4;6,4;5,3;5,5" --rounds 3 --launches 20
   tools/gpu_run.sh s26/sweep2u_ip 300 python tools/sweep.py --config 2 --layout umem --geoms auto --bpc 0 --orders="-1,0;4,4;6,4;5,3;5,5" --flags inplace,iphdr --rounds 3 --launches 20
   ;;
+s27)
+  # stream kernel (config 3): 64-frame groups visited in region order
+  # (XCSUM_STREAM_RLOG / _TLOG variants) vs descriptor order; stream tests
+  # under one variant
+  XCSUM_LIB=libxudp_amd/variants/so3t2/libxcsum.so tools/gpu_run.sh s27/pytest_stream 300 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_fullsize.py tests/test_gpu_offsets.py -m gpu -x -q --timeout 120 --timeout-method thread
+  for r in 1 2; do
+    for v in cur so3t2 so4t0 so5t2; do
+      L=libxudp_amd/libxcsum.so; [ $v = cur ] || L=libxudp_amd/variants/$v/libxcsum.so
+      XCSUM_LIB=$L tools/gpu_run.sh s27/bench_c3_${v}_$r 200 python bench.py --config 3 --steps 100 --warmup 5 --no-cpu-baseline --no-ceiling
+    done
+  done
+  ;;
+s28)
+  # stream kernel group orders, second set
+  for r in 1 2 3; do
+    for v in cur so4t0 so3t0 so4t1 so5t0; do
+      L=libxudp_amd/libxcsum.so; [ $v = cur ] || L=libxudp_amd/variants/$v/libxcsum.so
+      XCSUM_LIB=$L tools/gpu_run.sh s28/bench_c3_${v}_$r 200 python bench.py --config 3 --steps 100 --warmup 5 --no-cpu-baseline --no-ceiling
+    done
+  done
+  ;;
+s29)
+  # the final tree (stream kernel group order on): whole suite, smoke, the
+  # driver's bench, config 3 bench
+  tools/gpu_run.sh s29/pytest_gpu 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread
+  tools/gpu_run.sh s29/smoke 200 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')"
+  tools/gpu_run.sh s29/bench 300 python bench.py --gpus 1 --steps 20 --warmup 5
+  tools/gpu_run.sh s29/bench_c3 200 python bench.py --config 3 --steps 100 --no-cpu-baseline
+  ;;
 *)
-  echo "usage: $0 s3|s4|s5|s6|s7|s8|s10|s11|s12|s13|s14|s15|s16|s17|s18|s19|s20|s21|s22|s23|s24|s25|s26" >&2
+  echo "usage: $0 s3|s4|s5|s6|s7|s8|s10|s11|s12|s13|s14|s15|s16|s17|s18|s19|s20|s21|s22|s23|s24|s25|s26|s27|s28|s29" >&2
   exit 2
   ;;
 esac
