@@ -504,8 +504,10 @@ def main():
                        "family": cfg["family"], "mode": MODE_NAMES[cfg["mode"]],
                        "layout": "packed, 8-byte aligned frames" if args.layout == "packed"
                        else "xudp TX UMEM: one frame per 4096-byte chunk",
-                       "visiting_order": "automatic (region order if the batch is sparse in "
-                                         "the UMEM, else descriptor order)",
+                       "visiting_order": "automatic (32 regions of 16-frame tiles if the batch "
+                                         "is sparse in the UMEM, else the geometry's dense "
+                                         "order: 8 regions of 16-frame tiles at MTU, 16 of "
+                                         "4-frame tiles for mixed sizes)",
                        "rotating_buffers": len(bufs),
                        "alg_bytes_per_step": int(alg_all), "parallelism": f"dp{world}"},
             "pct_hbm_peak": round(100 * achieved / HBM_PEAK_GBS, 2),
