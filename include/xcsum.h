@@ -247,9 +247,16 @@ int xcsum_batch_host(xcsum_ctx *ctx, uint8_t *h_umem, const struct xcsum_desc *h
 		     uint32_t n, uint16_t *h_out, uint32_t mode, uint32_t flags);
 
 /* Page-lock and map a host region (xudp's UMEM, xudp/xsk.c:222-341) for DMA
- * and zero-copy access.  Ownership stays with the caller. */
+ * and zero-copy access.  Ownership stays with the caller.  Unregistering
+ * waits for all work on the context's device first, so the caller may unmap
+ * the region as soon as it returns. */
 int xcsum_register_umem(xcsum_ctx *ctx, void *base, size_t size);
 int xcsum_unregister_umem(xcsum_ctx *ctx, void *base);
+
+/* Number of the context's host-path slots with copies or kernels still in
+ * flight.  Always 0 after xcsum_batch_host / xcsum_rx_host return, on error
+ * returns too: no work of a finished call touches the caller's memory. */
+int xcsum_ctx_pending(xcsum_ctx *ctx);
 
 /* Diagnostics (no reference counterpart): the hipError_t of the last HIP call
  * that made an entry point of this thread return -XCSUM_ERR_HIP (0: none),

@@ -47,15 +47,59 @@ REG_GEOMETRIES = [(64, 1, 2), (64, 1, 9), (32, 1, 3), (32, 1, 6), (16, 1, 2), (1
                   (16, 1, 6), (16, 2, 6), (16, 1, 12), (8, 1, 2), (8, 2, 1), (8, 1, 12),
                   (4, 2, 2), (4, 4, 2), (4, 1, 2), (2, 1, 4), (2, 2, 4), (1, 1, 6), (1, 1, 8),
                   (1, 2, 6)]
-# LDS-DMA staged variant (csum_lds_kernel<K, D>): G = 16, U = 10 + ring depth D
-LDS_GEOMETRIES = [(16, 12, 6), (16, 13, 6), (16, 12, 3), (16, 14, 3)]
 # stream kernel (csum_stream_kernel<KC>): a wave per 64 packed frames, the
 # region they occupy streamed through a KC-KiB LDS stage: G = 64, U = 0, K = KC
 STREAM_GEOMETRIES = [(64, 0, 4), (64, 0, 8), (64, 0, 16)]
-# segmented stream for packed large / mixed frames (A/B, not a default):
-# (64, frames per unit, rows in flight)
+# every geometry libxcsum.so runs (the parity tests sweep them all)
+GEOMETRIES = REG_GEOMETRIES + STREAM_GEOMETRIES
+# A/B kernels outside libxcsum.so (csrc/variants/, `make -C libxudp_amd variant
+# NAME=ab`, loaded with XCSUM_LIB): LDS-DMA staged csum_lds_kernel<K, D>
+# (G = 16, U = 10 + ring depth D) and the segmented stream (64, frames per
+# unit, rows in flight)
+LDS_GEOMETRIES = [(16, 12, 6), (16, 13, 6), (16, 12, 3), (16, 14, 3)]
 SEG_GEOMETRIES = [(64, 64, 4), (64, 64, 8), (64, 16, 4)]
-GEOMETRIES = REG_GEOMETRIES + LDS_GEOMETRIES + STREAM_GEOMETRIES + SEG_GEOMETRIES
+
+
+# bounds-checked debug build (make -C libxudp_amd debug; BoundsSite in
+# csrc/xcsum_internal.h, in order from 1)
+BOUNDS_SITES = ["csum_chunk", "csum_walk", "csum_hdr", "csum_out", "csum_inplace",
+                "stream_region", "stream_stage", "build_src", "build_data", "build_out",
+                "rx_chunk", "rx_rec", "rx_part", "rx_stream", "gen_store"]
+
+
+def debug_build():
+    """True when the loaded library is the bounds-checked debug build."""
+    return hasattr(lib(), "xcsum_debug_bounds")
+
+
+def take_bounds(max_recs=16):
+    """(violations since the last call, [(site, index, addr, lo, hi), ...]);
+    synchronises the device.  Debug build only."""
+    L = lib()
+    fn = L.xcsum_debug_bounds
+    fn.restype = ctypes.c_int
+    fn.argtypes = [ctypes.POINTER(ctypes.c_uint64), ctypes.c_void_p, ctypes.c_int]
+    count = ctypes.c_uint64(0)
+    recs = np.zeros(4 * max_recs, dtype=np.uint64)
+    _check(fn(ctypes.byref(count), recs.ctypes.data, max_recs), "xcsum_debug_bounds")
+    out = []
+    for k in range(min(int(count.value), max_recs)):
+        sid, addr, lo, hi = (int(x) for x in recs[4 * k:4 * k + 4])
+        site = sid >> 32
+        name = BOUNDS_SITES[site - 1] if 1 <= site <= len(BOUNDS_SITES) else str(site)
+        out.append((name, sid & 0xffffffff, addr, lo, hi))
+    return int(count.value), out
+
+
+def variants_built():
+    """True when the loaded library is a variants build (A/B kernels in)."""
+    return hasattr(lib(), "xcsum_variants_built")
+
+
+def variant_geometries():
+    """The A/B geometries the loaded library runs ([] for libxcsum.so)."""
+    return LDS_GEOMETRIES + SEG_GEOMETRIES if variants_built() else []
+
 
 F_BUILD_INPLACE = 0x20
 F_SRC_ALIGNED = 0x40
@@ -113,6 +157,7 @@ _SIGS = {
     "xcsum_register_umem": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t]),
     "xcsum_unregister_umem": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
     "xcsum_sync": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
+    "xcsum_ctx_pending": (ctypes.c_int, [ctypes.c_void_p]),
     "xcsum_last_hip_error": (ctypes.c_int, [ctypes.POINTER(ctypes.c_int),
                                             ctypes.POINTER(ctypes.c_char_p)]),
     "xcsum_gen_layout": (ctypes.c_int, [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
@@ -167,6 +212,12 @@ def _check(rc, what):
             code = lib().xcsum_last_hip_error(ctypes.byref(line), ctypes.byref(name))
             what = f"{what} ({(name.value or b'?').decode()} = {code} at xcsum_api.hip:{line.value})"
         raise XcsumError(rc, what)
+    return rc
+
+
+def _check_nonneg(rc, what):
+    if rc < 0:
+        _check(rc, what)
     return rc
 
 
@@ -308,6 +359,10 @@ class Engine:
 
     def unregister_umem(self, buf):
         _check(lib().xcsum_unregister_umem(self._ctx, _ptr(buf)), "xcsum_unregister_umem")
+
+    def pending(self):
+        """Host-path slots with work still in flight (0 after every host call)."""
+        return _check_nonneg(lib().xcsum_ctx_pending(self._ctx), "xcsum_ctx_pending")
 
     def sync(self, stream=None):
         _check(lib().xcsum_sync(self._ctx, _ptr(stream)), "xcsum_sync")

@@ -30,6 +30,7 @@
  * slots) runs the frame-group kernel (checked once per launch, dense_batch).
  */
 #include "xcsum_csum.h"
+#include "xcsum_variants.h"
 
 namespace xcsum {
 

@@ -37,6 +37,46 @@ extern "C" int xcsum_last_hip_error(int *line, const char **name)
 	return t_hip_err;
 }
 
+#ifdef XCSUM_DEBUG_BOUNDS
+namespace xcsum {
+BoundsReader *&bounds_readers()
+{
+	static BoundsReader *head = nullptr;
+	return head;
+}
+} /* namespace xcsum */
+
+/* Debug build only (make -C libxudp_amd debug): synchronise the device, then
+ * collect and clear the bounds-violation logs of every kernel translation
+ * unit.  *count = violations since the last call; recs (may be null) gets up
+ * to max_recs records of 4 u64 each: {site << 32 | index, addr, lo, hi}. */
+extern "C" int xcsum_debug_bounds(uint64_t *count, uint64_t *recs, int max_recs)
+{
+	if (!count)
+		return -XCSUM_ERR_INVAL;
+	if (hipDeviceSynchronize() != hipSuccess)
+		return -XCSUM_ERR_HIP;
+	uint64_t total = 0;
+	int k = 0;
+	for (BoundsReader *r = bounds_readers(); r; r = r->next) {
+		BoundsLog log;
+		if (r->take(&log))
+			return -XCSUM_ERR_HIP;
+		total += log.count;
+		for (unsigned i = 0; i < log.count && i < (unsigned)BOUNDS_RECS; i++, k++) {
+			if (!recs || k >= max_recs)
+				continue;
+			recs[4 * k] = ((uint64_t)log.rec[i].site << 32) | log.rec[i].index;
+			recs[4 * k + 1] = log.rec[i].addr;
+			recs[4 * k + 2] = log.rec[i].lo;
+			recs[4 * k + 3] = log.rec[i].hi;
+		}
+	}
+	*count = total;
+	return 0;
+}
+#endif
+
 /* $XCSUM_GEOMETRY="G,U,K" forces a geometry for every new context (sweeps) */
 static Geometry env_geometry()
 {
@@ -201,11 +241,6 @@ extern "C" int xcsum_ctx_take_errors(xcsum_ctx *c, uint64_t *count)
  * (Round 1 measured forced region orders 1-4 % slower on packed frames,
  * with the kernel of that time.)  Other geometries keep descriptor order
  * for dense batches. */
-/* XCSUM_DENSE_ORDER=0 builds descriptor order for dense batches (A/B only) */
-#ifndef XCSUM_DENSE_ORDER
-#define XCSUM_DENSE_ORDER 1
-#endif
-
 static void set_order(const xcsum_ctx *c, CsumArgs &a, const Geometry &g)
 {
 	if (c->order_rlog >= 0) {
@@ -214,17 +249,20 @@ static void set_order(const xcsum_ctx *c, CsumArgs &a, const Geometry &g)
 		return;
 	}
 	a.ord = order_regions(a.n, 5, 4);
-	a.ord.sparse_only = a.ord.rshift != 0;
-	if (XCSUM_DENSE_ORDER && g.G == 16 && g.U == 2 && g.K == 6)
+	if (g.G == 16 && g.U == 2 && g.K == 6)
 		a.dense = order_regions(a.n, 3, 4);
-	else if (XCSUM_DENSE_ORDER && g.G == 16 && g.U == 1 && (g.K == 2 || g.K == 3))
+	else if (g.G == 16 && g.U == 1 && (g.K == 2 || g.K == 3))
 		a.dense = order_regions(a.n, 5, 4);   /* 400 / 700-byte payloads:
 							 0.0888 -> 0.0842 ms,
 							 0.1408 -> 0.1343 ms (s24) */
-	else if (XCSUM_DENSE_ORDER && g.G == 64 && g.U == 1)
+	else if (g.G == 64 && g.U == 1)
 		a.dense = order_regions(a.n, 4, 2);
 	else
 		a.dense = order_identity(a.n);
+	/* resolved in the kernel whenever either order is not the identity: a
+	 * batch of 128-511 frames is too small for 32 regions of 16-frame
+	 * tiles but still gets its dense order */
+	a.ord.sparse_only = a.ord.rshift != 0 || a.dense.rshift != 0;
 }
 
 static Geometry geometry_for(const xcsum_ctx *c, uint32_t len_hint, uint32_t flags)
@@ -445,6 +483,10 @@ extern "C" int xcsum_unregister_umem(xcsum_ctx *c, void *base)
 	for (size_t i = 0; i < c->regions.size(); i++) {
 		if (c->regions[i].host == (uint8_t *)base) {
 			HIPCHK(hipSetDevice(c->device));
+			/* no kernel or copy may still read or write the region once
+			 * it is unmapped: this context's host-path streams and any
+			 * stream a caller launched on its device alias */
+			(void)hipDeviceSynchronize();
 			(void)hipHostUnregister(base);
 			c->regions.erase(c->regions.begin() + i);
 			return 0;
@@ -477,20 +519,10 @@ static const Region *find_region(const xcsum_ctx *c, const uint8_t *lo, const ui
 static constexpr uint64_t DIRECT_MAX = XCSUM_DIRECT_MAX;
 static constexpr bool DIRECT_ON = DIRECT_MAX != 0;
 
-/* XCSUM_SPIN_WAIT=1: wait for a slot by polling its event (A/B only;
- * measured no faster than hipEventSynchronize) */
-#ifndef XCSUM_SPIN_WAIT
-#define XCSUM_SPIN_WAIT 0
-#endif
-
+/* a slot's completion (polling the event instead measured no faster,
+ * profiles/r02/session2/host_direct) */
 static hipError_t wait_slot(hipEvent_t e)
 {
-	if (XCSUM_SPIN_WAIT) {
-		hipError_t r;
-		while ((r = hipEventQuery(e)) == hipErrorNotReady)
-			;
-		return r;
-	}
 	return hipEventSynchronize(e);
 }
 
@@ -553,15 +585,11 @@ static int ensure_gather(xcsum_ctx *c)
  * profiles/r02/session2/rx_gather/): 64-byte frames 23.3 -> 6.9 ms per
  * 256K-frame receive batch; MTU frames 22.7 -> 33.6 ms (the single-thread
  * memcpy of 1.5 KB frames loses to the runtime's pipelined pageable copy of
- * the whole range), hence the 1/8.  XCSUM_RX_GATHER=0 builds the range copy
- * everywhere (A/B only). */
-#ifndef XCSUM_RX_GATHER
-#define XCSUM_RX_GATHER 1
-#endif
+ * the whole range), hence the 1/8. */
 static bool gather_pays(const xcsum_ctx *c, const uint8_t *h_umem, uint64_t lo, uint64_t hi,
 			uint64_t frame_bytes)
 {
-	return XCSUM_RX_GATHER && hi - lo > 8 * frame_bytes + 4096 &&
+	return hi - lo > 8 * frame_bytes + 4096 &&
 	       !find_region(c, h_umem + lo, h_umem + hi);
 }
 
@@ -582,7 +610,7 @@ static const Region *zerocopy_pays(const xcsum_ctx *c, const uint8_t *h_umem,
 		if (h_desc[i].addr + h_desc[i].len > hi) hi = h_desc[i].addr + h_desc[i].len;
 		sum += h_desc[i].len;
 	}
-	if (!XCSUM_RX_GATHER || n == 0 || hi - lo <= 2 * sum + 4096)
+	if (n == 0 || hi - lo <= 2 * sum + 4096)
 		return nullptr;
 	return find_region(c, h_umem + lo, h_umem + hi);
 }
@@ -644,10 +672,35 @@ static void retire(const Pending &pd, const uint16_t *h_res, uint8_t *h_umem,
 	}
 }
 
-namespace xcsum {
+/* Wait for everything the host path queued on the context's streams.  Every
+ * host entry point calls it before an error return: a slot still in flight
+ * reads the caller's UMEM (registered, or pinned in place by the copy) or the
+ * pinned stage, and writes the pinned result slot -- the caller may unmap
+ * the UMEM, and the next call reuses the slots, as soon as we return.
+ * Errors are ignored: the caller already gets the first one. */
+static void drain_slots(xcsum_ctx *c)
+{
+	for (int s = 0; s < Ctx::NSLOT; s++)
+		if (c->streams[s])
+			(void)hipStreamSynchronize(c->streams[s]);
+}
 
-int batch_host_impl(xcsum_ctx *c, uint8_t *h_umem, const struct xcsum_desc *h_desc, uint32_t n,
-		    uint16_t *h_out, uint16_t *h_out_ip, uint32_t mode, uint32_t flags, bool gather)
+extern "C" int xcsum_ctx_pending(xcsum_ctx *c)
+{
+	if (!c)
+		return -XCSUM_ERR_INVAL;
+	if (hipSetDevice(c->device) != hipSuccess)
+		return -XCSUM_ERR_HIP;
+	int busy = 0;
+	for (int s = 0; s < Ctx::NSLOT; s++)
+		if (c->streams[s] && hipStreamQuery(c->streams[s]) == hipErrorNotReady)
+			busy++;
+	return busy;
+}
+
+static int batch_host_run(xcsum_ctx *c, uint8_t *h_umem, const struct xcsum_desc *h_desc,
+			  uint32_t n, uint16_t *h_out, uint16_t *h_out_ip, uint32_t mode,
+			  uint32_t flags, bool gather)
 {
 	if (!c || mode > XCSUM_MODE_AUTO)
 		return -XCSUM_ERR_INVAL;
@@ -804,6 +857,17 @@ int batch_host_impl(xcsum_ctx *c, uint8_t *h_umem, const struct xcsum_desc *h_de
 	return 0;
 }
 
+namespace xcsum {
+
+int batch_host_impl(xcsum_ctx *c, uint8_t *h_umem, const struct xcsum_desc *h_desc, uint32_t n,
+		    uint16_t *h_out, uint16_t *h_out_ip, uint32_t mode, uint32_t flags, bool gather)
+{
+	const int rc = batch_host_run(c, h_umem, h_desc, n, h_out, h_out_ip, mode, flags, gather);
+	if (rc && c)
+		drain_slots(c);
+	return rc;
+}
+
 } /* namespace xcsum */
 
 extern "C" int xcsum_batch_host(xcsum_ctx *c, uint8_t *h_umem, const struct xcsum_desc *h_desc,
@@ -839,9 +903,21 @@ extern "C" int xcsum_batch_host(xcsum_ctx *c, uint8_t *h_umem, const struct xcsu
  *     pinned records in place (no copies).  The kernel then sees staged
  *     offsets: `frame` and `body` are moved back to UMEM offsets on the host
  *     as the records are collected. */
+static int rx_host_run(xcsum_ctx *c, const uint8_t *h_umem, const struct xcsum_desc *h_desc,
+		       uint32_t n, struct xcsum_rx_msg *h_msgs, uint32_t *h_count, uint32_t flags);
+
 extern "C" int xcsum_rx_host(xcsum_ctx *c, const uint8_t *h_umem, const struct xcsum_desc *h_desc,
 			     uint32_t n, struct xcsum_rx_msg *h_msgs, uint32_t *h_count,
 			     uint32_t flags)
+{
+	const int rc = rx_host_run(c, h_umem, h_desc, n, h_msgs, h_count, flags);
+	if (rc && c)
+		drain_slots(c);   /* see batch_host_impl */
+	return rc;
+}
+
+static int rx_host_run(xcsum_ctx *c, const uint8_t *h_umem, const struct xcsum_desc *h_desc,
+		       uint32_t n, struct xcsum_rx_msg *h_msgs, uint32_t *h_count, uint32_t flags)
 {
 	if (!c)
 		return -XCSUM_ERR_INVAL;

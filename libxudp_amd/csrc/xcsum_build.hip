@@ -47,6 +47,10 @@ struct Msg {
 	uint64_t data_off;      /* umem offset of data */
 	uint32_t len, sh;
 	bool ok, present;
+#ifdef XCSUM_DEBUG_BOUNDS
+	const uint8_t *slot, *slot_end;   /* the frame slot: every store stays inside */
+	const uint8_t *blk_end;           /* src rounded up to 16 past the payload */
+#endif
 };
 
 static __device__ __forceinline__ Msg resolve_msg(const BuildArgs &a, u32x4 m, bool present,
@@ -65,6 +69,11 @@ static __device__ __forceinline__ Msg resolve_msg(const BuildArgs &a, u32x4 m, b
 	g.blk = (const uint8_t *)((uintptr_t)src & ~(uintptr_t)15);
 	if (!g.ok)
 		g.len = 0;
+#ifdef XCSUM_DEBUG_BOUNDS
+	g.slot = a.umem + (uint64_t)m.w * a.frame_size;
+	g.slot_end = g.slot + a.frame_size;
+	g.blk_end = (const uint8_t *)(((uintptr_t)src + g.len + 15u) & ~(uintptr_t)15);
+#endif
 	return g;
 }
 
@@ -83,10 +92,14 @@ static __device__ __forceinline__ void issue_blocks(const Msg &g, uint32_t lane,
 #pragma unroll
 	for (int k = 0; k < K; k++) {
 		const uint32_t off = 16u * (lane + k * G);
-		v[k] = ld16(off < end ? g.blk + off : zero);
+		v[k] = ld16(off < end ? XB_LOAD(g.blk + off, 16, g.blk, g.blk_end, XB_BUILD_SRC, off, zero)
+				      : zero);
 	}
 	if (TWO)
-		vx = ld16(lane == 0 && 16u * K * G < end ? g.blk + 16u * K * G : zero);
+		vx = ld16(lane == 0 && 16u * K * G < end
+				  ? XB_LOAD(g.blk + 16u * K * G, 16, g.blk, g.blk_end, XB_BUILD_SRC,
+					    16u * K * G, zero)
+				  : zero);
 }
 
 /* a where the lane's bit of `lanes` is clear, b where it is set: v_cndmask
@@ -182,7 +195,7 @@ static __device__ __forceinline__ void finish_frame(const BuildArgs &a, const Ms
 						    uint32_t ipconst)
 {
 	if (!g.ok) {
-		if (lane == 0) {
+		if (lane == 0 && XB_IDX(p, a.n, XB_BUILD_OUT)) {
 			struct xcsum_desc d0 = {g.data_off, 0u, 0u};
 			a.desc_out[p] = d0;
 			if (a.out)
@@ -224,7 +237,13 @@ static __device__ __forceinline__ void finish_frame(const BuildArgs &a, const Ms
 			w.w = bswap16(ulen) | (ucheck << 16);
 		uint8_t *pb = g.data - 64 + 16 * lane;
 		const uint32_t first = v6 ? 0u : 1u;      /* piece holding header byte 0 */
-		if (lane > first) {
+		/* the header's pieces: [data - hdr, data) */
+		if (lane >= first &&
+		    !XB_STORE(lane > first ? pb : g.data - hdr,
+			      lane > first ? 16u : 16u * (lane + 1) - (64u - hdr), g.slot, g.slot_end,
+			      XB_BUILD_DATA, 64u - 16u * lane)) {
+			/* outside the slot: not written (debug build only) */
+		} else if (lane > first) {
 			*reinterpret_cast<u32x4 *>(pb) = w;
 		} else if (lane == first) {
 			if (v6) {                          /* bytes 2..15 */
@@ -237,7 +256,7 @@ static __device__ __forceinline__ void finish_frame(const BuildArgs &a, const Ms
 			*reinterpret_cast<u32x2 *>(pb + 8) = u32x2{w.z, w.w};
 		}
 	}
-	if (lane == 0) {
+	if (lane == 0 && XB_IDX(p, a.n, XB_BUILD_OUT)) {
 		struct xcsum_desc d0 = {g.data_off - hdr, hdr + g.len, 0u};
 		a.desc_out[p] = d0;
 		if (a.out)
@@ -270,8 +289,12 @@ static __device__ __forceinline__ void build_msg(const BuildArgs &a, const Msg &
 	if (__builtin_amdgcn_ballot_w64(gc.len > 16u * K * G)) {
 		/* jumbo payloads: plain walk (own copy of the body) */
 		for (uint32_t off = 16u * lane; off < gc.len; off += 16u * G) {
-			u32x4 v = load_payload(gc.blk, gc.sh, off, gc.len - off);
-			if (!inplace)
+			u32x4 v = XB_IN(gc.blk + off, (gc.sh && 16u - gc.sh < gc.len - off) ? 32u : 16u,
+					gc.blk, gc.blk_end, XB_BUILD_SRC, off)
+					  ? load_payload(gc.blk, gc.sh, off, gc.len - off)
+					  : u32x4{0u, 0u, 0u, 0u};
+			if (!inplace && XB_STORE(gc.data + off, gc.len - off < 16u ? gc.len - off : 16u,
+						 gc.slot, gc.slot_end, XB_BUILD_DATA, off))
 				store_payload(gc.data + off, v, gc.len - off);
 			accum(v, E, O);
 		}
@@ -300,7 +323,8 @@ static __device__ __forceinline__ void build_msg(const BuildArgs &a, const Msg &
 					   __builtin_amdgcn_alignbyte(d3, d2, s8),
 					   __builtin_amdgcn_alignbyte(d4, d3, s8)};
 				v = shift_chunk(v, v, 0u, gc.len - off);     /* clear past the end */
-				if (!inplace)
+				if (!inplace && XB_STORE(gc.data + off, gc.len - off < 16u ? gc.len - off : 16u,
+							 gc.slot, gc.slot_end, XB_BUILD_DATA, off))
 					store_payload(gc.data + off, v, gc.len - off);
 				accum(v, E, O);
 			}
@@ -311,7 +335,8 @@ static __device__ __forceinline__ void build_msg(const BuildArgs &a, const Msg &
 			uint32_t off = 16u * (lane + k * G);
 			if (off < gc.len) {
 				u32x4 v = shift_chunk(vc[k], vc[k], 0u, gc.len - off);
-				if (!inplace)
+				if (!inplace && XB_STORE(gc.data + off, gc.len - off < 16u ? gc.len - off : 16u,
+							 gc.slot, gc.slot_end, XB_BUILD_DATA, off))
 					store_payload(gc.data + off, v, gc.len - off);
 				accum(v, E, O);
 			}

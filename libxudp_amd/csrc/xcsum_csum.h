@@ -78,8 +78,16 @@ static __device__ __forceinline__ Frame resolve(const CsumArgs &a, u32x4 d, bool
 	uint32_t len = d.z;
 	int mode = (int)a.mode;
 	f.eth = a.umem + addr;
+#ifdef XCSUM_DEBUG_BOUNDS
+	f.lim = (const uint8_t *)(((uintptr_t)f.eth + len + 15u) & ~(uintptr_t)15);
+	f.dlen = len;
+#endif
 	if (present && mode == XCSUM_MODE_AUTO) {
-		uint32_t proto = ((uint32_t)f.eth[12] << 8) | f.eth[13];
+		/* h_proto only inside the frame: a descriptor shorter than the
+		 * Ethernet header is malformed whatever its next bytes hold */
+		uint32_t proto = 0;
+		if (len >= 14 && XB_IN(f.eth + 12, 2, f.eth, f.eth + len, XB_CSUM_HDR, 12))
+			proto = ((uint32_t)f.eth[12] << 8) | f.eth[13];
 		mode = proto == 0x0800u ? ((a.flags & XCSUM_F_V4_RFC) ? 1 : 0)
 		     : proto == 0x86DDu ? 2 : -1;
 	}
@@ -111,8 +119,12 @@ static __device__ __forceinline__ Frame resolve(const CsumArgs &a, u32x4 d, bool
 		 * them apart cost every mode 20 %: it coarsened the waitcnts. */
 		const uint8_t *z = (const uint8_t *)g_zero_chunk;
 		const uint32_t lo = mode == 2 ? 58u : 38u;
-		f.ul = *(const uint16_t *)(f.nchunks ? f.eth + lo : z);
-		f.ck = *(const uint16_t *)(f.nchunks ? f.eth + lo + 2 : z + 8);
+		f.ul = *(const uint16_t *)(f.nchunks ? XB_LOAD(f.eth + lo, 2, f.eth, f.eth + len,
+								XB_CSUM_HDR, lo, z)
+						     : z);
+		f.ck = *(const uint16_t *)(f.nchunks ? XB_LOAD(f.eth + lo + 2, 2, f.eth, f.eth + len,
+								XB_CSUM_HDR, lo + 2, z + 8)
+						     : z + 8);
 	}
 	/* IPHDR: the IPv4 header too (six dwords, same reasoning) */
 	if (FEAT == 2 && (a.flags & XCSUM_F_IPHDR)) {
@@ -120,6 +132,9 @@ static __device__ __forceinline__ Frame resolve(const CsumArgs &a, u32x4 d, bool
 							   : (const uint8_t *)g_zero_chunk;
 		f.ihs = (uint32_t)(uintptr_t)ih & 3u;
 		const uint32_t *w = (const uint32_t *)((uintptr_t)ih & ~(uintptr_t)3);
+		if (ih != (const uint8_t *)g_zero_chunk &&
+		    !XB_IN(w, 24, (uintptr_t)f.eth & ~(uintptr_t)3, f.lim, XB_CSUM_HDR, 14))
+			w = (const uint32_t *)g_zero_chunk;
 #pragma unroll
 		for (int j = 0; j < 6; j++)
 			f.ih[j] = w[j];
@@ -227,12 +242,12 @@ static __device__ __forceinline__ void finalize(const CsumArgs &a, const Frame &
 			wire = bswap16(r);
 			if ((a.flags & XCSUM_F_IPHDR) && f.mode != 2) {
 				uint16_t ipr = ip_header_csum<FEAT == 2>(f, true);
-				if (a.out_ip)
+				if (a.out_ip && XB_IDX(p, a.n, XB_CSUM_OUT))
 					st_res(a.out_ip + p, ipr);
 				if (wire == 0)
 					wire = ipr;  /* 0 only if both verify */
 			}
-			if (a.out)
+			if (a.out && XB_IDX(p, a.n, XB_CSUM_OUT))
 				st_res(a.out + p, wire);
 			return;
 		}
@@ -247,13 +262,18 @@ static __device__ __forceinline__ void finalize(const CsumArgs &a, const Frame &
 				r = 0xffffu; /* CSUM_MANGLED_0, packet.c:23, :115-116 */
 		}
 		wire = bswap16(r);
-		if (a.flags & XCSUM_F_INPLACE)
+		/* frame end: eth + hdr + udp_len (udp_len is not re-cut without VERIFY) */
+		const uint8_t *fend = f.eth + (f.mode == 2 ? 54u : 34u) + f.udp_len;
+		(void)fend;
+		if ((a.flags & XCSUM_F_INPLACE) &&
+		    XB_STORE(f.eth + (f.mode == 2 ? 60 : 40), 2, f.eth, fend, XB_CSUM_INPLACE, p))
 			store_u16(f.eth + (f.mode == 2 ? 60 : 40), wire);
 		if ((a.flags & XCSUM_F_IPHDR) && f.mode != 2) {
 			uint16_t ipc = ip_header_csum<FEAT == 2>(f, false);
-			if (a.flags & XCSUM_F_INPLACE)
+			if ((a.flags & XCSUM_F_INPLACE) &&
+			    XB_STORE(f.eth + 24, 2, f.eth, fend, XB_CSUM_INPLACE, p))
 				store_u16(f.eth + 24, ipc);
-			if (a.out_ip)
+			if (a.out_ip && XB_IDX(p, a.n, XB_CSUM_OUT))
 				st_res(a.out_ip + p, ipc);
 		}
 	} else {
@@ -262,9 +282,10 @@ static __device__ __forceinline__ void finalize(const CsumArgs &a, const Frame &
 		if (a.flags & XCSUM_F_VERIFY)
 			wire = 0xffffu;  /* a malformed frame never verifies */
 	}
-	if (a.out)
+	if (a.out && XB_IDX(p, a.n, XB_CSUM_OUT))
 		st_res(a.out + p, wire);
-	if (a.out_ip && !((a.flags & XCSUM_F_IPHDR) && f.mode >= 0 && f.mode != 2))
+	if (a.out_ip && !((a.flags & XCSUM_F_IPHDR) && f.mode >= 0 && f.mode != 2) &&
+	    XB_IDX(p, a.n, XB_CSUM_OUT))
 		st_res(a.out_ip + p, (uint16_t)0);
 }
 
@@ -294,12 +315,6 @@ static __device__ __forceinline__ void consume(const CsumArgs &a, const Frame (&
 			finalize<FEAT>(a, f, fidx<ORD>(a, p0 + u * nseg), s);
 	}
 }
-
-/* XCSUM_PINGPONG=0 builds the previous loop shape (A/B only): "next" copied
- * into "current" at the loop latch */
-#ifndef XCSUM_PINGPONG
-#define XCSUM_PINGPONG 1
-#endif
 
 /* wave-uniform split: the jumbo path lives in its own copy of the body, so
  * its drains never merge into the common path's vmcnt bookkeeping */
@@ -361,7 +376,6 @@ static __device__ __forceinline__ void csum_loop(const CsumArgs &a)
 	__builtin_amdgcn_sched_barrier(0);
 	issue<G, U, K>(fa, lane, va);
 
-#if XCSUM_PINGPONG
 	Frame fb[U];
 	u32x4 vb[U][K];
 	for (uint32_t p0 = seg; p0 < limit; p0 += 2 * step) {
@@ -386,28 +400,6 @@ static __device__ __forceinline__ void csum_loop(const CsumArgs &a)
 		issue<G, U, K>(fa, lane, va);
 		consume_any<G, U, K, ORD, FEAT>(a, fb, vb, lane, p0 + step, nseg);
 	}
-#else
-	for (uint32_t p0 = seg; p0 < limit; p0 += step) {
-		Frame fn[U];
-		u32x4 vn[U][K];
-#pragma unroll
-		for (int u = 0; u < U; u++)
-			fn[u] = resolve<Grid<G, K>::DW, FEAT>(a, d[u], has(p0 + step + u * nseg));
-#pragma unroll
-		for (int u = 0; u < U; u++)
-			d[u] = load_desc<G == 64>(a, fidx<ORD>(a, p0 + 2 * step + u * nseg));
-		__builtin_amdgcn_sched_barrier(0);
-		issue<G, U, K>(fn, lane, vn);
-		consume_any<G, U, K, ORD, FEAT>(a, fa, va, lane, p0, nseg);
-#pragma unroll
-		for (int u = 0; u < U; u++) {
-			fa[u] = fn[u];
-#pragma unroll
-			for (int k = 0; k < K; k++)
-				va[u][k] = vn[u][k];
-		}
-	}
-#endif
 }
 
 /* The identity order gets its own copy of the loop, so descriptor-order

@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <atomic>
+#include "xcsum_internal.h"
 
 namespace xcsum {
 
@@ -59,6 +60,67 @@ static __device__ __forceinline__ uint32_t seg_sum(uint32_t v)
 	}
 	return v;
 }
+
+/* ---- bounds checks (XCSUM_DEBUG_BOUNDS only; see xcsum_internal.h) ----
+ * XB_IN(p, n, lo, hi, site, index): is [p, p + n) inside [lo, hi)?  Records
+ * a violation when not.  XB_LOAD(...) yields p, or `safe` (a zero block) for
+ * an access outside; XB_STORE(...) says whether to store; XB_IDX(i, n, site)
+ * checks an array index.  Without the debug build: p / true, no code. */
+#ifdef XCSUM_DEBUG_BOUNDS
+static __device__ BoundsLog g_bounds;
+
+static __device__ __noinline__ void bounds_fail(uint32_t site, uint32_t index, uint64_t addr,
+						 uint64_t lo, uint64_t hi)
+{
+	const unsigned long long k = atomicAdd(&g_bounds.count, 1ull);
+	if (k < (unsigned long long)BOUNDS_RECS) {
+		BoundsRec r;
+		r.site = site;
+		r.index = index;
+		r.addr = addr;
+		r.lo = lo;
+		r.hi = hi;
+		g_bounds.rec[k] = r;
+	}
+}
+
+static __device__ __forceinline__ bool xb_in(uint64_t a, uint64_t n, uint64_t lo, uint64_t hi,
+					     uint32_t site, uint32_t index)
+{
+	if (a >= lo && a + n <= hi)
+		return true;
+	bounds_fail(site, index, a, lo, hi);
+	return false;
+}
+
+#define XB_IN(p, n, lo, hi, site, index)                                                   \
+	xb_in((uint64_t)(uintptr_t)(p), (uint64_t)(n), (uint64_t)(uintptr_t)(lo),          \
+	      (uint64_t)(uintptr_t)(hi), (site), (uint32_t)(index))
+#define XB_LOAD(p, n, lo, hi, site, index, safe)                                           \
+	(XB_IN((p), (n), (lo), (hi), (site), (index)) ? (const uint8_t *)(p)               \
+						      : (const uint8_t *)(safe))
+#define XB_STORE(p, n, lo, hi, site, index) XB_IN((p), (n), (lo), (hi), (site), (index))
+#define XB_IDX(i, n, site) xb_in((uint64_t)(i), 1, 0, (uint64_t)(n), (site), (uint32_t)(i))
+
+/* this translation unit's log, read and cleared by xcsum_debug_bounds() */
+static int bounds_take_tu(BoundsLog *out)
+{
+	BoundsLog z = {};
+	if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_bounds), sizeof(*out), 0,
+				hipMemcpyDeviceToHost) != hipSuccess)
+		return -1;
+	return hipMemcpyToSymbol(HIP_SYMBOL(g_bounds), &z, sizeof(z), 0, hipMemcpyHostToDevice) ==
+			       hipSuccess ? 0 : -1;
+}
+static BoundsReader g_bounds_reader = {bounds_take_tu, nullptr};
+__attribute__((unused)) static const int g_bounds_registered =
+	(g_bounds_reader.next = bounds_readers(), bounds_readers() = &g_bounds_reader, 0);
+#else
+#define XB_IN(p, n, lo, hi, site, index) true
+#define XB_LOAD(p, n, lo, hi, site, index, safe) (p)
+#define XB_STORE(p, n, lo, hi, site, index) true
+#define XB_IDX(i, n, site) true
+#endif
 
 /* low 16 bits byte-swapped (host <-> network order of a 16-bit field) */
 static __device__ __forceinline__ uint32_t bswap16(uint32_t x)

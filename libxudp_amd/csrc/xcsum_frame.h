@@ -38,22 +38,21 @@ struct Frame {
 	uint32_t ih[6];         /* IPHDR: the dwords holding the IPv4 header
 				   [eth+14, eth+34), loaded a step ahead */
 	uint32_t ihs;           /* byte phase of eth+14 in ih[0] */
+#ifdef XCSUM_DEBUG_BOUNDS
+	const uint8_t *lim;     /* the frame's end rounded up to 16 bytes: no
+				   load may reach past it (nor before eth) */
+	uint32_t dlen;          /* descriptor length: stores stay below eth + dlen */
+#endif
 };
 
 /* 16 zero bytes: lanes past the end of their frame load these, so the
  * accumulation needs no data masking (one select per chunk) */
 __device__ u32x4 g_zero_chunk[4];
 
-/* XCSUM_NT=0 builds a variant with default-policy chunk loads (A/B only) */
-#ifndef XCSUM_NT
-#define XCSUM_NT 1
-#endif
-
+/* chunk loads are nontemporal: every byte is read exactly once */
 static __device__ __forceinline__ u32x4 load_chunk(const uint8_t *p)
 {
-	if (XCSUM_NT)
-		return __builtin_nontemporal_load((gu32x4 *)p);
-	return *((gu32x4 *)p);
+	return __builtin_nontemporal_load((gu32x4 *)p);
 }
 
 typedef __attribute__((address_space(4))) const u32x4 cu32x4;
@@ -227,7 +226,8 @@ static __device__ __forceinline__ void sum_walk(const Frame &f, uint32_t lane, u
 						uint32_t &O)
 {
 	for (uint32_t c = lane; c < f.nchunks; c += G) {
-		u32x4 v = load_chunk(f.base + 16u * c);
+		u32x4 v = load_chunk(XB_LOAD(f.base + 16u * c, 16, f.eth, f.lim, XB_CSUM_WALK, c,
+					     g_zero_chunk));
 		if (DW) {
 			accum(edge_mask_one(f, c, v), E, O);
 		} else {
@@ -238,30 +238,20 @@ static __device__ __forceinline__ void sum_walk(const Frame &f, uint32_t lane, u
 }
 
 /* the chunk grid a geometry uses (measured, see the Frame comment) */
-/* XCSUM_GRID_DW=1 builds a variant with the dword grid everywhere (A/B only) */
-#ifndef XCSUM_GRID_DW
-#define XCSUM_GRID_DW 0
-#endif
 template <int G, int K>
 struct Grid {
-	static constexpr bool DW = XCSUM_GRID_DW || (!(G == 16 && K >= 6) && !(G == 8 && K >= 12));
+	static constexpr bool DW = !(G == 16 && K >= 6) && !(G == 8 && K >= 12);
 };
 
-/* XCSUM_NT_STORE=1 builds a variant whose result and in-place stores are
- * nontemporal (A/B only) */
-#ifndef XCSUM_NT_STORE
-#define XCSUM_NT_STORE 0
-#endif
-
+/* Result and in-place stores are plain (temporal): nontemporal 2-byte stores
+ * each became a partial write, config 2 +12 % (profiles/r02) */
 template <typename T>
 static __device__ __forceinline__ void st_res(T *p, T v)
 {
-	if (XCSUM_NT_STORE)
-		__builtin_nontemporal_store(v, p);
-	else
-		*p = v;
+	*p = v;
 }
 
+/* a 2-byte check field of the frame (in-place writes) */
 static __device__ __forceinline__ void store_u16(uint8_t *p, uint16_t v)
 {
 	if (((uintptr_t)p & 1) == 0) {
@@ -271,12 +261,6 @@ static __device__ __forceinline__ void store_u16(uint8_t *p, uint16_t v)
 		st_res(p + 1, (uint8_t)(v >> 8));
 	}
 }
-
-/* XCSUM_EDGE_T=1 builds a variant whose first chunk row of each frame is
- * loaded with the default (temporal) policy at G = 64 (A/B only) */
-#ifndef XCSUM_EDGE_T
-#define XCSUM_EDGE_T 0
-#endif
 
 template <int G, int U, int K>
 static __device__ __forceinline__ void issue(const Frame (&f)[U], uint32_t lane,
@@ -288,11 +272,9 @@ static __device__ __forceinline__ void issue(const Frame (&f)[U], uint32_t lane,
 #pragma unroll
 		for (int k = 0; k < K; k++) {
 			uint32_t c = lane + k * G;
-			const uint8_t *p = c < f[u].nchunks ? f[u].base + 16u * c : zero;
-			if (XCSUM_EDGE_T && G == 64 && k == 0)
-				v[u][k] = *((gu32x4 *)p);
-			else
-				v[u][k] = load_chunk(p);
+			v[u][k] = load_chunk(c < f[u].nchunks ? XB_LOAD(f[u].base + 16u * c, 16, f[u].eth,
+									f[u].lim, XB_CSUM_CHUNK, c, zero)
+							      : zero);
 		}
 }
 

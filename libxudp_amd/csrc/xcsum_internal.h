@@ -47,6 +47,52 @@ static __device__ __forceinline__ uint32_t frame_of(const Order &o, uint32_t p)
 	return ((r * o.q + (t >> o.rshift)) << o.tshift) | (p & ((1u << o.tshift) - 1u));
 }
 
+/* ---- XCSUM_DEBUG_BOUNDS (make -C libxudp_amd debug): device-side bounds
+ * checks.  Every frame load and store of every kernel is tested against the
+ * bytes it may touch (its frame's extent from the descriptor, the stream
+ * region of its 64-frame group, the result arrays' n entries); a violation is
+ * recorded in a per-translation-unit device log (first BOUNDS_RECS kept) and
+ * the access is skipped or redirected to zeros, so the run goes on without
+ * faulting.  xcsum_debug_bounds() collects and clears the logs.  Not in
+ * libxcsum.so: the macros compile to nothing there. */
+enum BoundsSite : uint32_t {
+	XB_CSUM_CHUNK = 1,      /* frame-group kernel: chunk load */
+	XB_CSUM_WALK,           /* jumbo / re-cut walk load */
+	XB_CSUM_HDR,            /* h_proto, udp len/check, IPv4 header loads */
+	XB_CSUM_OUT,            /* out[p] / out_ip[p]: p < n */
+	XB_CSUM_INPLACE,        /* in-place udp->check / iph->check store */
+	XB_STREAM_REGION,       /* stream kernel: region load vs its frames' extent */
+	XB_STREAM_STAGE,        /* stream kernel: LDS stage index */
+	XB_BUILD_SRC,           /* build: payload block load */
+	XB_BUILD_DATA,          /* build: payload / header store vs the frame slot */
+	XB_BUILD_OUT,           /* build: desc_out[p] / out[p]: p < n */
+	XB_RX_CHUNK,            /* receive: frame chunk load */
+	XB_RX_REC,              /* receive: record store, p < n */
+	XB_RX_PART,             /* receive: per-block count slot */
+	XB_RX_STREAM,           /* receive stream kernel: region load */
+	XB_GEN_STORE,           /* synthetic fill: store vs the frame */
+	XB_SITE_COUNT
+};
+
+#ifdef XCSUM_DEBUG_BOUNDS
+struct BoundsRec {
+	uint32_t site, index;
+	uint64_t addr, lo, hi;  /* the access [addr, ...) and the allowed [lo, hi) */
+};
+constexpr int BOUNDS_RECS = 16;
+struct BoundsLog {
+	unsigned long long count;
+	unsigned long long pad;
+	BoundsRec rec[BOUNDS_RECS];
+};
+/* one reader per translation unit with kernels (xcsum_device.h) */
+struct BoundsReader {
+	int (*take)(BoundsLog *out);
+	BoundsReader *next;
+};
+BoundsReader *&bounds_readers();
+#endif
+
 /* Kernel arguments (passed by value). */
 struct CsumArgs {
 	uint8_t *umem;                 /* frame i starts at umem + desc[i].addr - bias */
@@ -103,10 +149,13 @@ struct Geometry {
 	int B; /* 256-thread blocks per CU (0: occupancy limit) */
 };
 
-/* segmented-stream checksum kernel (csrc/xcsum_seg.hip): Geometry{64, F, D},
- * F frames per unit, D rows of 1 KiB in flight per wave */
-#define XCSUM_SEG_GEOMETRIES(X) X(64, 4) X(64, 8) X(16, 4)
-hipError_t launch_seg(const CsumArgs &a, int F, int D, int cus, int bpc, hipStream_t s);
+/* A/B kernels that lost their measurements live outside the product library
+ * (csrc/variants/: the LDS-DMA staged kernel and the segmented stream; built
+ * only by `make variant`).  Weak: null in libxcsum.so, so its
+ * geometry table and dispatch hold the product kernels only. */
+#define XCSUM_VARIANT_HOOK __attribute__((weak, visibility("hidden")))
+XCSUM_VARIANT_HOOK bool variant_supported(Geometry g);
+XCSUM_VARIANT_HOOK hipError_t launch_variant(const CsumArgs &a, Geometry g, int cus, hipStream_t s);
 Geometry pick_geometry(uint32_t len_hint);
 /* gather: stage each frame on its own (pinned host copy, frames packed)
  * instead of copying the UMEM range the chunk's frames span -- for frames

@@ -36,140 +36,6 @@
 #include <stdlib.h>
 
 namespace xcsum {
-/* ---- LDS-staged variant ---------------------------------------------------
- * Same arithmetic, chunks moved by LDS-DMA (gfx950 global_load_lds_dwordx4:
- * per-lane global address, 1 KiB per wave-instruction landing contiguously
- * in LDS) into a D-deep ring of K-slot stages per wave, read back with
- * ds_read_b128.  In-flight chunks hold LDS instead of VGPRs, so a wave keeps
- * D iterations of loads in flight.  G = 16: a wave's 4 frames per iteration
- * are consecutive, so their descriptors come from wave-uniform scalar loads
- * (lgkmcnt) and the vmcnt queue holds only the DMAs -- the wait for stage d
- * is then exactly vmcnt((D-1)*K).  The compiler does not order ds_read after
- * LDS-DMA, so the waits are explicit and fenced with sched_barrier. */
-#define WAIT_VM(n) __builtin_amdgcn_s_waitcnt(((n) & 0xF) | (((n) >> 4) << 14) | 0x70 | 0xF00)
-#define WAIT_LGKM0() __builtin_amdgcn_s_waitcnt(0xC07F)
-
-typedef __attribute__((address_space(3))) void lds_void;
-
-static __device__ __forceinline__ u32x4 load_desc_scalar(const CsumArgs &a, uint32_t p)
-{
-	uint32_t q = p < a.n ? p : a.n - 1;
-	q = __builtin_amdgcn_readfirstlane(q);
-	return *((cu32x4 *)(a.desc + q));
-}
-
-template <int K, int D>
-__global__ void __launch_bounds__(256) csum_lds_kernel(CsumArgs a)
-{
-	constexpr int G = 16;
-	extern __shared__ u32x4 lds_ring[];  /* [4 waves][D][K][64] */
-	const uint32_t wave = threadIdx.x >> 6;
-	const uint32_t lw = threadIdx.x & 63;
-	const uint32_t lane = lw & (G - 1);
-	const uint32_t sub = lw >> 4;                  /* frame of the wave: 0..3 */
-	const uint32_t nwave = gridDim.x * 4;
-	const uint32_t wave_id = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + wave);
-	u32x4 *ring = lds_ring + (size_t)wave * D * K * 64;
-	const uint8_t *zero = (const uint8_t *)g_zero_chunk;
-	/* iteration j of this wave covers frames 4*(wave_id + j*nwave) + 0..3 */
-	auto frame0 = [&](uint32_t j) { return 4u * (wave_id + j * nwave); };
-	auto pick = [&](u32x4 d0, u32x4 d1, u32x4 d2, u32x4 d3) {
-		u32x4 d = d0;
-		d = sub == 1 ? d1 : d;
-		d = sub == 2 ? d2 : d;
-		d = sub == 3 ? d3 : d;
-		return d;
-	};
-	auto resolve_j = [&](uint32_t j) {
-		uint32_t f = frame0(j);
-		u32x4 d = pick(load_desc_scalar(a, f), load_desc_scalar(a, f + 1),
-			       load_desc_scalar(a, f + 2), load_desc_scalar(a, f + 3));
-		return resolve<Grid<G, K>::DW, 2>(a, d, f + sub < a.n);
-	};
-	auto issue_stage = [&](const Frame &f, int slot) {
-#pragma unroll
-		for (int k = 0; k < K; k++) {
-			uint32_t c = lane + k * G;
-			const uint8_t *src = c < f.nchunks ? f.base + 16u * c : zero;
-			__builtin_amdgcn_global_load_lds((gu32x4 *)src,
-							 (lds_void *)(ring + (slot * K + k) * 64), 16, 0,
-							 XCSUM_NT ? 2 : 0);
-		}
-	};
-
-	if (frame0(0) >= a.n)
-		return;
-	Frame fs[D];
-#pragma unroll
-	for (int d = 0; d < D; d++) {
-		fs[d] = resolve_j(d);
-		WAIT_LGKM0();
-		__builtin_amdgcn_sched_barrier(0);
-		issue_stage(fs[d], d);
-	}
-	for (uint32_t j0 = 0; frame0(j0) < a.n; j0 += D) {
-#pragma unroll
-		for (int d = 0; d < D; d++) {
-			const uint32_t j = j0 + d;
-			if (frame0(j) >= a.n)
-				break;
-			/* next frames of this stage (descriptors: scalar loads) */
-			Frame fn = resolve_j(j + D);
-			__builtin_amdgcn_sched_barrier(0);
-			WAIT_VM((D - 1) * K);                  /* stage d has landed */
-			__builtin_amdgcn_sched_barrier(0);
-			u32x4 v[K];
-#pragma unroll
-			for (int k = 0; k < K; k++)
-				v[k] = ring[(d * K + k) * 64 + lw];
-			WAIT_LGKM0();                          /* reads done: slot reusable */
-			__builtin_amdgcn_sched_barrier(0);
-			issue_stage(fn, d);
-			__builtin_amdgcn_sched_barrier(0);
-			const Frame &f = fs[d];
-			uint32_t E = 0, O = 0;
-			if (__builtin_amdgcn_ballot_w64(f.nchunks > K * G))
-				sum_walk<G, Grid<G, K>::DW>(f, lane, E, O);
-			else
-				sum_frame<G, K, 2, Grid<G, K>::DW>(f, v, lane, E, O);
-			uint32_t sum = f.odd ? (O << 8) + E : (E << 8) + O;
-			sum = seg_sum<G>(sum);
-			if (lane == 0 && f.mode != -2)
-				finalize<2>(a, f, frame0(j) + sub, sum);
-			fs[d] = fn;
-		}
-	}
-	WAIT_VM(0);  /* drain the DMAs still in flight before the wave exits */
-}
-
-template <int K, int D>
-static hipError_t launch_lds_t(const CsumArgs &a, int cus, int bpc, hipStream_t s)
-{
-	const size_t lds = (size_t)4 * D * K * 64 * 16;
-	static std::atomic<int> occ_cache[OCC_MAX_DEVICES];
-	const int occ = occupancy_cached(occ_cache, [&] {
-		int nb = 0;
-		(void)hipFuncSetAttribute((const void *)csum_lds_kernel<K, D>,
-					  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-		if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, csum_lds_kernel<K, D>, 256,
-								 lds) != hipSuccess || nb <= 0)
-			nb = 1;
-		return nb;
-	});
-	int per_cu = (bpc > 0 && bpc < occ) ? bpc : occ;
-	uint64_t waves = ((uint64_t)a.n + 3) / 4;
-	uint64_t blocks = (waves + 3) / 4;
-	uint64_t cap = (uint64_t)cus * per_cu;
-	if (blocks > cap)
-		blocks = cap;
-	if (blocks == 0)
-		blocks = 1;
-	(void)hipGetLastError();  /* clear a stale error (e.g. hipErrorNotReady from
-	                           * someone's hipEventQuery) before checking ours */
-	hipLaunchKernelGGL((csum_lds_kernel<K, D>), dim3((unsigned)blocks), dim3(256), lds, s, a);
-	return hipGetLastError();
-}
-
 /* ---- stream kernel: packed batches of small frames -------------------------
  * A wave takes 64 consecutive descriptors (one per lane) and reads the UMEM
  * region their frames occupy -- [min eth, max end) -- as one coalesced stream:
@@ -201,21 +67,6 @@ static __device__ __forceinline__ uint32_t lds_bytes4(const uint8_t *st, uint32_
 	return __builtin_amdgcn_alignbyte(w[1], w[0], o & 3u);
 }
 
-/* XCSUM_STREAM_RLOG / _TLOG (A/B only, off): visit the 64-frame groups of a
- * batch in 2^RLOG regions of 2^TLOG-group tiles instead of descriptor order.
- * Config 3 in the bench, two processes each (profiles/r02/session2/
- * stream_order/): 16 regions of single groups 0.0231 -> 0.0227 ms; 8
- * regions of 4-group tiles 0.0230; 32 regions of 4-group tiles 0.0235.  Not
- * the default: the first full GPU suite with it on hit an illegal address in
- * a test that does not launch this kernel (s29), which was not explained in
- * the round; the 1.7 % was not worth an unexplained fault. */
-#ifndef XCSUM_STREAM_RLOG
-#define XCSUM_STREAM_RLOG 0
-#endif
-#ifndef XCSUM_STREAM_TLOG
-#define XCSUM_STREAM_TLOG 0
-#endif
-
 template <int KC>
 static __device__ __forceinline__ void stream_loop(const CsumArgs &a, u32x4 *stage)
 {
@@ -224,58 +75,72 @@ static __device__ __forceinline__ void stream_loop(const CsumArgs &a, u32x4 *sta
 	const uint8_t *zero = (const uint8_t *)g_zero_chunk;
 	const uint8_t *st8 = (const uint8_t *)stage;
 	const uint32_t ngroups = (uint32_t)(((uint64_t)a.n + 63) >> 6);
-	const Order go = XCSUM_STREAM_RLOG ? order_regions(ngroups, XCSUM_STREAM_RLOG, XCSUM_STREAM_TLOG)
-					   : order_identity(ngroups);
-	/* logical wave-iteration -> group of 64 frames (>= ngroups: none) */
-	auto grp = [&](uint32_t wi) { return wi < go.nlog ? frame_of(go, wi) : ngroups; };
+	/* wave-iteration wi reads group wi: 64 frames in descriptor order */
 	uint32_t w = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
 
 	auto span_of = [&](uint32_t wi, u32x4 d) {
 		StreamSpan sp;
-		const uint64_t p = 64ull * grp(wi) + lane;
+		const uint64_t p = 64ull * wi + lane;
 		sp.present = p < a.n;
 		sp.eth = ((((uint64_t)d.y << 32) | d.x) - a.bias);
 		sp.len = d.z;
 		return sp;
 	};
-	/* Region of a wave-iteration: base (16-aligned UMEM offset) and chunk
+	/* Region of a wave-iteration: base (16-aligned ADDRESS) and chunk
 	 * count, or ~0u when the frames do not fit the stage.  The bounds are
 	 * the first lane's frame start and the last present lane's frame end
 	 * (two readlanes -- a packed batch is in UMEM order); every frame must
-	 * then lie inside them (one ballot), else the wave walks its frames. */
+	 * then lie inside them (one ballot), else the wave walks its frames.
+	 * Aligned as addresses, not as UMEM offsets: with a d_umem that is not
+	 * 16-byte aligned, a region aligned as offsets would end up to 15 bytes
+	 * past the 16-byte block of the last frame byte (another page,
+	 * possibly unmapped), and every load would be misaligned. */
 	auto region = [&](uint32_t wi, const StreamSpan &sp, uint64_t &base, uint32_t &nch) {
-		if (grp(wi) >= ngroups) {   /* a padding slot of the order: no frames */
-			base = 0;
-			nch = 0;
-			return;
-		}
-		const uint64_t rem = a.n - 64ull * grp(wi);
+		const uint64_t rem = a.n - 64ull * wi;
 		const uint32_t last = rem > 64 ? 63u : (uint32_t)rem - 1u;
-		const uint64_t end = sp.eth + sp.len;
+		const uint64_t e = (uint64_t)(uintptr_t)(a.umem + sp.eth);
+		const uint64_t end = e + sp.len;
 		const uint64_t lo =
-			((uint64_t)__builtin_amdgcn_readlane((uint32_t)(sp.eth >> 32), 0) << 32) |
-			(uint32_t)__builtin_amdgcn_readlane((uint32_t)sp.eth, 0);
+			((uint64_t)__builtin_amdgcn_readlane((uint32_t)(e >> 32), 0) << 32) |
+			(uint32_t)__builtin_amdgcn_readlane((uint32_t)e, 0);
 		const uint64_t hi =
 			((uint64_t)__builtin_amdgcn_readlane((uint32_t)(end >> 32), last) << 32) |
 			(uint32_t)__builtin_amdgcn_readlane((uint32_t)end, last);
 		base = lo & ~15ull;
-		const bool out = sp.present && (sp.eth < lo || end > hi);
+		const bool out = sp.present && (e < lo || end > hi);
 		nch = (__builtin_amdgcn_ballot_w64(out) || hi < lo || hi - base > (uint64_t)KC * 1024u)
 			      ? ~0u : (uint32_t)((hi - base + 15) >> 4);
 	};
-	auto issue_region = [&](uint64_t base, uint32_t nch, u32x4 (&v)[KC]) {
+	auto issue_region = [&](const StreamSpan &sp, uint64_t base, uint32_t nch,
+				u32x4 (&v)[KC]) {
+		(void)sp;
+#ifdef XCSUM_DEBUG_BOUNDS
+		/* the 16-byte blocks of the present frames, computed apart from
+		 * region(): min start / max end over the lanes */
+		uint64_t mn = sp.present ? (uint64_t)(uintptr_t)(a.umem + sp.eth) : ~0ull;
+		uint64_t mx = sp.present ? (uint64_t)(uintptr_t)(a.umem + sp.eth) + sp.len : 0ull;
+		for (int o = 32; o; o >>= 1) {
+			const uint64_t m2 = __shfl_xor(mn, o), x2 = __shfl_xor(mx, o);
+			mn = m2 < mn ? m2 : mn;
+			mx = x2 > mx ? x2 : mx;
+		}
+		const uint64_t ok_lo = mn & ~15ull, ok_hi = (mx + 15) & ~15ull;
+#endif
 #pragma unroll
 		for (int k = 0; k < KC; k++) {
 			const uint32_t c = (uint32_t)k * 64u + lane;
-			v[k] = load_chunk(nch != ~0u && c < nch ? a.umem + base + 16u * c : zero);
+			v[k] = load_chunk(nch != ~0u && c < nch
+						  ? XB_LOAD((const uint8_t *)(uintptr_t)(base + 16u * c), 16,
+							    ok_lo, ok_hi, XB_STREAM_REGION, c, zero)
+						  : zero);
 		}
 	};
 	auto load_d = [&](uint32_t wi) {
-		const uint64_t p = 64ull * grp(wi) + lane;
+		const uint64_t p = 64ull * wi + lane;
 		return *((gu32x4 *)(a.desc + (p < a.n ? p : a.n - 1)));
 	};
 
-	if (w >= go.nlog)
+	if (w >= ngroups)
 		return;
 	u32x4 d = load_d(w);
 	StreamSpan sc = span_of(w, d);
@@ -283,9 +148,9 @@ static __device__ __forceinline__ void stream_loop(const CsumArgs &a, u32x4 *sta
 	uint32_t nc;
 	region(w, sc, bc, nc);
 	u32x4 v[KC];
-	issue_region(bc, nc, v);
+	issue_region(sc, bc, nc, v);
 	d = load_d(w + nw);
-	for (; w < go.nlog; w += nw) {
+	for (; w < ngroups; w += nw) {
 		/* this iteration's region -> LDS (waits for its loads only: the
 		 * descriptors issued after them may still be in flight) */
 #pragma unroll
@@ -295,11 +160,11 @@ static __device__ __forceinline__ void stream_loop(const CsumArgs &a, u32x4 *sta
 		const uint64_t cbase = bc;
 		const uint32_t cnch = nc;
 		/* next iteration: its region's loads go out before this one is summed */
-		if (w + nw < go.nlog) {
+		if (w + nw < ngroups) {
 			sc = span_of(w + nw, d);
 			region(w + nw, sc, bc, nc);
 			__builtin_amdgcn_sched_barrier(0);
-			issue_region(bc, nc, v);
+			issue_region(sc, bc, nc, v);
 			d = load_d(w + 2 * nw);
 		}
 		__builtin_amdgcn_sched_barrier(0);
@@ -310,7 +175,7 @@ static __device__ __forceinline__ void stream_loop(const CsumArgs &a, u32x4 *sta
 		if (cnch == ~0u) {
 			/* does not fit the stage: the whole wave walks each frame */
 			for (uint32_t i = 0; i < 64; i++) {
-				const uint64_t p64 = 64ull * grp(w) + i;
+				const uint64_t p64 = 64ull * w + i;
 				if (p64 >= a.n)
 					break;
 				const uint32_t p = (uint32_t)p64;
@@ -325,9 +190,14 @@ static __device__ __forceinline__ void stream_loop(const CsumArgs &a, u32x4 *sta
 			}
 		} else if (cur.present) {
 			/* lane = frame: everything from the LDS copy of the region */
-			const uint32_t oe = (uint32_t)(cur.eth - cbase);   /* frame in the stage */
+			/* frame in the stage */
+			const uint32_t oe = (uint32_t)((uint64_t)(uintptr_t)(a.umem + cur.eth) - cbase);
 			Frame f;
 			f.eth = a.umem + cur.eth;
+#ifdef XCSUM_DEBUG_BOUNDS
+			f.lim = (const uint8_t *)(((uintptr_t)f.eth + cur.len + 15u) & ~(uintptr_t)15);
+			f.dlen = cur.len;
+#endif
 			int mode = (int)a.mode;
 			if (mode == XCSUM_MODE_AUTO) {
 				const uint32_t pr = lds_bytes4(st8, oe + 12) & 0xffffu;  /* h_proto, LE */
@@ -356,7 +226,10 @@ static __device__ __forceinline__ void stream_loop(const CsumArgs &a, u32x4 *sta
 			const uint32_t lo = oe + hdr - pre, hi = oe + hdr + f.udp_len;
 			f.odd = lo & 1u;
 			if (mode >= 0) {
-				const uint32_t c0 = lo >> 4, c1 = (hi + 15) >> 4;
+				const uint32_t c0 = lo >> 4;
+				uint32_t c1 = (hi + 15) >> 4;
+				if (!XB_IDX(c1 - 1, (uint32_t)KC * 64u, XB_STREAM_STAGE))
+					c1 = c0 + 1;
 				for (uint32_t c = c0; c < c1; c++)
 					accum(stage[c], E, O);
 				drop_prefix(stage[c0], lo & 15u, E, O);
@@ -370,7 +243,7 @@ static __device__ __forceinline__ void stream_loop(const CsumArgs &a, u32x4 *sta
 				}
 			}
 			const uint32_t s = f.odd ? (O << 8) + E : (E << 8) + O;
-			finalize<2>(a, f, 64u * grp(w) + lane, s);
+			finalize<2>(a, f, 64u * w + lane, s);
 		}
 		/* the stage is rewritten next iteration: all reads done first */
 		__builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -379,25 +252,13 @@ static __device__ __forceinline__ void stream_loop(const CsumArgs &a, u32x4 *sta
 	}
 }
 
-/* XCSUM_STREAM_WPE=N builds a variant capped for N waves per SIMD (A/B) */
-#if defined(XCSUM_STREAM_WPE) && XCSUM_STREAM_WPE > 0
-#define STREAM_ATTR __attribute__((amdgpu_waves_per_eu(XCSUM_STREAM_WPE)))
-#else
-#define STREAM_ATTR
-#endif
-
-/* frame-group geometry (G, 1, 2) of the sparse fallback (A/B knob) */
-#ifndef XCSUM_STREAM_SPARSE_G
-#define XCSUM_STREAM_SPARSE_G 4
-#endif
-
 template <int KC>
-__global__ void __launch_bounds__(256) STREAM_ATTR csum_stream_kernel(CsumArgs a)
+__global__ void __launch_bounds__(256) csum_stream_kernel(CsumArgs a)
 {
 	extern __shared__ u32x4 stream_stage[];   /* [4 waves][KC * 64] chunks */
 	if (!dense_batch(a)) {
 		/* sparse batch: the frame-group kernel, region order as usual */
-		csum_body<XCSUM_STREAM_SPARSE_G, 1, 2, 2>(a);
+		csum_body<4, 1, 2, 2>(a);
 		return;
 	}
 	stream_loop<KC>(a, stream_stage + (threadIdx.x >> 6) * (KC * 64));
@@ -461,12 +322,7 @@ bool geometry_supported(Geometry g)
 {
 	if (g.G == 64 && g.U == 0 && (g.K == 4 || g.K == 8 || g.K == 16))
 		return true;
-#define X(f_, d_) if (g.G == 64 && g.U == f_ && g.K == d_) return true;
-	XCSUM_SEG_GEOMETRIES(X)
-#undef X
-	if (g.G == 16 && ((g.U == 12 || g.U == 13) && g.K == 6))
-		return true;
-	if (g.G == 16 && ((g.U == 12 || g.U == 14) && g.K == 3))
+	if (variant_supported && variant_supported(g))
 		return true;
 #define X(g_, u_, k_) if (g.G == g_ && g.U == u_ && g.K == k_) return true;
 	XCSUM_GEOMETRIES(X)
@@ -479,7 +335,6 @@ hipError_t launch_csum(const CsumArgs &a, Geometry g, int cus, hipStream_t s)
 {
 	if (a.n == 0)
 		return hipSuccess;
-	/* LDS-staged variant: G = 16, U = 10 + ring depth; identity order */
 	/* stream kernel: G = 64 lanes per 64 frames, U = 0, K = KiB of stage */
 	if (g.G == 64 && g.U == 0) {
 		if (g.K == 4) return launch_stream_t<4>(a, cus, g.B, s);
@@ -487,17 +342,9 @@ hipError_t launch_csum(const CsumArgs &a, Geometry g, int cus, hipStream_t s)
 		if (g.K == 16) return launch_stream_t<16>(a, cus, g.B, s);
 		return hipErrorInvalidValue;
 	}
-	/* segmented stream: G = 64 lanes, U = frames per unit (8..64), K = rows
-	 * in flight (XCSUM_SEG_GEOMETRIES) */
-	if (g.G == 64 && g.U >= 8)
-		return launch_seg(a, g.U, g.K, cus, g.B, s);
-	CsumArgs b = a;
-	b.ord = order_identity(a.n);
-	b.dense = b.ord;
-	if (g.G == 16 && g.U == 12 && g.K == 6) return launch_lds_t<6, 2>(b, cus, g.B, s);
-	if (g.G == 16 && g.U == 13 && g.K == 6) return launch_lds_t<6, 3>(b, cus, g.B, s);
-	if (g.G == 16 && g.U == 14 && g.K == 3) return launch_lds_t<3, 4>(b, cus, g.B, s);
-	if (g.G == 16 && g.U == 12 && g.K == 3) return launch_lds_t<3, 2>(b, cus, g.B, s);
+	/* A/B kernels of a variants build (csrc/variants/, not in libxcsum.so) */
+	if (variant_supported && variant_supported(g))
+		return launch_variant(a, g, cus, s);
 	/* Three instantiations per geometry (FEAT): 0 plain, 1 + VERIFY
 	 * (udp->len and udp->check prefetched a pipeline step ahead), 2 + IPHDR
 	 * (the IPv4 header prefetched too).  Each keeps only the registers and
@@ -547,7 +394,8 @@ __global__ void __launch_bounds__(256) gen_kernel(uint8_t *umem, const struct xc
 		for (uintptr_t w = ((uintptr_t)eth & ~(uintptr_t)3) + 4 * lane; w < e; w += 256) {
 			long o0 = (long)(w - (uintptr_t)eth);
 			if (w >= (uintptr_t)eth && w + 4 <= e) {
-				*reinterpret_cast<uint32_t *>(w) = gen_dword(family, key, d.len, hdr, o0);
+				if (XB_STORE(w, 4, eth, e, XB_GEN_STORE, p))
+					*reinterpret_cast<uint32_t *>(w) = gen_dword(family, key, d.len, hdr, o0);
 			} else {
 				for (int k = 0; k < 4; k++) {
 					long o = o0 + k;
@@ -575,4 +423,24 @@ hipError_t launch_gen(uint8_t *d_umem, const struct xcsum_desc *d_desc, uint32_t
 	return hipGetLastError();
 }
 
+#ifdef XCSUM_DEBUG_BOUNDS
+/* positive control of the debug build: one check that must fail, so a test
+ * can see the log -> xcsum_debug_bounds() path report it (nothing is
+ * accessed) */
+__global__ void bounds_selftest_kernel(uint32_t index)
+{
+	if (threadIdx.x == 0)
+		(void)XB_IN((const void *)0x1000, 16, (const void *)0x2000, (const void *)0x3000,
+			    XB_GEN_STORE, index);
+}
+#endif
+
 } /* namespace xcsum */
+
+#ifdef XCSUM_DEBUG_BOUNDS
+extern "C" int xcsum_debug_bounds_selftest(uint32_t index)
+{
+	hipLaunchKernelGGL(xcsum::bounds_selftest_kernel, dim3(1), dim3(64), 0, nullptr, index);
+	return hipGetLastError() == hipSuccess && hipDeviceSynchronize() == hipSuccess ? 0 : -1;
+}
+#endif

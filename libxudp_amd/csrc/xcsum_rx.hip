@@ -56,18 +56,10 @@ namespace xcsum {
  * Plain stores left 64 MB of dirty lines per 1M frames in L2 among the
  * streaming frame reads: MTU VERIFY 0.287 -> 0.259 ms (1.21x -> 1.09x the
  * checksum kernel), IPv6 1.17x -> 1.08x, config 5 1.03x -> 1.02x, same
- * call (profiles/r02/session2/rx_ntrec).  XCSUM_RX_NTREC=0 builds the plain
- * stores (A/B only). */
-#ifndef XCSUM_RX_NTREC
-#define XCSUM_RX_NTREC 1
-#endif
-
+ * call (profiles/r02/session2/rx_ntrec). */
 static __device__ __forceinline__ void store_rec(u32x4 *dst, u32x4 v)
 {
-	if (XCSUM_RX_NTREC)
-		__builtin_nontemporal_store(v, dst);
-	else
-		*dst = v;
+	__builtin_nontemporal_store(v, dst);
 }
 
 static __device__ __forceinline__ uint32_t be16(const uint8_t *p)
@@ -160,10 +152,13 @@ static __device__ Parsed packet_parse(const uint8_t *pkt, uint32_t len)
 
 /* chunk c of the dword grid over [lo, hi): masked, for summing */
 static __device__ __forceinline__ u32x4 grid_chunk(const uint8_t *base, uint32_t n,
-						   uint32_t head, uint32_t tail, uint32_t c)
+						   uint32_t head, uint32_t tail, uint32_t c,
+						   const uint8_t *ok_lo, const uint8_t *ok_hi)
 {
 	u32x4 v = {0u, 0u, 0u, 0u};
-	if (c < n) {
+	(void)ok_lo;
+	(void)ok_hi;
+	if (c < n && XB_IN(base + 16u * c, 16, ok_lo, ok_hi, XB_RX_CHUNK, c)) {
 		v = __builtin_nontemporal_load((gu32x4 *)(base + 16u * c));
 		if (c == 0) {
 			const uint64_t k0 = head >= 8 ? 0ull : ~0ull << (8 * (head & 7));
@@ -221,7 +216,10 @@ static __device__ Rec rx_slow(const uint8_t *pkt, uint32_t len, uint32_t lane, b
 			uint32_t E = 0, O = 0;
 			for (uint32_t c = lane; c < n; c += G)   /* one chunk per lane in flight:
 								    rare path, few registers */
-				accum(grid_chunk(base, n, head, tail, c), E, O);
+				accum(grid_chunk(base, n, head, tail, c, pkt,
+						 (const uint8_t *)(((uintptr_t)pkt + len + 15u) &
+								   ~(uintptr_t)15)),
+				      E, O);
 			uint32_t s = (lo & 1u) ? (O << 8) + E : (E << 8) + O;
 			s = seg_sum<G>(s);
 			/* pseudo header (RFC 768 / RFC 2460 8.1) */
@@ -338,6 +336,18 @@ static __device__ __forceinline__ int rx_chunk_off(uint32_t h, uint32_t c)
 	return 12 - (int)h + 16 * (int)c;
 }
 
+/* what a frame's chunk loads may touch (bounds checks of the debug build):
+ * the 16-byte blocks from the one holding eth + 12 to the one holding the
+ * last byte */
+__attribute__((unused)) static __device__ __forceinline__ const uint8_t *rx_ok_lo(const RFrame &f)
+{
+	return (const uint8_t *)(((uintptr_t)f.eth + 12u) & ~(uintptr_t)15);
+}
+__attribute__((unused)) static __device__ __forceinline__ const uint8_t *rx_ok_hi(const RFrame &f)
+{
+	return (const uint8_t *)(((uintptr_t)f.eth + rx_len(f) + 15u) & ~(uintptr_t)15);
+}
+
 __device__ u32x4 g_rx_zero[4];
 
 template <int G, int K>
@@ -353,7 +363,9 @@ static __device__ __forceinline__ void rx_issue(const RxArgs &a, const RFrame &f
 	for (int k = 0; k < K; k++) {
 		const uint32_t c = lane + k * G;
 		v[k] = __builtin_nontemporal_load(
-			(gu32x4 *)(c < nl ? f.eth + rx_chunk_off(h, c) : zero));
+			(gu32x4 *)(c < nl ? XB_LOAD(f.eth + rx_chunk_off(h, c), 16, rx_ok_lo(f),
+						    rx_ok_hi(f), XB_RX_CHUNK, c, zero)
+					  : zero));
 	}
 }
 
@@ -476,7 +488,8 @@ static __device__ __forceinline__ void rx_frame(const RxArgs &a, uint32_t *st, c
 		if (__builtin_amdgcn_ballot_w64(good && nchunks > K * G)) {
 			for (uint32_t c = lane; c < nchunks; c += G) {
 				const int cb = rx_chunk_off(fh, c);
-				u32x4 v = __builtin_nontemporal_load((gu32x4 *)(fc.eth + cb));
+				u32x4 v = __builtin_nontemporal_load((gu32x4 *)XB_LOAD(
+					fc.eth + cb, 16, rx_ok_lo(fc), rx_ok_hi(fc), XB_RX_CHUNK, c, g_rx_zero));
 				if (cb < lo || cb + 16 > hi)
 					v = keep_span(tab, v, lo - cb, hi - cb);
 				accum(v, E, O);
@@ -545,7 +558,7 @@ static __device__ __forceinline__ void rx_frame(const RxArgs &a, uint32_t *st, c
 	for (int i = 0; i < (G < 4 ? 4 / G : 1); i++) {
 		const uint32_t j = lane + i * G;       /* piece */
 		const u32x4 w = j == 0 ? w0 : (j == 1 ? w1 : (j == 2 ? saddr : daddr));
-		if (present && j < 4)
+		if (present && j < 4 && XB_IDX(p, a.n, XB_RX_REC))
 			store_rec((u32x4 *)(a.msgs + p) + j, w);
 	}
 	if (lane == 0 && present && r.status == XCSUM_RX_OK)
@@ -659,7 +672,7 @@ static __device__ __forceinline__ void rx_group_body(RxArgs a, uint32_t *stage,
 		if ((threadIdx.x & 63) == 0)
 			wsum[threadIdx.x >> 6] = tot;
 		__syncthreads();
-		if (threadIdx.x == 0)
+		if (threadIdx.x == 0 && XB_IDX(blockIdx.x, RX_PART_MAX, XB_RX_PART))
 			a.part[blockIdx.x] = wsum[0] + wsum[1] + wsum[2] + wsum[3];
 	}
 }
@@ -833,7 +846,8 @@ static __device__ __forceinline__ uint32_t rx_step_sum(const uint32_t *tab, cons
 	if (__builtin_amdgcn_ballot_w64((s.fl & 2u) && nchunks > K * G)) {
 		for (uint32_t c = lane; c < nchunks; c += G) {
 			const int cb = rx_chunk_off(fh, c);
-			u32x4 x = __builtin_nontemporal_load((gu32x4 *)(s.f.eth + cb));
+			u32x4 x = __builtin_nontemporal_load((gu32x4 *)XB_LOAD(
+				s.f.eth + cb, 16, rx_ok_lo(s.f), rx_ok_hi(s.f), XB_RX_CHUNK, c, g_rx_zero));
 			if (cb < lo || cb + 16 > hi)
 				x = keep_span(tab, x, lo - cb, hi - cb);
 			accum(x, E, O);
@@ -852,13 +866,6 @@ static __device__ __forceinline__ uint32_t rx_step_sum(const uint32_t *tab, cons
 }
 
 
-/* XCSUM_RX_WIDE_WPE=N builds a variant capped for N waves per SIMD (A/B) */
-#if defined(XCSUM_RX_WIDE_WPE) && XCSUM_RX_WIDE_WPE > 0
-#define RX_WIDE_ATTR __attribute__((amdgpu_waves_per_eu(XCSUM_RX_WIDE_WPE)))
-#else
-#define RX_WIDE_ATTR
-#endif
-
 /* hstage: 256 * WSTAGE dwords of LDS, 16-byte aligned; span: the mask table,
  * initialised (span_init + block barrier) by the caller */
 template <int G, int K>
@@ -867,10 +874,9 @@ static __device__ __forceinline__ void rx_wide_body(RxArgs a, uint32_t *hstage,
 {
 	constexpr uint32_t FPS = 64 / G;        /* frames per step */
 	constexpr uint32_t STEPS = G;           /* 64 frames per batch */
-#ifndef XCSUM_RX_WIDE_HDR_LEAD
-#define XCSUM_RX_WIDE_HDR_LEAD 4   /* 4 steps: config 2 -2.3%, config 5 -3.1% vs 0 (rx_wide/rxlead) */
-#endif
-	constexpr uint32_t HDR_LEAD = XCSUM_RX_WIDE_HDR_LEAD;   /* even */
+	/* the next batch's headers go out HDR_LEAD steps before this batch ends:
+	 * 4 steps config 2 -2.3 %, config 5 -3.1 % against 0 (rx_wide/rxlead) */
+	constexpr uint32_t HDR_LEAD = 4;   /* even */
 	const uint32_t wl = threadIdx.x & 63u;  /* lane = frame of the batch */
 	const uint32_t lane = wl & (G - 1);     /* lane in the step's group */
 	const uint32_t grp = wl / G;
@@ -896,8 +902,10 @@ static __device__ __forceinline__ void rx_wide_body(RxArgs a, uint32_t *hstage,
 			/* temporal: the span loads re-read these lines one batch
 			 * later; loaded nontemporal they were evicted first and
 			 * fetched twice (+220 B per MTU frame, FETCH_SIZE) */
-			hv[i] = *((gu32x4 *)(c < nc && c < STAGE_CHUNKS ? s.f.eth + rx_chunk_off(h, c)
-									 : zero));
+			hv[i] = *((gu32x4 *)(c < nc && c < STAGE_CHUNKS
+						     ? XB_LOAD(s.f.eth + rx_chunk_off(h, c), 16, rx_ok_lo(s.f),
+							       rx_ok_hi(s.f), XB_RX_CHUNK, c, zero)
+						     : zero));
 		}
 	};
 	auto span_issue = [&](const WStep &s, u32x4 (&v)[K]) {
@@ -907,7 +915,9 @@ static __device__ __forceinline__ void rx_wide_body(RxArgs a, uint32_t *hstage,
 		for (int k = 0; k < K; k++) {
 			const uint32_t c = lane + k * G;
 			v[k] = __builtin_nontemporal_load(
-				(gu32x4 *)(c < nc ? s.f.eth + rx_chunk_off(h, c) : zero));
+				(gu32x4 *)(c < nc ? XB_LOAD(s.f.eth + rx_chunk_off(h, c), 16, rx_ok_lo(s.f),
+							    rx_ok_hi(s.f), XB_RX_CHUNK, c, zero)
+						  : zero));
 		}
 	};
 
@@ -1036,7 +1046,8 @@ static __device__ __forceinline__ void rx_wide_body(RxArgs a, uint32_t *hstage,
 #pragma unroll
 			for (uint32_t i = 0; i < 4; i++) {
 				const u32x4 v = *((const u32x4 *)(wst + 256u * i + 4u * wl));
-				if (fb + 16u * i + (wl >> 2) < a.n)
+				if (fb + 16u * i + (wl >> 2) < a.n &&
+				    XB_IDX(fb + 16u * i + (wl >> 2), a.n, XB_RX_REC))
 					store_rec(&m[64u * i + wl], v);
 			}
 			__builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -1054,13 +1065,13 @@ static __device__ __forceinline__ void rx_wide_body(RxArgs a, uint32_t *hstage,
 		if ((threadIdx.x & 63) == 0)
 			wsum[threadIdx.x >> 6] = tot;
 		__syncthreads();
-		if (threadIdx.x == 0)
+		if (threadIdx.x == 0 && XB_IDX(blockIdx.x, RX_PART_MAX, XB_RX_PART))
 			a.part[blockIdx.x] = wsum[0] + wsum[1] + wsum[2] + wsum[3];
 	}
 }
 
 template <int G, int K>
-__global__ void __launch_bounds__(256) RX_WIDE_ATTR rx_wide_kernel(RxArgs a)
+__global__ void __launch_bounds__(256) rx_wide_kernel(RxArgs a)
 {
 	__shared__ __attribute__((aligned(16))) uint32_t span[SPAN_DWORDS];
 	__shared__ __attribute__((aligned(16))) uint32_t hstage[256 * WSTAGE];
@@ -1143,12 +1154,27 @@ __global__ void __launch_bounds__(256) rx_stream_kernel(RxArgs a)
 		nch = (__builtin_amdgcn_ballot_w64(out) || hi < lo ||
 		       hi - base > (uint64_t)KC * 1024u) ? ~0u : (uint32_t)((hi - base + 15) >> 4);
 	};
-	auto issue_region = [&](uintptr_t base, uint32_t nch, u32x4 (&v)[KC]) {
+	auto issue_region = [&](const RFrame &f, uintptr_t base, uint32_t nch, u32x4 (&v)[KC]) {
+		(void)f;
+#ifdef XCSUM_DEBUG_BOUNDS
+		/* the present frames' 16-byte blocks, apart from region() */
+		uint64_t mn = rx_present(f) ? (uint64_t)(uintptr_t)f.eth : ~0ull;
+		uint64_t mx = rx_present(f) ? (uint64_t)(uintptr_t)f.eth + rx_len(f) : 0ull;
+		for (int o = 32; o; o >>= 1) {
+			const uint64_t m2 = __shfl_xor(mn, o), x2 = __shfl_xor(mx, o);
+			mn = m2 < mn ? m2 : mn;
+			mx = x2 > mx ? x2 : mx;
+		}
+		const uint64_t ok_lo = mn & ~15ull, ok_hi = (mx + 15) & ~15ull;
+#endif
 #pragma unroll
 		for (int k = 0; k < KC; k++) {
 			const uint32_t c = (uint32_t)k * 64u + lane;
 			v[k] = __builtin_nontemporal_load(
-				(gu32x4 *)(nch != ~0u && c < nch ? (const uint8_t *)base + 16u * c : zero));
+				(gu32x4 *)(nch != ~0u && c < nch
+						   ? XB_LOAD((const uint8_t *)base + 16u * c, 16, ok_lo, ok_hi,
+							     XB_RX_STREAM, c, zero)
+						   : zero));
 		}
 	};
 	auto wave_sync = [] {
@@ -1163,7 +1189,7 @@ __global__ void __launch_bounds__(256) rx_stream_kernel(RxArgs a)
 	u32x4 v[KC];
 	if (64ull * w < a.n) {
 		region(w, fc, bc, nc);
-		issue_region(bc, nc, v);
+		issue_region(fc, bc, nc, v);
 	}
 	u32x3 dn = desc_at(w + nw);
 	for (; 64ull * w < a.n; w += nw) {
@@ -1179,7 +1205,7 @@ __global__ void __launch_bounds__(256) rx_stream_kernel(RxArgs a)
 			fc = frame_at(w + nw, dn);
 			region(w + nw, fc, bc, nc);
 			__builtin_amdgcn_sched_barrier(0);
-			issue_region(bc, nc, v);
+			issue_region(fc, bc, nc, v);
 			dn = desc_at(w + 2 * nw);
 		}
 		__builtin_amdgcn_sched_barrier(0);
@@ -1280,7 +1306,8 @@ __global__ void __launch_bounds__(256) rx_stream_kernel(RxArgs a)
 #pragma unroll
 		for (uint32_t i = 0; i < 4; i++) {
 			const u32x4 x = stage[64u * i + lane];
-			if (64ull * w + 16u * i + (lane >> 2) < a.n)
+			if (64ull * w + 16u * i + (lane >> 2) < a.n &&
+			    XB_IDX(64ull * w + 16u * i + (lane >> 2), a.n, XB_RX_REC))
 				store_rec(&m[64u * i + lane], x);
 		}
 		wave_sync();   /* the next region overwrites the stage */
@@ -1293,7 +1320,7 @@ __global__ void __launch_bounds__(256) rx_stream_kernel(RxArgs a)
 		if ((threadIdx.x & 63) == 0)
 			wsum[threadIdx.x >> 6] = tot;
 		__syncthreads();
-		if (threadIdx.x == 0)
+		if (threadIdx.x == 0 && XB_IDX(blockIdx.x, RX_PART_MAX, XB_RX_PART))
 			a.part[blockIdx.x] = wsum[0] + wsum[1] + wsum[2] + wsum[3];
 	}
 }
@@ -1424,16 +1451,10 @@ hipError_t launch_rx(const RxArgs &a, uint32_t len_hint, int cus, hipStream_t s)
 		if (U == 0 && tlog < 6)
 			tlog = 6;
 		b.ord = order_regions(a.n, rlog, tlog);
+		/* dense batches keep descriptor order: 8-32 regions measured
+		 * slower for the receive kernels (session2/order_dense s23), and
+		 * the stream kernel (U = 3) reads consecutive frames */
 		b.ord.sparse_only = 1u;
-		/* dense batches: XCSUM_RX_DENSE="R,T" (A/B; the stream kernel,
-		 * U = 3, needs descriptor order for them) */
-		const char *de = getenv("XCSUM_RX_DENSE");
-		int dr = 0, dt = 6;
-		if (U != 3 && de && sscanf(de, "%d,%d", &dr, &dt) >= 1 && dr > 0) {
-			if (U == 0 && dt < 6)
-				dt = 6;
-			b.dense = order_regions(a.n, dr, dt);
-		}
 	}
 #define X(g_, k_, u_) \
 	if (G == g_ && K == k_ && U == u_) return launch_rx_t<g_, k_, u_>(b, cus, B, s);

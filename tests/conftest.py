@@ -47,6 +47,23 @@ def engine():
     e.close()
 
 
+@pytest.fixture(autouse=True)
+def bounds_checked(request):
+    """Under the bounds-checked debug build (XCSUM_LIB=libxudp_amd/debug/
+    libxcsum.so, make -C libxudp_amd debug) every GPU test ends by reading the
+    kernels' violation logs: any load or store outside its frame, stream
+    region or result array fails the test that made it."""
+    yield
+    if "gpu" not in request.keywords or not os.environ.get("XCSUM_LIB"):
+        return
+    import libxudp_amd as X
+    if not X.debug_build():
+        return
+    count, recs = X.take_bounds()
+    assert count == 0, f"{count} out-of-bounds accesses, first: " + "; ".join(
+        f"{s}[{i}] addr {a:#x} allowed [{lo:#x}, {hi:#x})" for s, i, a, lo, hi in recs[:4])
+
+
 @pytest.fixture(scope="session")
 def torch_cuda():
     import torch

@@ -138,20 +138,22 @@ def test_argument_validation_without_gpu():
 def test_geometry_list_matches_kernel_source():
     """X.GEOMETRIES (what the parity tests sweep) == the instantiations in
     the XCSUM_GEOMETRIES table (csrc/xcsum_csum.h, instantiated per feature set
-    in xcsum_csum_f{0,1,2}.hip) + the LDS, stream and segmented-stream dispatch of
-    csrc/xcsum_kernels.hip."""
+    in xcsum_csum_f{0,1,2}.hip) + the stream dispatch of csrc/xcsum_kernels.hip;
+    the A/B lists == the dispatch of csrc/variants/ (LDS-staged, segmented)."""
     import re
     csrc = os.path.join(ROOT, "libxudp_amd", "csrc")
     src = open(os.path.join(csrc, "xcsum_kernels.hip")).read()
+    vsrc = open(os.path.join(csrc, "variants", "xcsum_lds.hip")).read()
     hdr = open(os.path.join(csrc, "xcsum_csum.h")).read()
     table = hdr[hdr.index("#define XCSUM_GEOMETRIES"):]
     table = table[:table.index("\n\n")]
     reg = [tuple(map(int, m)) for m in re.findall(r"X\((\d+), (\d+), (\d+)\)", table)]
     lds = [tuple(map(int, m)) for m in re.findall(
-        r"g\.G == (\d+) && g\.U == (\d+) && g\.K == (\d+)\) return launch_lds_t", src)]
+        r"g\.U == (\d+) && g\.K == (\d+)\) return launch_lds_t", vsrc)]
+    lds = [(16, int(u), int(k)) for u, k in lds]
     stream = [(64, 0, int(k)) for k in re.findall(
         r"if \(g\.K == (\d+)\) return launch_stream_t", src)]
-    internal = open(os.path.join(csrc, "xcsum_internal.h")).read()
+    internal = open(os.path.join(csrc, "variants", "xcsum_variants.h")).read()
     segt = internal[internal.index("#define XCSUM_SEG_GEOMETRIES"):]
     segt = segt[:segt.index("\n")]
     seg = [(64, int(f), int(d)) for f, d in re.findall(r"X\((\d+), (\d+)\)", segt)]
@@ -159,6 +161,7 @@ def test_geometry_list_matches_kernel_source():
     assert reg == X.REG_GEOMETRIES
     assert sorted(lds) == sorted(X.LDS_GEOMETRIES)
     assert sorted(stream) == sorted(X.STREAM_GEOMETRIES)
+    assert X.GEOMETRIES == X.REG_GEOMETRIES + X.STREAM_GEOMETRIES
 
 
 def test_rx_msg_layout_matches_c():

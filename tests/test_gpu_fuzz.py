@@ -122,6 +122,10 @@ def test_fuzz_host_path_vs_device(torch_cuda, engine, seed):
     """xcsum_batch_host (staged copies, or zero-copy from a registered UMEM)
     on random batches: the same results as the oracle, and with INPLACE the
     same frame bytes as the device path writes."""
+    host_fuzz_case(torch_cuda, engine, seed)
+
+
+def host_fuzz_case(torch_cuda, engine, seed):
     rng = np.random.default_rng(3000 + seed)
     umem, desc = random_batch(rng)
     mode = MODES[int(rng.integers(len(MODES)))]

@@ -16,10 +16,13 @@ from conftest import golden_desc
 
 pytestmark = pytest.mark.gpu
 
-GEOMETRIES = X.GEOMETRIES
-# the default pick plus the LDS-staged variant: the feature tests below run
-# under each, so both kernels see INPLACE/IPHDR/VERIFY, ragged and maximum sizes
-FEATURE_GEOMS = [None] + X.LDS_GEOMETRIES + X.STREAM_GEOMETRIES + X.SEG_GEOMETRIES
+# every product geometry, plus the A/B kernels when XCSUM_LIB loads a variants
+# build (csrc/variants/)
+GEOMETRIES = X.GEOMETRIES + X.variant_geometries()
+# the default pick plus the stream kernels (and the A/B kernels of a variants
+# build): the feature tests below run under each, so every kernel sees
+# INPLACE/IPHDR/VERIFY, ragged and maximum sizes
+FEATURE_GEOMS = [None] + X.STREAM_GEOMETRIES + X.variant_geometries()
 
 
 @contextlib.contextmanager
@@ -374,3 +377,32 @@ def test_verify_padded_frames_pass(torch_cuda, engine):
     engine.batch_host(umem, desc, out, X.MODE_AUTO, X.F_VERIFY | X.F_IPHDR)
     assert (out == 0).all()
     assert engine.take_errors() == 0
+
+
+@pytest.mark.parametrize("base_off", [1, 3, 8, 13])
+@pytest.mark.parametrize("geom", [None, (4, 1, 2), (16, 2, 6)] + X.STREAM_GEOMETRIES)
+def test_unaligned_umem_base(torch_cuda, engine, base_off, geom):
+    """d_umem not 16-byte aligned (the ABI allows any base): descriptors are
+    offsets from it.  The stream kernel aligns its regions as addresses, so
+    no load reaches past the 16-byte block of a frame's last byte.  Small
+    packed frames (the stream kernel's case) and MTU frames, every flag set,
+    against the oracle; the frame bytes around the batch stay untouched."""
+    dev = torch_cuda.device("cuda:0")
+    for fam, pmin, pmax in ((4, 0, 80), (6, 0, 80), (4, 1400, 1472)):
+        umem, desc = X.gen_frames_host(700, fam, pmin, pmax, seed=fam + pmax + base_off, align=2)
+        mode = X.MODE_V6 if fam == 6 else X.MODE_V4_RFC
+        for flags in (0, X.F_INPLACE | X.F_IPHDR, X.F_VERIFY):
+            buf = np.zeros(len(umem) + 64, np.uint8)
+            buf[base_off:base_off + len(umem)] = umem
+            d_buf = torch_cuda.from_numpy(buf).to(dev)
+            d_desc = torch_cuda.from_numpy(desc.view(np.uint8)).to(dev)
+            d_out = torch_cuda.zeros(len(desc), dtype=torch_cuda.int16, device=dev)
+            with geometry(engine, geom):
+                engine.batch_device(d_buf.data_ptr() + base_off, d_desc, len(desc), d_out, mode,
+                                    flags, stream=torch_cuda.cuda.current_stream(dev).cuda_stream)
+                torch_cuda.cuda.synchronize(dev)
+            got = d_out.cpu().numpy().view(np.uint16)
+            exp = oracle.batch(umem, desc, mode, flags & ~X.F_INPLACE)
+            assert np.array_equal(got, exp), (fam, flags, int((got != exp).sum()))
+            after = d_buf.cpu().numpy()
+            assert not after[:base_off].any() and not after[base_off + len(umem):].any()

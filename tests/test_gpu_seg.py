@@ -1,4 +1,6 @@
-"""GPU: the segmented-stream checksum kernel (csrc/xcsum_seg.hip, geometries
+"""GPU: the segmented-stream checksum kernel (csrc/variants/xcsum_seg.hip, an
+A/B kernel outside libxcsum.so: runs only when XCSUM_LIB loads a variants
+build; geometries
 X.SEG_GEOMETRIES) against the oracle on the batch shapes it treats
 differently: mixed sizes U[0, 9000] packed at byte and 8-byte alignment,
 ragged unit counts, units whose descriptors are out of UMEM order or
@@ -12,7 +14,9 @@ import libxudp_amd as X
 import oracle
 from test_gpu_parity import geometry, run_device
 
-pytestmark = pytest.mark.gpu
+pytestmark = [pytest.mark.gpu,
+              pytest.mark.skipif(not X.variants_built(),
+                                 reason="segmented stream: variants build only (XCSUM_LIB)")]
 
 MODES = {4: X.MODE_V4_LEGACY, 6: X.MODE_V6}
 
