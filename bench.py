@@ -57,6 +57,38 @@ CONFIGS = {
             name="8M x U[64,9000]B UDP/IPv4 sharded by bytes over the GPUs (BASELINE config 5)"),
 }
 MODE_NAMES = {0: "v4_legacy", 1: "v4_rfc", 2: "v6", 3: "auto"}
+FLAG_NAMES = {"inplace": X.F_INPLACE, "iphdr": X.F_IPHDR, "rfc": X.F_V4_RFC, "verify": X.F_VERIFY}
+
+
+def parse_flags(text):
+    """--flags inplace,iphdr -> XCSUM_F_* bits"""
+    f = 0
+    for w in filter(None, (t.strip() for t in text.split(","))):
+        if w not in FLAG_NAMES:
+            raise SystemExit(f"--flags: unknown flag {w!r} (known: {', '.join(FLAG_NAMES)})")
+        f |= FLAG_NAMES[w]
+    return f
+
+
+def alg_bytes_flags(desc, family, flags, with_out):
+    """Algorithmic bytes of one launch: the span read (UDP
+    length + pseudo-header addresses), plus with XCSUM_F_IPHDR on IPv4 the 12
+    header bytes before the addresses; writes: the 2-byte result when there
+    is a result array, and every 2-byte check field written in place."""
+    span = X.alg_bytes(desc, family) - 2 * len(desc)
+    v4 = family == 4
+    read = span + (12 * len(desc) if (flags & X.F_IPHDR) and v4 else 0)
+    inplace = (flags & X.F_INPLACE) and not (flags & X.F_VERIFY)
+    fields = (1 if inplace else 0) + (1 if inplace and (flags & X.F_IPHDR) and v4 else 0)
+    return read + 2 * len(desc) * ((1 if with_out else 0) + fields)
+
+
+def lib_sha16():
+    """SHA-256 prefix of the loaded libxcsum.so: ties committed PMC counters
+    to the binary that was timed"""
+    import hashlib
+    with open(X.LIB_PATH, "rb") as f:
+        return hashlib.sha256(f.read()).hexdigest()[:16]
 
 
 def dist_env():
@@ -129,7 +161,9 @@ def host_cpu_facts():
 
 def cpu_baseline(cfg, seconds=15.0):
     """The reference checksum.h timed on this host over a bounded sample:
-    1 thread, 16 threads and os.cpu_count() threads (static frame partition)."""
+    1 thread, 16 threads and os.cpu_count() threads (static frame partition).
+    Each leg first runs one untimed repetition (thread creation, caches), then
+    one timed repetition sizes the leg to its share of `seconds`."""
     import oracle  # test infrastructure, used here only as the CPU baseline
     seed = SEED_BASE ^ cfg["id"]
     m = min(cfg["n"], 1 << 16)
@@ -145,45 +179,64 @@ def cpu_baseline(cfg, seconds=15.0):
         kind, L = "port", oracle.port()
         timed = lambda th, reps: L.orc_batch_timed(umem.ctypes.data, desc.ctypes.data, m,
                                                    out.ctypes.data, mode, 0, th, reps)
+    facts = host_cpu_facts()
+    usable = min(v for v in (facts.get("affinity_cpus"), facts.get("cgroup_cpu_quota"),
+                             facts.get("host_cpus")) if v)
+    facts["cores_usable"] = usable
     allc = max(1, min(256, os.cpu_count() or 1))
     legs = [(1, 0.3), (min(16, allc), 0.35)]
     if allc > 16:
         legs.append((allc, 0.35))
-    res = {}
+    res, secs = {}, {}
+    t_start = time.perf_counter()
     for th, share in legs:
+        timed(th, 1)                       # warm: threads, page faults, caches
         t1 = timed(th, 1)
         reps = max(1, int(seconds * share / max(t1, 1e-6)))
         t = timed(th, reps)
         res[th] = alg * reps / t / 2**30
+        secs[th] = round(t + 2 * t1, 3)
+    total = time.perf_counter() - t_start
     exp = oracle.ref_batch(umem, desc, mode) if kind == "reference" else oracle.batch(umem, desc,
                                                                                         mode)
     assert np.array_equal(out, exp)
     best_th = max(res, key=lambda k: res[k])
-    facts = host_cpu_facts()
+    legs_txt = ", ".join(f"{th} thread{'s' if th > 1 else ''} {secs[th]:.1f} s"
+                         for th, _ in legs)
     return {"value": round(res[best_th], 3), "unit": "GiB/s", "cores": best_th, "kind": kind,
             "by_threads": {str(k): round(v, 3) for k, v in sorted(res.items())},
+            "seconds_by_threads": {str(k): v for k, v in sorted(secs.items())},
+            "seconds_total": round(total, 2),
             "value_1core": round(res[1], 3), **facts,
             "sample": f"{m} frames of the same config ({alg / 1e6:.1f} MB algorithmic), "
-                      f"repeated for ~{seconds:.0f} s in all; xudp/checksum.h "
-                      f"{'udp_csum6' if mode == 2 else 'udp_checksum'} compiled -O2 from the "
-                      f"reference, static frame partition over 1, 16 and os.cpu_count() "
-                      f"pthreads; value = the fastest of those"}
+                      f"xudp/checksum.h {'udp_csum6' if mode == 2 else 'udp_checksum'} compiled "
+                      f"-O2 from the reference, static frame partition; legs: {legs_txt} "
+                      f"({total:.1f} s in all, warm-up repetitions included); "
+                      f"{usable:g} CPUs usable by this job (affinity / cgroup quota), so "
+                      f"thread counts above that time-slice; value = the fastest leg"}
 
 
-def pmc_traffic(cid, layout):
+def pmc_traffic(cid, layout, flags, sha):
     """HBM bytes per launch from the rocprofv3 PMC summary committed under
     profiles/ (FETCH_SIZE + WRITE_SIZE passes of this bench, tools/pmc_summary.py);
-    counters cannot be read inside the timed process itself."""
-    for rnd in ("r02", "r01", ""):
-        name = f"pmc_config{cid}{'_umem' if layout == 'umem' else ''}.json"
-        path = os.path.join(ROOT, "profiles", rnd, name)
-        if os.path.exists(path):
-            try:
-                return (json.load(open(path)).get("hbm_bytes_per_launch"),
-                        os.path.relpath(path, ROOT))
-            except Exception:
-                pass
-    return None, None
+    counters cannot be read inside the timed process itself.  Only counters
+    taken on this very library (same SHA-256 prefix) are reported; otherwise
+    traffic is null and the reason says which binary they came from."""
+    tag = f"{'_umem' if layout == 'umem' else ''}{'_f%x' % flags if flags else ''}"
+    for rnd in ("r03", "r02", "r01", ""):
+        path = os.path.join(ROOT, "profiles", rnd, f"pmc_config{cid}{tag}.json")
+        if not os.path.exists(path):
+            continue
+        try:
+            j = json.load(open(path))
+        except Exception:
+            continue
+        src = os.path.relpath(path, ROOT)
+        if j.get("lib_sha16") != sha:
+            return None, src, (f"counters in {src} were taken on libxcsum.so "
+                               f"{j.get('lib_sha16') or '(unrecorded)'}, not this build {sha}")
+        return j.get("hbm_bytes_per_launch"), src, None
+    return None, None, "no PMC summary for this workload under profiles/"
 
 
 def gpu_clocks(dev):
@@ -263,6 +316,54 @@ def stream_ceiling(torch, dev, bufs, sptr):
                     f"two events, median of 5"}
 
 
+def inplace_ceiling(torch, dev, bufs, desc, flags, family, sptr):
+    """Same-run ceiling of the in-place pass: tools/libhbmprobe.so's stream
+    read of the same buffers plus one 2-byte store per frame into its
+    udp->check (and iph->check with IPHDR) field, from the thread that read
+    the chunk holding it (probe_stream_read_inplace).  Frames must sit at a
+    fixed stride (the bench's layouts do).  Writes garbage into the check
+    fields: run it after timing, before the parity pass regenerates the
+    frames."""
+    path = os.path.join(ROOT, "tools", "libhbmprobe.so")
+    a = desc["addr"].astype(np.int64)
+    if not os.path.exists(path) or len(a) < 2:
+        return None
+    fstride = int(a[1] - a[0])
+    if fstride <= 0 or not np.all(np.diff(a) == fstride):
+        return None
+    L = ctypes.CDLL(path)
+    fn = L.probe_stream_read_inplace
+    fn.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64,
+                   ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p,
+                   ctypes.c_int, ctypes.c_void_p]
+    f1 = 60 if family == 6 else 40
+    f2 = 24 if (flags & X.F_IPHDR) and family == 4 else f1
+    cus = torch.cuda.get_device_properties(dev).multi_processor_count
+    blocks = cus * 8
+    scratch = torch.empty(blocks * 256, dtype=torch.int32, device=dev)
+    nbytes = (bufs[0].numel() - 64) & ~15
+    per = max(10, len(bufs))
+    s = torch.cuda.current_stream(dev)
+    ts = []
+    for r in range(6):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(s)
+        for k in range(per):
+            if fn(bufs[k % len(bufs)].data_ptr(), nbytes, fstride, int(a[0]), len(a), f1, f2,
+                  scratch.data_ptr(), blocks, sptr) != 0:
+                return None
+        e1.record(s)
+        torch.cuda.synchronize(dev)
+        ts.append(e0.elapsed_time(e1) / per)
+    t = float(np.median(ts[1:]))
+    return {"ms": round(t, 4), "GBps_read": round(nbytes / (t * 1e-3) / 1e9, 1),
+            "what": f"stream read of the same {nbytes / 1e9:.3f} GB buffer"
+                    f"{'s' if len(bufs) > 1 else ''} + a 2-byte store per frame at eth+{f1}"
+                    f"{f' and eth+{f2}' if f2 != f1 else ''} from the thread that read it "
+                    f"(tools/hbm_probe.hip probe_stream_read_inplace), {per} back-to-back "
+                    f"launches between two events, median of 5"}
+
+
 def digest_check(cfg, out, count, world, rank, dist, sdev):
     """SHA-256 of the timed output against the digest the REFERENCE produced
     over the same synthetic frames (tests/golden/digests.json, made by
@@ -324,7 +425,14 @@ def main():
                     help="untimed back-to-back K-step bodies before timing (clock ramp)")
     ap.add_argument("--no-ceiling", action="store_true",
                     help="skip the same-run streaming-read ceiling probe")
+    ap.add_argument("--flags", default="",
+                    help="comma list of inplace,iphdr,rfc,verify (XCSUM_F_*); with inplace the "
+                         "checks go into the frames and no result array is written, as in "
+                         "libxudp's TX drop-in (tx.c:696-726)")
     args = ap.parse_args()
+    flags = parse_flags(args.flags)
+    # the TX drop-in writes udp->check / iph->check into the frames: no array
+    with_out = not (flags & X.F_INPLACE) or bool(flags & X.F_VERIFY)
 
     import torch
     import torch.distributed as dist
@@ -351,12 +459,13 @@ def main():
     stream = torch.cuda.current_stream(dev)
     sptr = stream.cuda_stream
     desc, d_desc, bufs, out, first, count = build_batch(cfg, rank, world, torch, dev, eng, sptr)
-    alg = X.alg_bytes(desc, cfg["family"])
+    alg = alg_bytes_flags(desc, cfg["family"], flags, with_out)
     len_hint = int(desc["len"].mean()) if count else 0
+    out_arg = out if with_out else None
 
     def step(k):
-        eng.batch_device(bufs[k % len(bufs)], d_desc, count, out, cfg["mode"], 0, len_hint,
-                         stream=sptr)
+        eng.batch_device(bufs[k % len(bufs)], d_desc, count, out_arg, cfg["mode"], flags,
+                         len_hint, stream=sptr)
 
     for k in range(args.warmup):
         step(k)
@@ -375,8 +484,8 @@ def main():
             with torch.cuda.graph(graph, stream=cap):
                 cptr = torch.cuda.current_stream(dev).cuda_stream
                 for k in range(args.steps):
-                    eng.batch_device(bufs[k % len(bufs)], d_desc, count, out, cfg["mode"], 0,
-                                     len_hint, stream=cptr)
+                    eng.batch_device(bufs[k % len(bufs)], d_desc, count, out_arg, cfg["mode"],
+                                     flags, len_hint, stream=cptr)
             stream.wait_stream(cap)
             torch.cuda.synchronize(dev)
         except Exception as e:  # capture unsupported: fall back to eager launches
@@ -397,15 +506,26 @@ def main():
     # ramping clock (round 1: 274 us first replays vs 241 us steady).  So the
     # K-step body runs back to back for at least --ramp-ms of wall time
     # before anything is timed, whatever --warmup says.
+    # It ends once --ramp-ms have passed AND the last three bodies agree
+    # within 1 % (event-timed), or after 4 s: some boxes were still speeding
+    # up after 300 ms (round 3: repetitions 0.268 -> 0.235 ms on one box).
     torch.cuda.synchronize(dev)
     t_r = time.perf_counter()
     n_ramp = 0
+    body_ms = []
     while True:
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
         run_k()
+        e1.record(stream)
         torch.cuda.synchronize(dev)
+        body_ms.append(e0.elapsed_time(e1))
         n_ramp += 1
         ramp_ms = (time.perf_counter() - t_r) * 1e3
-        if ramp_ms >= args.ramp_ms and n_ramp >= 2:
+        last = body_ms[-3:]
+        steady = len(last) == 3 and max(last) <= 1.01 * min(last)
+        if (ramp_ms >= args.ramp_ms and n_ramp >= 2 and (steady or args.ramp_ms <= 0)) \
+                or ramp_ms >= max(4000.0, args.ramp_ms):
             break
     # clocks while the kernel is running: enqueue ~40 ms more, sample, drain
     per_body = ramp_ms / n_ramp
@@ -444,19 +564,40 @@ def main():
     sdev = dev if args.dist_backend == "nccl" else torch.device("cpu")
     wt = torch.tensor(walls, dtype=torch.float64, device=sdev)
     tot = torch.tensor([float(alg), float(count)], dtype=torch.float64, device=sdev)
+    kern_ms = float(np.median(kms))
+    # per rank: its kernel's median launch time, algorithmic bytes and frames
+    mine = torch.tensor([kern_ms, float(alg), float(count)], dtype=torch.float64, device=sdev)
+    per_rank = [mine]
     if world > 1:
         dist.all_reduce(wt, op=dist.ReduceOp.MAX)
         dist.all_reduce(tot, op=dist.ReduceOp.SUM)
+        per_rank = [torch.zeros_like(mine) for _ in range(world)]
+        dist.all_gather(per_rank, mine)
+    per_rank = [[float(x) for x in t.cpu()] for t in per_rank]
     walls_max = [float(x) for x in wt.cpu()]
     elapsed_max = float(np.median(walls_max))
     alg_all, frames_all = float(tot[0]), float(tot[1])
-    kern_ms = float(np.median(kms))
 
-    ceiling = None
+    ceiling = inplace = None
     if rank == 0 and not args.no_ceiling:
         ceiling = stream_ceiling(torch, dev, bufs, sptr)
+        if flags & X.F_INPLACE and with_out is False:
+            inplace = inplace_ceiling(torch, dev, bufs, desc, flags, cfg["family"], sptr)
 
-    # parity spot check of the timed output (rank's last buffer pass)
+    if not with_out and count:
+        # the in-place passes rewrote the check fields of every buffer (and the
+        # probe wrote garbage there): regenerate the frames, then one pass with
+        # the result array as well, which the parity checks read
+        eng.gen_fill_device(bufs[0], d_desc, count, cfg["family"], SEED_BASE ^ cfg["id"], first,
+                            stream=sptr)
+        eng.batch_device(bufs[0], d_desc, count, out, cfg["mode"], flags, len_hint, stream=sptr)
+        torch.cuda.synchronize(dev)
+    else:
+        # the last timed pass may have read another buffer: one more on bufs[0]
+        step(0)
+        torch.cuda.synchronize(dev)
+
+    # parity spot check of the output (and, in place, of the frame bytes)
     ok = None
     if rank == 0 and count:
         import oracle  # checker only
@@ -464,16 +605,40 @@ def main():
         got = out[:m].cpu().numpy().view(np.uint16)
         ubytes = int(desc["addr"][m - 1]) + int(desc["len"][m - 1])
         hu = bufs[0][:ubytes].cpu().numpy()
-        ok = bool(np.array_equal(got, oracle.batch(hu, desc[:m], cfg["mode"])))
-    digest = digest_check(cfg, out, count, world, rank, dist, sdev)
+        if flags & X.F_INPLACE and not flags & X.F_VERIFY:
+            fresh = hu.copy()
+            off = 60 if cfg["family"] == 6 else 40
+            for k in range(m):       # the pristine frames, check fields 0
+                a0 = int(desc["addr"][k])
+                fresh[a0 + off:a0 + off + 2] = 0
+                if flags & X.F_IPHDR and cfg["family"] == 4:
+                    fresh[a0 + 24:a0 + 26] = 0
+            exp = oracle.batch(fresh, desc[:m], cfg["mode"], flags & ~X.F_INPLACE)
+            ok = bool(np.array_equal(got, exp))
+            for k in range(m):
+                a0 = int(desc["addr"][k])
+                ok = ok and int(hu[a0 + off:a0 + off + 2].view("<u2")[0]) == int(exp[k])
+                if flags & X.F_IPHDR and cfg["family"] == 4:
+                    f = fresh[a0:a0 + int(desc["len"][k])]
+                    ok = ok and int(hu[a0 + 24:a0 + 26].view("<u2")[0]) == oracle.ip_header_rfc(f)
+        else:
+            ok = bool(np.array_equal(got, oracle.batch(hu, desc[:m], cfg["mode"], flags)))
+    digest = None if flags & X.F_VERIFY else digest_check(cfg, out, count, world, rank, dist,
+                                                          sdev)
 
+    parity_ok = True
     if rank == 0:
         value = alg_all * args.steps / elapsed_max / 2**30
-        achieved = alg / (kern_ms * 1e-3) / 1e9  # GB/s, this rank's kernel
-        traffic, traffic_src = pmc_traffic(args.config, args.layout)
+        # the slowest rank's kernel sets the fraction (at N = 1: this one)
+        slow = max(per_rank, key=lambda r: r[0])
+        achieved = slow[1] / (slow[0] * 1e-3) / 1e9  # GB/s
+        sha = lib_sha16()
+        traffic, traffic_src, why = pmc_traffic(args.config, args.layout, flags, sha)
         roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                 "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": traffic, "traffic_source": traffic_src}
+        if why:
+            roof["traffic_note"] = why
         # bytes the kernel must move per launch (every 64-byte line holding a
         # frame byte, once, + 16-byte descriptors + 2-byte results): the
         # apples-to-apples numerator for the stream-read ceiling
@@ -484,11 +649,19 @@ def main():
             roof["ceiling_measured"] = ceiling["GBps"]
             roof["frac_vs_ceiling"] = round(roof["real_achieved"] / ceiling["GBps"], 4)
             roof["ceiling_probe"] = ceiling["what"]
+        if inplace:
+            # same buffers, same reads, the same stores per frame, no arithmetic
+            roof["inplace_probe_ms"] = inplace["ms"]
+            roof["frac_vs_inplace_probe"] = round(inplace["ms"] / kern_ms, 4)
+            roof["inplace_probe"] = inplace["what"]
+        parity_ok = ok is not False and (digest is None or digest.get("ok") is not False)
+        fl = ",".join(k for k, v in FLAG_NAMES.items() if flags & v)
         line = {
-            "metric": "device-resident UDP checksum GiB/s + %HBM-peak, 1M x 1472B IPv4 packets"
-                      if args.config == 2 else f"device-resident UDP checksum GiB/s (config "
-                                                f"{args.config})",
-            "value": round(value, 2),
+            "metric": ("device-resident UDP checksum GiB/s + %HBM-peak, 1M x 1472B IPv4 packets"
+                       if args.config == 2 else f"device-resident UDP checksum GiB/s (config "
+                                                f"{args.config})")
+                      + (f" [flags {fl}]" if flags else ""),
+            "value": round(value, 2) if parity_ok else None,
             "unit": "GiB/s",
             "n_gpus": world,
             "steps": args.steps,
@@ -502,6 +675,8 @@ def main():
             "config": {"workload": cfg["name"], "frames_per_gpu": count,
                        "frames_total": int(frames_all), "payload_bytes": [cfg["pmin"], cfg["pmax"]],
                        "family": cfg["family"], "mode": MODE_NAMES[cfg["mode"]],
+                       "flags": fl or "none",
+                       "result_array": with_out,
                        "layout": "packed, 8-byte aligned frames" if args.layout == "packed"
                        else "xudp TX UMEM: one frame per 4096-byte chunk",
                        "visiting_order": "automatic (32 regions of 16-frame tiles if the batch "
@@ -513,15 +688,26 @@ def main():
             "pct_hbm_peak": round(100 * achieved / HBM_PEAK_GBS, 2),
             "mpps": round(frames_all * args.steps / elapsed_max / 1e6, 1),
             "kernel_ms": round(kern_ms, 4),
+            "per_rank": {"ranks": world,
+                         "kernel_ms": [round(r[0], 4) for r in per_rank],
+                         "achieved_GBps": [round(r[1] / (r[0] * 1e-3) / 1e9, 1) for r in per_rank],
+                         "kernel_ms_min_median_max": [round(min(r[0] for r in per_rank), 4),
+                                                      round(float(np.median([r[0] for r in
+                                                                             per_rank])), 4),
+                                                      round(slow[0], 4)],
+                         "frac_from": "the slowest rank's kernel"},
+            "lib_sha16": sha,
             "kernel_ms_reps": [round(x, 4) for x in kms],
             "wall_ms_reps": [round(x * 1e3, 4) for x in walls_max],
             "timing": (f"median of {reps} repetitions of the K steps "
                        f"({'hipGraph replay' if graph is not None else 'eager launches'}), "
                        f"each bracketed by barrier + synchronize"),
             "clock_ramp_ms": round(ramp_ms, 1),
+            "ramp_bodies_ms_last3": [round(x, 3) for x in body_ms[-3:]],
             "clocks": {"under_load": clocks_load, "after_timing": clocks_after},
             "parity_spot_check": ok,
             "parity_digest": digest,
+            "parity_ok": parity_ok,
             "roofline": roof,
         }
         if world == 1 and not args.no_cpu_baseline:
@@ -531,6 +717,9 @@ def main():
     eng.close()
     if world > 1:
         dist.destroy_process_group()
+    if rank == 0 and not parity_ok:
+        print("bench: the output differs from the reference; value withheld", file=sys.stderr)
+        sys.exit(3)
 
 
 if __name__ == "__main__":

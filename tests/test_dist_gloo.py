@@ -82,9 +82,31 @@ def test_bench_helpers_present_and_real_bytes():
     byte count is the union of touched 64-byte lines + 18 bytes per frame."""
     import bench
     for name in ("digest_check", "stream_ceiling", "gpu_clocks", "cpu_baseline", "pmc_traffic",
-                 "host_cpu_facts", "real_bytes", "rank_slice", "build_batch"):
+                 "host_cpu_facts", "real_bytes", "rank_slice", "build_batch", "inplace_ceiling",
+                 "lib_sha16", "parse_flags", "alg_bytes_flags"):
         assert callable(getattr(bench, name)), name
     d = np.zeros(3, dtype=X.DESC_DTYPE)
     d["addr"] = [0, 100, 4096]
     d["len"] = [100, 28, 64]
     assert bench.real_bytes(d) == (2 + 1) * 64 + 3 * 18
+
+
+def test_bench_flags_and_algorithmic_bytes():
+    """--flags parsing and the algorithmic bytes per mode:
+    span + 2-byte result; in place without a result array, + 2 per written
+    check field, + the 12 IPv4 header bytes before the addresses with IPHDR."""
+    import bench
+    assert bench.parse_flags("") == 0
+    assert bench.parse_flags("inplace,iphdr") == X.F_INPLACE | X.F_IPHDR
+    with pytest.raises(SystemExit):
+        bench.parse_flags("bogus")
+    d = np.zeros(2, dtype=X.DESC_DTYPE)
+    d["len"] = [1514, 106]                       # IPv4 payloads 1472 and 64
+    span = (1472 + 16) + (64 + 16)
+    assert bench.alg_bytes_flags(d, 4, 0, True) == span + 4
+    assert bench.alg_bytes_flags(d, 4, X.F_INPLACE, False) == span + 4
+    assert bench.alg_bytes_flags(d, 4, X.F_INPLACE | X.F_IPHDR, False) == span + 24 + 8
+    assert bench.alg_bytes_flags(d, 4, X.F_VERIFY | X.F_IPHDR, True) == span + 24 + 4
+    d6 = np.zeros(1, dtype=X.DESC_DTYPE)
+    d6["len"] = [1534]
+    assert bench.alg_bytes_flags(d6, 6, X.F_INPLACE | X.F_IPHDR, False) == 1472 + 40 + 2

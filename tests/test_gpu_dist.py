@@ -22,12 +22,12 @@ def free_port():
         return s.getsockname()[1]
 
 
-def run_dist(config, steps=2):
+def run_dist(config, steps=2, extra=()):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", str(free_port()),
            os.path.join(ROOT, "bench.py"), "--gpus", "2", "--same-device", "--dist-backend",
            "gloo", "--config", str(config), "--steps", str(steps), "--warmup", "1",
-           "--reps", "2", "--ramp-ms", "0", "--no-ceiling", "--no-cpu-baseline"]
+           "--reps", "2", "--ramp-ms", "0", "--no-ceiling", "--no-cpu-baseline", *extra]
     env = dict(os.environ, MASTER_ADDR="127.0.0.1")
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, cwd=ROOT, env=env)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
@@ -49,3 +49,22 @@ def test_two_ranks_config2_weak_scaling():
     assert line["n_gpus"] == 2 and line["config"]["frames_total"] == 2 << 20
     assert line["scaling"] == "weak"
     assert line["parity_digest"]["ok"] is True
+    check_per_rank(line, 2)
+
+
+def check_per_rank(line, world):
+    """Every rank's kernel time and rate reach rank 0's line; the roofline
+    fraction comes from the slowest rank (an 8-GPU run shows a slow GPU)."""
+    pr = line["per_rank"]
+    assert pr["ranks"] == world and len(pr["kernel_ms"]) == world
+    assert len(pr["achieved_GBps"]) == world and all(v > 0 for v in pr["achieved_GBps"])
+    lo, med, hi = pr["kernel_ms_min_median_max"]
+    assert lo <= med <= hi == max(pr["kernel_ms"])
+    slow = pr["kernel_ms"].index(hi)
+    assert abs(line["roofline"]["achieved"] - pr["achieved_GBps"][slow]) <= 0.2
+    assert line["parity_ok"] is True and line["value"] is not None
+
+
+def test_two_ranks_config5_per_rank_fields():
+    line = run_dist(5)
+    check_per_rank(line, 2)

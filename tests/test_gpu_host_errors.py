@@ -25,6 +25,16 @@ pytestmark = pytest.mark.gpu
 N_OK = 20000          # MTU frames of the first chunk: 30 MB < 32 MiB
 
 
+def rc_of(fn, *args):
+    """fn(*args)'s error code (0: none), keeping no traceback: its frames
+    would hold the UMEM array and keep the mapping exported"""
+    try:
+        fn(*args)
+    except X.XcsumError as e:
+        return e.rc
+    return 0
+
+
 def umem_with_bad_tail(buf):
     """N_OK packed MTU frames in `buf`, then one descriptor of 40 MB (longer
     than a chunk may be: the second chunk's check fails)."""
@@ -46,9 +56,7 @@ def test_batch_host_error_leaves_nothing_in_flight(engine, registered, flags):
     if registered:
         engine.register_umem(arr)
     try:
-        with pytest.raises(X.XcsumError) as e:
-            engine.batch_host(arr, desc, out, X.MODE_V4_RFC, flags)
-        assert e.value.rc == -X.ERR_INVAL
+        assert rc_of(engine.batch_host, arr, desc, out, X.MODE_V4_RFC, flags) == -X.ERR_INVAL
         assert engine.pending() == 0
     finally:
         if registered:
@@ -72,9 +80,7 @@ def test_rx_host_error_leaves_nothing_in_flight(engine, registered):
     if registered:
         engine.register_umem(arr)
     try:
-        with pytest.raises(X.XcsumError) as e:
-            engine.rx_host(arr, desc, msgs, X.F_VERIFY)
-        assert e.value.rc == -X.ERR_INVAL
+        assert rc_of(engine.rx_host, arr, desc, msgs, X.F_VERIFY) == -X.ERR_INVAL
         assert engine.pending() == 0
     finally:
         if registered:

@@ -133,3 +133,60 @@ extern "C" int probe_slot_read(const void *p, uint64_t nslots, uint32_t slot_byt
 			   perm_mul, perm_shift, out);
 	return hipGetLastError() == hipSuccess ? 0 : -1;
 }
+
+/* In-place ceiling (the TX drop-in's mode, XCSUM_F_INPLACE | XCSUM_F_IPHDR):
+ * the stream read of stream_read<true, 1> over the same buffer, plus one
+ * 2-byte store per frame at eth + f1 and one at eth + f2 (udp->check at +40,
+ * iph->check at +24), each issued by the thread that read the chunk holding
+ * it, with a value taken from that chunk -- the write pattern of the
+ * checksum kernel's in-place pass (one dirtied line per field per frame,
+ * interleaved with the read stream) with none of its arithmetic.  Frames
+ * are regular: frame j at j * fstride + off (packed layout, or xudp's
+ * 4096-byte slots).  The candidate frame of a chunk comes from a double
+ * product (exact to far below one frame at these sizes), corrected by one. */
+__device__ __forceinline__ void probe_field_store(uint8_t *p, uint64_t i, u32x4 v, uint64_t fstride,
+						  uint64_t off, uint64_t nframes, uint32_t f,
+						  double inv)
+{
+	const int64_t x = (int64_t)(16 * i) - (int64_t)(off + f);   /* want j*fstride in [x, x+16) */
+	if (x + 16 <= 0)
+		return;
+	int64_t j = x <= 0 ? 0 : (int64_t)((double)x * inv);
+	if ((int64_t)(j * fstride) < x)
+		j++;
+	if (j >= 0 && (uint64_t)j < nframes && (int64_t)(j * fstride) < x + 16)
+		*reinterpret_cast<uint16_t *>(p + j * fstride + off + f) = (uint16_t)(v.x ^ v.w);
+}
+
+__global__ void __launch_bounds__(256) stream_read_inplace(uint8_t *p, uint64_t n16, uint64_t fstride,
+							    uint64_t off, uint64_t nframes,
+							    uint32_t f1, uint32_t f2, double inv,
+							    uint32_t *out)
+{
+	uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+	const uint64_t stride = (uint64_t)gridDim.x * 256;
+	uint32_t acc = 0;
+	for (; i < n16; i += stride) {
+		const u32x4 v = __builtin_nontemporal_load((gu32x4 *)(p + 16 * i));
+		acc += v.x ^ v.y ^ v.z ^ v.w;
+		probe_field_store(p, i, v, fstride, off, nframes, f1, inv);
+		if (f2 != f1)
+			probe_field_store(p, i, v, fstride, off, nframes, f2, inv);
+	}
+	out[(uint64_t)blockIdx.x * 256 + threadIdx.x] = acc;
+}
+
+extern "C" int probe_stream_read_inplace(void *p, uint64_t nbytes, uint64_t fstride, uint64_t off,
+					 uint64_t nframes, uint32_t f1, uint32_t f2, uint32_t *out,
+					 int blocks, void *stream)
+{
+	if (fstride < 16 || !nframes)
+		return -1;
+	/* no store past the buffer: the last frame's fields lie below nbytes */
+	if ((nframes - 1) * fstride + off + (f1 > f2 ? f1 : f2) + 2 > nbytes)
+		return -1;
+	hipLaunchKernelGGL(stream_read_inplace, dim3(blocks), dim3(256), 0, (hipStream_t)stream,
+			   (uint8_t *)p, nbytes / 16, fstride, off, nframes, f1, f2, 1.0 / (double)fstride,
+			   out);
+	return hipGetLastError() == hipSuccess ? 0 : -1;
+}
