@@ -30,6 +30,25 @@ def digests():
     return json.load(open(os.path.join(GOLDEN, "digests.json")))
 
 
+def h2d(torch, arr, dev):
+    """Host array -> device tensor through torch's pinned host memory (cached,
+    never returned to the OS).  Test helpers never hand pageable buffers to
+    the HIP runtime for DMA: it pins such buffers in place and can reuse that
+    pinning for a later buffer at the same addresses after the first one was
+    freed -- the likely cause of the two illegal-address faults seen at a
+    >= 1 MB pageable device-to-host copy."""
+    import numpy as _np
+    return torch.from_numpy(_np.ascontiguousarray(arr)).pin_memory().to(dev)
+
+
+def d2h(t):
+    """Device tensor -> numpy array in pinned host memory (see h2d)."""
+    import torch
+    h = torch.empty(t.shape, dtype=t.dtype, pin_memory=True)
+    h.copy_(t)
+    return h.numpy()
+
+
 def golden_desc(g, sel=None):
     import libxudp_amd as X
     idx = np.arange(len(g["len"])) if sel is None else sel

@@ -3,6 +3,7 @@ import numpy as np
 import pytest
 
 import libxudp_amd as X
+from conftest import h2d, d2h
 import oracle
 from test_build import ROUTES, bfix, split  # noqa: F401
 
@@ -45,16 +46,16 @@ def device_build(torch, engine, route, pays, inplace=False, flags=0, len_hint=0,
         src = src[:off] if off else src
     msgs["len"] = [len(p) for p in pays]
     msgs["slot"] = slots
-    d_umem = torch.from_numpy(umem).to(dev)
-    d_src = torch.from_numpy(np.ascontiguousarray(src)).to(dev)
-    d_msgs = torch.from_numpy(msgs.view(np.uint8)).to(dev)
+    d_umem = h2d(torch, umem, dev)
+    d_src = h2d(torch, np.ascontiguousarray(src), dev)
+    d_msgs = h2d(torch, msgs.view(np.uint8), dev)
     d_desc = torch.zeros(n * 16, dtype=torch.uint8, device=dev)
     d_out = torch.zeros(n, dtype=torch.int16, device=dev)
     engine.build_device(route, d_src, d_msgs, n, d_umem, FRAME, DATA_OFF, d_desc, d_out,
                         flags | (X.F_BUILD_INPLACE if inplace else 0), len_hint)
     torch.cuda.synchronize()
-    return (d_umem.cpu().numpy(), d_desc.cpu().numpy().view(X.DESC_DTYPE),
-            d_out.cpu().numpy().view(np.uint16), umem)
+    return (d2h(d_umem), d2h(d_desc).view(X.DESC_DTYPE),
+            d2h(d_out).view(np.uint16), umem)
 
 
 @pytest.mark.parametrize("fam", [4, 6])

@@ -9,6 +9,7 @@ import pytest
 
 import bench
 import libxudp_amd as X
+from conftest import h2d, d2h
 
 pytestmark = [pytest.mark.gpu, pytest.mark.slow]
 
@@ -22,7 +23,7 @@ def device_batch(torch, engine, cid, first=0, count=None, umem_layout=False):
     desc, nbytes = X.gen_layout(count, cfg["family"], cfg["pmin"], cfg["pmax"],
                                 seed=bench.SEED_BASE ^ cid, first_index=first, **kw)
     dev = torch.device("cuda:0")
-    d_desc = torch.from_numpy(desc.view(np.uint8)).to(dev)
+    d_desc = h2d(torch, desc.view(np.uint8), dev)
     d_umem = torch.empty(nbytes + 64, dtype=torch.uint8, device=dev)
     engine.gen_fill_device(d_umem, d_desc, count, cfg["family"], bench.SEED_BASE ^ cid, first)
     return cfg, desc, d_desc, d_umem
@@ -32,7 +33,7 @@ def run(torch, engine, d_umem, d_desc, n, mode, flags=0, hint=0):
     out = torch.empty(n, dtype=torch.int16, device="cuda:0")
     engine.batch_device(d_umem, d_desc, n, out, mode, flags, hint)
     torch.cuda.synchronize()
-    return out.cpu().numpy().view(np.uint16)
+    return d2h(out).view(np.uint16)
 
 
 def sha(a):
@@ -52,7 +53,7 @@ def test_config_digest(torch_cuda, engine, digests, cid):
     # the frames themselves equal the host generator's (which equals the
     # reference builder's, tests/test_generator.py)
     h = hashlib.sha256()
-    host = d_umem.cpu().numpy()
+    host = d2h(d_umem)
     for d in desc:
         h.update(host[d["addr"]:d["addr"] + d["len"]].tobytes())
     assert h.hexdigest() == dg["sha256_frames"]

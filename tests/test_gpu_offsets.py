@@ -8,6 +8,7 @@ import numpy as np
 import pytest
 
 import libxudp_amd as X
+from conftest import h2d, d2h
 import oracle
 
 pytestmark = pytest.mark.gpu
@@ -45,7 +46,7 @@ def test_checksum_across_2g_and_4g(torch_cuda, engine, big, geom, sizes):
             engine.batch_device(big, d_desc, len(desc), out, X.MODE_V4_LEGACY, 0,
                                 int(desc["len"].mean()))
             torch_cuda.cuda.synchronize()
-            assert np.array_equal(out.cpu().numpy().view(np.uint16), exp), (geom, off)
+            assert np.array_equal(d2h(out).view(np.uint16), exp), (geom, off)
     finally:
         engine.set_geometry(0)
 
@@ -61,7 +62,7 @@ def test_receive_across_2g_and_4g(torch_cuda, engine, big, geometry, monkeypatch
         msgs = torch_cuda.zeros(len(desc) * 64, dtype=torch_cuda.uint8, device="cuda:0")
         engine.rx_device(big, d_desc, len(desc), msgs, None, X.F_VERIFY, 1500)
         torch_cuda.cuda.synchronize()
-        got = msgs.cpu().numpy().view(X.RX_MSG_DTYPE)
+        got = d2h(msgs).view(X.RX_MSG_DTYPE)
         # records hold UMEM offsets: compare with the expected ones moved by off
         e = exp.copy()
         e["frame"] += off
@@ -93,18 +94,18 @@ def test_build_across_2g_and_4g(torch_cuda, engine, big, inplace):
     else:
         src = np.concatenate(pays + [np.zeros(16, np.uint8)])
         msgs["src"] = np.concatenate([[0], np.cumsum([len(p) for p in pays])[:-1]])
-        d_src = torch.from_numpy(src).to("cuda:0")
-    d_msgs = torch.from_numpy(msgs.view(np.uint8)).to("cuda:0")
+        d_src = h2d(torch, src, "cuda:0")
+    d_msgs = h2d(torch, msgs.view(np.uint8), "cuda:0")
     d_desc = torch.zeros(n * 16, dtype=torch.uint8, device="cuda:0")
     d_out = torch.zeros(n, dtype=torch.int16, device="cuda:0")
     engine.build_device(route, d_src, d_msgs, n, big, FRAME, DATA_OFF, d_desc, d_out,
                         X.F_BUILD_INPLACE if inplace else 0, 1500)
     torch.cuda.synchronize()
-    desc = d_desc.cpu().numpy().view(X.DESC_DTYPE)
+    desc = d2h(d_desc).view(X.DESC_DTYPE)
     for i, p in enumerate(pays):
         exp = oracle.build_frame(p.tobytes(), 4, r["smac"], r["dmac"], r["saddr"], r["sport"],
                                  r["daddr"], r["dport"], False)
         eth = int(slots[i]) * FRAME + DATA_OFF - 42
         assert int(desc["addr"][i]) == eth and int(desc["len"][i]) == len(exp)
-        got = big[eth:eth + len(exp)].cpu().numpy()
+        got = d2h(big[eth:eth + len(exp)])
         assert np.array_equal(got, exp), (i, int(slots[i]))

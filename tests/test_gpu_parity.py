@@ -12,7 +12,7 @@ import pytest
 
 import libxudp_amd as X
 import oracle
-from conftest import golden_desc
+from conftest import golden_desc, h2d, d2h
 
 pytestmark = pytest.mark.gpu
 
@@ -37,15 +37,15 @@ def geometry(engine, geom):
 
 def run_device(torch, eng, umem, desc, mode, flags=0, len_hint=0, out=True):
     dev = torch.device("cuda:0")
-    d_umem = torch.from_numpy(umem).to(dev)
-    d_desc = torch.from_numpy(desc.view(np.uint8)).to(dev)
+    d_umem = h2d(torch, umem, dev)
+    d_desc = h2d(torch, desc.view(np.uint8), dev)
     d_out = torch.full((max(len(desc), 1),), 0x5a5a, dtype=torch.int32,
                        device=dev).to(torch.int16) if out else None
     s = torch.cuda.current_stream(dev).cuda_stream
     eng.batch_device(d_umem, d_desc, len(desc), d_out, mode, flags, len_hint, stream=s)
     torch.cuda.synchronize(dev)
-    res = d_out[:len(desc)].cpu().numpy().view(np.uint16) if out else None
-    return res, d_umem.cpu().numpy()
+    res = d2h(d_out[:len(desc)]).view(np.uint16) if out else None
+    return res, d2h(d_umem)
 
 
 @pytest.mark.parametrize("geom", GEOMETRIES)
@@ -167,10 +167,10 @@ def test_device_generator_matches_host(torch_cuda, engine):
             umem, desc = X.gen_frames_host(500, family, 0, 2000, seed=5, first_index=77, **kw)
             dev = torch_cuda.device("cuda:0")
             d_umem = torch_cuda.zeros(len(umem), dtype=torch_cuda.uint8, device=dev)
-            d_desc = torch_cuda.from_numpy(desc.view(np.uint8)).to(dev)
+            d_desc = h2d(torch_cuda, desc.view(np.uint8), dev)
             engine.gen_fill_device(d_umem, d_desc, len(desc), family, 5, 77)
             torch_cuda.cuda.synchronize()
-            assert np.array_equal(d_umem.cpu().numpy(), umem)
+            assert np.array_equal(d2h(d_umem), umem)
 
 
 @pytest.mark.parametrize("geom", FEATURE_GEOMS)
@@ -394,15 +394,15 @@ def test_unaligned_umem_base(torch_cuda, engine, base_off, geom):
         for flags in (0, X.F_INPLACE | X.F_IPHDR, X.F_VERIFY):
             buf = np.zeros(len(umem) + 64, np.uint8)
             buf[base_off:base_off + len(umem)] = umem
-            d_buf = torch_cuda.from_numpy(buf).to(dev)
-            d_desc = torch_cuda.from_numpy(desc.view(np.uint8)).to(dev)
+            d_buf = h2d(torch_cuda, buf, dev)
+            d_desc = h2d(torch_cuda, desc.view(np.uint8), dev)
             d_out = torch_cuda.zeros(len(desc), dtype=torch_cuda.int16, device=dev)
             with geometry(engine, geom):
                 engine.batch_device(d_buf.data_ptr() + base_off, d_desc, len(desc), d_out, mode,
                                     flags, stream=torch_cuda.cuda.current_stream(dev).cuda_stream)
                 torch_cuda.cuda.synchronize(dev)
-            got = d_out.cpu().numpy().view(np.uint16)
+            got = d2h(d_out).view(np.uint16)
             exp = oracle.batch(umem, desc, mode, flags & ~X.F_INPLACE)
             assert np.array_equal(got, exp), (fam, flags, int((got != exp).sum()))
-            after = d_buf.cpu().numpy()
+            after = d2h(d_buf)
             assert not after[:base_off].any() and not after[base_off + len(umem):].any()

@@ -11,6 +11,7 @@ import pytest
 
 import bench
 import libxudp_amd as X
+from conftest import h2d, d2h
 import oracle
 
 pytestmark = pytest.mark.gpu
@@ -32,8 +33,8 @@ def rx():
 
 def run_rx(torch, eng, umem, desc, flags, len_hint=0, geometry=None):
     dev = torch.device("cuda:0")
-    d_umem = torch.from_numpy(umem).to(dev)
-    d_desc = torch.from_numpy(desc.view(np.uint8)).to(dev)
+    d_umem = h2d(torch, umem, dev)
+    d_desc = h2d(torch, desc.view(np.uint8), dev)
     d_msgs = torch.full((max(len(desc), 1) * 64,), 0xA5, dtype=torch.uint8, device=dev)
     d_count = torch.full((1,), 77, dtype=torch.int32, device=dev)
     old = os.environ.get("XCSUM_RX_GEOMETRY")
@@ -48,7 +49,7 @@ def run_rx(torch, eng, umem, desc, flags, len_hint=0, geometry=None):
                 del os.environ["XCSUM_RX_GEOMETRY"]
             else:
                 os.environ["XCSUM_RX_GEOMETRY"] = old
-    recs = d_msgs.cpu().numpy()[:len(desc) * 64].view(X.RX_MSG_DTYPE)
+    recs = d2h(d_msgs)[:len(desc) * 64].view(X.RX_MSG_DTYPE)
     return recs, int(d_count.cpu().item())
 
 
@@ -186,7 +187,7 @@ def test_rx_round_trip_full_size(torch_cuda, engine, cid):
     desc, nbytes = X.gen_layout(n, cfg["family"], cfg["pmin"], cfg["pmax"],
                                 seed=bench.SEED_BASE ^ cid)
     dev = torch_cuda.device("cuda:0")
-    d_desc = torch_cuda.from_numpy(desc.view(np.uint8)).to(dev)
+    d_desc = h2d(torch_cuda, desc.view(np.uint8), dev)
     d_umem = torch_cuda.empty(nbytes + 64, dtype=torch_cuda.uint8, device=dev)
     engine.gen_fill_device(d_umem, d_desc, n, cfg["family"], bench.SEED_BASE ^ cid, 0)
     mode = X.MODE_V6 if cfg["family"] == 6 else X.MODE_V4_RFC
@@ -196,7 +197,7 @@ def test_rx_round_trip_full_size(torch_cuda, engine, cid):
     engine.rx_device(d_umem, d_desc, n, d_msgs, d_count, X.F_VERIFY | X.F_IPHDR,
                      int(desc["len"][0]))
     torch_cuda.cuda.synchronize()
-    recs = d_msgs.cpu().numpy().view(X.RX_MSG_DTYPE)
+    recs = d2h(d_msgs).view(X.RX_MSG_DTYPE)
     assert int(d_count.item()) == n
     assert (recs["status"] == X.RX_OK).all()
     hdr = 42 if cfg["family"] == 4 else 62
@@ -207,7 +208,7 @@ def test_rx_round_trip_full_size(torch_cuda, engine, cid):
     d_umem[last] ^= 0x10
     engine.rx_device(d_umem, d_desc, n, d_msgs, d_count, X.F_VERIFY, int(desc["len"][0]))
     torch_cuda.cuda.synchronize()
-    recs = d_msgs.cpu().numpy().view(X.RX_MSG_DTYPE)
+    recs = d2h(d_msgs).view(X.RX_MSG_DTYPE)
     assert int(d_count.item()) == 0
     assert (recs["status"] == X.RX_CSUM).all()
 
