@@ -560,7 +560,8 @@ static int ensure_staging(xcsum_ctx *c)
 static int ensure_gather(xcsum_ctx *c)
 {
 	for (int s = 0; s < Ctx::NSLOT; s++) {
-		if (!c->h_stage[s] && hipHostMalloc(&c->h_stage[s], c->frame_cap, PINNED_FLAGS) != hipSuccess)
+		/* + 64: a range copy is up to frame_cap + 15 bytes (16-aligned start) */
+		if (!c->h_stage[s] && hipHostMalloc(&c->h_stage[s], c->frame_cap + 64, PINNED_FLAGS) != hipSuccess)
 			return -XCSUM_ERR_NOMEM;
 		if (!c->h_dstage[s] &&
 		    hipHostMalloc(&c->h_dstage[s], c->desc_cap * sizeof(struct xcsum_desc), PINNED_FLAGS) !=
@@ -620,6 +621,36 @@ static const Region *zerocopy_pays(const xcsum_ctx *c, const uint8_t *h_umem,
 static inline uint64_t stage_off(uint64_t pos, uint64_t addr)
 {
 	return ((pos + 15) & ~(uint64_t)15) + (addr & 15);
+}
+
+/* The source of a host-to-device copy of caller memory [p, p + n): the
+ * memory itself when it lies in a registered region (page-locked by
+ * xcsum_register_umem: the DMA reads it in place), else a copy in the slot's
+ * pinned stage.  Unregistered (pageable) caller memory is never handed to
+ * the copy engine: for copies of 1 MiB and more the HIP runtime pins such
+ * memory in place and keeps that pinning for later copies
+ * (tools/diag_pinning.py: "HSA Copy Using Pinned resource" from 1.5 MB up),
+ * and a caller that frees the buffer and gets the same addresses back for
+ * another one would have a later copy go through the stale pinning -- the
+ * likely cause of the illegal-address faults of DESIGN.md 6.  The slot's
+ * previous copy has completed (its event was waited for) before the stage
+ * is overwritten. */
+static const void *host_dma_src(xcsum_ctx *c, int slot, const uint8_t *p, uint64_t n)
+{
+	if (find_region(c, p, p + n))
+		return p;
+	memcpy(c->h_stage[slot], p, n);
+	return c->h_stage[slot];
+}
+
+/* the same for a descriptor range (up to 1 MiB per chunk) */
+static const void *host_desc_src(xcsum_ctx *c, int slot, const struct xcsum_desc *d, uint32_t n)
+{
+	const uint8_t *p = (const uint8_t *)d;
+	if (find_region(c, p, p + (uint64_t)n * sizeof(*d)))
+		return d;
+	memcpy(c->h_dstage[slot], d, (size_t)n * sizeof(*d));
+	return c->h_dstage[slot];
 }
 
 /* udp->check / iph->check offsets of a frame for the resolved family */
@@ -733,7 +764,9 @@ static int batch_host_run(xcsum_ctx *c, uint8_t *h_umem, const struct xcsum_desc
 
 	if (zc)
 		gather = false;
-	if (gather && (rc = ensure_gather(c)))
+	/* the pinned stages: every byte that crosses PCIe from unregistered
+	 * caller memory goes through them (see host_dma_src) */
+	if ((rc = ensure_gather(c)))
 		return rc;
 
 	/* zero-copy + INPLACE: the kernel already wrote the host frames */
@@ -823,7 +856,8 @@ static int batch_host_run(xcsum_ctx *c, uint8_t *h_umem, const struct xcsum_desc
 			/* 16-byte aligned copy of [lo, hi) keeps every frame's address
 			 * parity and 16-byte phase identical to the host UMEM */
 			uint64_t alo = lo & ~(uint64_t)15;
-			HIPCHK(hipMemcpyAsync(c->d_frames[slot], h_umem + alo, hi - alo,
+			HIPCHK(hipMemcpyAsync(c->d_frames[slot],
+					      host_dma_src(c, slot, h_umem + alo, hi - alo), hi - alo,
 					      hipMemcpyHostToDevice, st));
 			a.umem = c->d_frames[slot];
 			a.bias = alo;
@@ -831,7 +865,8 @@ static int batch_host_run(xcsum_ctx *c, uint8_t *h_umem, const struct xcsum_desc
 			a.flags = flags & (XCSUM_F_IPHDR | XCSUM_F_V4_RFC | XCSUM_F_VERIFY);
 		}
 		if (!direct)
-			HIPCHK(hipMemcpyAsync(c->d_desc[slot], gather ? c->h_dstage[slot] : h_desc + i,
+			HIPCHK(hipMemcpyAsync(c->d_desc[slot], gather ? c->h_dstage[slot]
+							       : host_desc_src(c, slot, h_desc + i, cnt),
 					      cnt * sizeof(struct xcsum_desc), hipMemcpyHostToDevice, st));
 		uint32_t avg = (uint32_t)((gather ? gpos : hi - lo) / cnt);
 		HIPCHK(launch_csum(a, geometry_for(c, avg, a.flags), c->cus, st));
@@ -962,7 +997,7 @@ static int rx_host_run(xcsum_ctx *c, const uint8_t *h_umem, const struct xcsum_d
 			zc = nullptr;
 	}
 	const bool gather = !zc && gather_pays(c, h_umem, blo, bhi, bsum);
-	if (gather && (rc = ensure_gather(c)))
+	if ((rc = ensure_gather(c)))   /* the pinned stages (host_dma_src) */
 		return rc;
 	Pending pend[Ctx::NSLOT];
 	for (int s = 0; s < Ctx::NSLOT; s++)
@@ -1044,12 +1079,14 @@ static int rx_host_run(xcsum_ctx *c, const uint8_t *h_umem, const struct xcsum_d
 			/* 16-byte aligned copy of [lo, hi): every frame keeps its
 			 * address phase; the kernel sees umem + addr inside it */
 			const uint64_t alo = lo & ~(uint64_t)15;
-			HIPCHK(hipMemcpyAsync(c->d_frames[slot], h_umem + alo, hi - alo,
+			HIPCHK(hipMemcpyAsync(c->d_frames[slot],
+					      host_dma_src(c, slot, h_umem + alo, hi - alo), hi - alo,
 					      hipMemcpyHostToDevice, st));
 			a.umem = (const uint8_t *)((uintptr_t)c->d_frames[slot] - (uintptr_t)alo);
 		}
 		if (!direct)
-			HIPCHK(hipMemcpyAsync(c->d_desc[slot], gather ? c->h_dstage[slot] : h_desc + i,
+			HIPCHK(hipMemcpyAsync(c->d_desc[slot], gather ? c->h_dstage[slot]
+							       : host_desc_src(c, slot, h_desc + i, cnt),
 					      cnt * sizeof(struct xcsum_desc), hipMemcpyHostToDevice, st));
 		a.n = cnt;
 		a.flags = flags & (XCSUM_F_VERIFY | XCSUM_F_IPHDR);

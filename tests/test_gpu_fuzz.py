@@ -146,4 +146,14 @@ def host_fuzz_case(torch_cuda, engine, seed):
     bad = np.nonzero(out != exp)[0]
     assert len(bad) == 0, f"seed {seed}: mode {mode} flags {flags:#x} zerocopy {zerocopy}: " \
                           f"frames {bad[:8].tolist()}"
-    assert np.array_equal(host, exp_after), f"seed {seed}: in-place bytes differ"
+    if not np.array_equal(host, exp_after):
+        diff = np.nonzero(host != exp_after)[0]
+        starts = desc["addr"].astype(np.int64)
+        where = []
+        for o in diff[:6].tolist():
+            k = int(np.searchsorted(np.sort(starts), o, side="right")) - 1
+            a0 = int(np.sort(starts)[k]) if k >= 0 else -1
+            where.append(f"byte {o} (frame at {a0} +{o - a0}): host {host[o]} device "
+                         f"{exp_after[o]} original {umem[o]}")
+        raise AssertionError(f"seed {seed}: {len(diff)} in-place bytes differ "
+                             f"(zerocopy {zerocopy}, flags {flags:#x}): " + "; ".join(where))

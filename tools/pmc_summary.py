@@ -46,6 +46,11 @@ def main():
     ap.add_argument("--write", required=True)
     ap.add_argument("--alg-bytes", type=float, required=True)
     ap.add_argument("--out", default="")
+    ap.add_argument("--flags", type=lambda v: int(v, 0), default=0,
+                    help="the bench's XCSUM_F_* flags (file name tag _f<hex>)")
+    ap.add_argument("--lib-sha", default="",
+                    help="SHA-256 prefix of the profiled libxcsum.so (bench.py lib_sha16); "
+                         "bench.py reports the counters only for that very build")
     args = ap.parse_args()
     fetch = counter_values(args.fetch, "FETCH_SIZE")
     write = counter_values(args.write, "WRITE_SIZE")
@@ -58,10 +63,12 @@ def main():
            "FETCH_SIZE_KiB_median": f_kib, "WRITE_SIZE_KiB_median": w_kib,
            "hbm_bytes_per_launch": round(hbm), "alg_bytes_per_launch": args.alg_bytes,
            "traffic_over_alg": round(hbm / args.alg_bytes, 4),
+           "flags": args.flags, "lib_sha16": args.lib_sha or None,
            "formula": "(2*FETCH_SIZE + WRITE_SIZE) * 1024  (gfx950 FETCH_SIZE = half of "
                       "wide streaming read bytes, MI355X_MICROARCH.md HBM)"}
     out = args.out or os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(
-        __file__))), "profiles", "r02", f"pmc_config{args.config}.json")
+        __file__))), "profiles", "r03",
+        f"pmc_config{args.config}{'_f%x' % args.flags if args.flags else ''}.json")
     json.dump(rec, open(out, "w"), indent=1)
     print(json.dumps(rec))
 
