@@ -1,30 +1,50 @@
 #!/bin/bash
-# Round profile refresh on the GPU box (each GPU step under its own timeout,
-# stop at the first fault/timeout via tools/gpu_run.sh):
-#   bench.py JSON per config (the driver's exact command for config 2),
-#   rocprofv3 --kernel-trace --stats per config, separate FETCH_SIZE /
-#   WRITE_SIZE PMC passes for configs 2 and 3.
+# Round profile refresh on the GPU box (each GPU step under its own time limit
+# via tools/gpu_run.sh, which stops the chain at a fault or time-out):
+#   the bench line under the driver's exact command; bench lines per config,
+#   xudp's slot layout and the in-place mode; rocprofv3 --kernel-trace --stats
+#   per workload; separate FETCH_SIZE / WRITE_SIZE PMC passes per workload,
+#   summarised into profiles-ready JSON (tools/pmc_summary.py, tied to the
+#   library's SHA-256 prefix).
 #   tools/profile_round.sh <outdir under gpurun_out>
-set -e
+set -eu
 out="$1"; mkdir -p "gpurun_out/$out"
 export TMPDIR=/tmp
+SHA=$(python3 -c "import bench; print(bench.lib_sha16())")
+B="python3 bench.py --no-cpu-baseline"
 tools/gpu_run.sh $out/bench_driver_cmd 300 python bench.py --gpus 1 --steps 20 --warmup 5
 for c in 2 3 4 5; do
-  tools/gpu_run.sh $out/bench_config$c 300 python bench.py --config $c --steps 100 --no-cpu-baseline
+  tools/gpu_run.sh $out/bench_config$c 300 $B --config $c --steps 100
 done
-tools/gpu_run.sh $out/bench_config2_umem 300 python bench.py --config 2 --layout umem --no-cpu-baseline
-tools/gpu_run.sh $out/bench_config3_umem 300 python bench.py --config 3 --layout umem --no-cpu-baseline
-for c in 2 3 4 5; do
-  tools/gpu_run.sh $out/stats$c 300 rocprofv3 --kernel-trace --stats --output-format csv \
-      -d gpurun_out/$out/stats$c -o run -- python3 bench.py --config $c --steps 20 --warmup 5 --no-cpu-baseline
+tools/gpu_run.sh $out/bench_config2_umem 300 $B --config 2 --layout umem --steps 100
+for c in 2 4; do
+  tools/gpu_run.sh $out/bench_config${c}_inplace 300 $B --config $c --steps 100 --flags inplace,iphdr
 done
-for c in 2 3; do
-  tools/gpu_run.sh $out/fetch$c 300 rocprofv3 --pmc FETCH_SIZE --output-format csv \
-      -d gpurun_out/$out/fetch$c -o run -- python3 bench.py --config $c --steps 10 --warmup 2 --no-cpu-baseline --no-graph --ramp-ms 0 --reps 1 --no-ceiling
-  tools/gpu_run.sh $out/write$c 300 rocprofv3 --pmc WRITE_SIZE --output-format csv \
-      -d gpurun_out/$out/write$c -o run -- python3 bench.py --config $c --steps 10 --warmup 2 --no-cpu-baseline --no-graph --ramp-ms 0 --reps 1 --no-ceiling
+# name:bench args
+WL="c2:--config 2|c3:--config 3|c4:--config 4|c5:--config 5|c2_inplace:--config 2 --flags inplace,iphdr"
+IFS='|' read -ra wls <<< "$WL"
+for w in "${wls[@]}"; do
+  n=${w%%:*}; a=${w#*:}
+  tools/gpu_run.sh $out/stats_$n 300 rocprofv3 --kernel-trace --stats --output-format csv \
+      -d gpurun_out/$out/stats_$n -o run -- $B $a --steps 20 --warmup 5
 done
-# receive kernels: every mode on configs 2, 4, 3, 5, and rocprofv3 stats of config 2
-tools/gpu_run.sh $out/bench_rx 300 python tools/bench_rx.py --configs 2,4,3,5
-tools/gpu_run.sh $out/rx_stats2 300 rocprofv3 --kernel-trace --stats --output-format csv \
-    -d gpurun_out/$out/rx_stats2 -o run -- python3 tools/bench_rx.py --configs 2 --reps 5
+for w in "${wls[@]}"; do
+  n=${w%%:*}; a=${w#*:}
+  P="$B $a --steps 10 --warmup 2 --no-graph --ramp-ms 0 --reps 1 --no-ceiling"
+  tools/gpu_run.sh $out/fetch_$n 120 rocprofv3 --pmc FETCH_SIZE --output-format csv \
+      -d gpurun_out/$out/fetch_$n -o run -- $P
+  tools/gpu_run.sh $out/write_$n 120 rocprofv3 --pmc WRITE_SIZE --output-format csv \
+      -d gpurun_out/$out/write_$n -o run -- $P
+  cid=$(echo "$a" | sed -n 's/.*--config \([0-9]\).*/\1/p')
+  fl=$(echo "$a" | grep -q inplace && echo 0x3 || echo 0)
+  alg=$(python3 -c "
+import bench, libxudp_amd as X
+cfg = dict(bench.CONFIGS[$cid], id=$cid)
+desc, _ = X.gen_layout(cfg['n'], cfg['family'], cfg['pmin'], cfg['pmax'], seed=bench.SEED_BASE ^ $cid)
+f = $fl
+print(bench.alg_bytes_flags(desc, cfg['family'], f, not (f & X.F_INPLACE)))")
+  python3 tools/pmc_summary.py --config $cid --flags $fl --lib-sha $SHA --alg-bytes $alg \
+      --fetch "$(find gpurun_out/$out/fetch_$n -name "*counter_collection.csv" -print -quit)" \
+      --write "$(find gpurun_out/$out/write_$n -name "*counter_collection.csv" -print -quit)" \
+      --out gpurun_out/$out/pmc_$n.json > gpurun_out/$out/pmc_$n.log 2>&1 || true
+done
