@@ -335,7 +335,7 @@ def inplace_ceiling(torch, dev, bufs, desc, flags, family, sptr):
     fn = L.probe_stream_read_inplace
     fn.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64,
                    ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p,
-                   ctypes.c_int, ctypes.c_void_p]
+                   ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
     f1 = 60 if family == 6 else 40
     f2 = 24 if (flags & X.F_IPHDR) and family == 4 else f1
     cus = torch.cuda.get_device_properties(dev).multi_processor_count
@@ -344,24 +344,29 @@ def inplace_ceiling(torch, dev, bufs, desc, flags, family, sptr):
     nbytes = (bufs[0].numel() - 64) & ~15
     per = max(10, len(bufs))
     s = torch.cuda.current_stream(dev)
-    ts = []
-    for r in range(6):
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record(s)
-        for k in range(per):
-            if fn(bufs[k % len(bufs)].data_ptr(), nbytes, fstride, int(a[0]), len(a), f1, f2,
-                  scratch.data_ptr(), blocks, sptr) != 0:
-                return None
-        e1.record(s)
-        torch.cuda.synchronize(dev)
-        ts.append(e0.elapsed_time(e1) / per)
-    t = float(np.median(ts[1:]))
-    return {"ms": round(t, 4), "GBps_read": round(nbytes / (t * 1e-3) / 1e9, 1),
+    by_unroll = {}
+    for unroll in (1, 4):           # 1 or 4 chunks in flight per thread, the faster counts
+        ts = []
+        for r in range(6):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(s)
+            for k in range(per):
+                if fn(bufs[k % len(bufs)].data_ptr(), nbytes, fstride, int(a[0]), len(a), f1, f2,
+                      scratch.data_ptr(), blocks, unroll, sptr) != 0:
+                    return None
+            e1.record(s)
+            torch.cuda.synchronize(dev)
+            ts.append(e0.elapsed_time(e1) / per)
+        by_unroll[unroll] = float(np.median(ts[1:]))
+    t = min(by_unroll.values())
+    return {"ms": round(t, 4), "ms_by_unroll": {str(k): round(v, 4) for k, v in by_unroll.items()},
+            "GBps_read": round(nbytes / (t * 1e-3) / 1e9, 1),
             "what": f"stream read of the same {nbytes / 1e9:.3f} GB buffer"
                     f"{'s' if len(bufs) > 1 else ''} + a 2-byte store per frame at eth+{f1}"
                     f"{f' and eth+{f2}' if f2 != f1 else ''} from the thread that read it "
-                    f"(tools/hbm_probe.hip probe_stream_read_inplace), {per} back-to-back "
-                    f"launches between two events, median of 5"}
+                    f"(tools/hbm_probe.hip probe_stream_read_inplace, 1 or 4 chunks in flight "
+                    f"per thread, the faster), {per} back-to-back launches between two events, "
+                    f"median of 5"}
 
 
 def digest_check(cfg, out, count, world, rank, dist, sdev):
@@ -652,6 +657,7 @@ def main():
         if inplace:
             # same buffers, same reads, the same stores per frame, no arithmetic
             roof["inplace_probe_ms"] = inplace["ms"]
+            roof["inplace_probe_ms_by_unroll"] = inplace["ms_by_unroll"]
             roof["frac_vs_inplace_probe"] = round(inplace["ms"] / kern_ms, 4)
             roof["inplace_probe"] = inplace["what"]
         parity_ok = ok is not False and (digest is None or digest.get("ok") is not False)

@@ -110,3 +110,38 @@ def test_bench_flags_and_algorithmic_bytes():
     d6 = np.zeros(1, dtype=X.DESC_DTYPE)
     d6["len"] = [1534]
     assert bench.alg_bytes_flags(d6, 6, X.F_INPLACE | X.F_IPHDR, False) == 1472 + 40 + 2
+
+
+def test_pmc_traffic_only_from_the_same_library(tmp_path, monkeypatch):
+    """roofline.traffic comes from a committed PMC summary only when it was
+    taken on this very library (SHA-256 prefix); otherwise null + reason."""
+    import json
+    import bench
+    monkeypatch.setattr(bench, "ROOT", str(tmp_path))
+    d = tmp_path / "profiles" / "r03"
+    d.mkdir(parents=True)
+    (d / "pmc_config2.json").write_text(json.dumps({"hbm_bytes_per_launch": 123,
+                                                    "lib_sha16": "aaaa"}))
+    assert bench.pmc_traffic(2, "packed", 0, "aaaa")[0] == 123
+    t, src, why = bench.pmc_traffic(2, "packed", 0, "bbbb")
+    assert t is None and src.endswith("pmc_config2.json") and "aaaa" in why
+    t, src, why = bench.pmc_traffic(3, "packed", 0, "aaaa")
+    assert t is None and src is None and why
+    (d / "pmc_config2_f3.json").write_text(json.dumps({"hbm_bytes_per_launch": 7,
+                                                       "lib_sha16": "aaaa"}))
+    assert bench.pmc_traffic(2, "packed", X.F_INPLACE | X.F_IPHDR, "aaaa")[0] == 7
+
+
+def test_cpu_baseline_legs_report_their_seconds():
+    """cpu_baseline times every leg after an untimed warm repetition and
+    reports each leg's measured seconds and the usable cores; the sample
+    text is generated from those numbers."""
+    import bench
+    cfg = dict(bench.CONFIGS[3], id=3, n=4096)
+    r = bench.cpu_baseline(cfg, seconds=0.6)
+    assert r["unit"] == "GiB/s" and r["value"] > 0 and r["cores"] >= 1
+    assert set(r["seconds_by_threads"]) == set(r["by_threads"])
+    assert r["cores_usable"] >= 1
+    assert r["seconds_total"] < 10
+    for th, sec in r["seconds_by_threads"].items():
+        assert f"{th} thread" in r["sample"] and sec > 0

@@ -158,6 +158,7 @@ __device__ __forceinline__ void probe_field_store(uint8_t *p, uint64_t i, u32x4 
 		*reinterpret_cast<uint16_t *>(p + j * fstride + off + f) = (uint16_t)(v.x ^ v.w);
 }
 
+template <int UNROLL>
 __global__ void __launch_bounds__(256) stream_read_inplace(uint8_t *p, uint64_t n16, uint64_t fstride,
 							    uint64_t off, uint64_t nframes,
 							    uint32_t f1, uint32_t f2, double inv,
@@ -166,6 +167,20 @@ __global__ void __launch_bounds__(256) stream_read_inplace(uint8_t *p, uint64_t 
 	uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
 	const uint64_t stride = (uint64_t)gridDim.x * 256;
 	uint32_t acc = 0;
+	/* UNROLL chunks in flight per thread, then their stores */
+	for (; i + (UNROLL - 1) * stride < n16; i += UNROLL * stride) {
+		u32x4 v[UNROLL];
+#pragma unroll
+		for (int u = 0; u < UNROLL; u++)
+			v[u] = __builtin_nontemporal_load((gu32x4 *)(p + 16 * (i + u * stride)));
+#pragma unroll
+		for (int u = 0; u < UNROLL; u++) {
+			acc += v[u].x ^ v[u].y ^ v[u].z ^ v[u].w;
+			probe_field_store(p, i + u * stride, v[u], fstride, off, nframes, f1, inv);
+			if (f2 != f1)
+				probe_field_store(p, i + u * stride, v[u], fstride, off, nframes, f2, inv);
+		}
+	}
 	for (; i < n16; i += stride) {
 		const u32x4 v = __builtin_nontemporal_load((gu32x4 *)(p + 16 * i));
 		acc += v.x ^ v.y ^ v.z ^ v.w;
@@ -178,15 +193,22 @@ __global__ void __launch_bounds__(256) stream_read_inplace(uint8_t *p, uint64_t 
 
 extern "C" int probe_stream_read_inplace(void *p, uint64_t nbytes, uint64_t fstride, uint64_t off,
 					 uint64_t nframes, uint32_t f1, uint32_t f2, uint32_t *out,
-					 int blocks, void *stream)
+					 int blocks, int unroll, void *stream)
 {
 	if (fstride < 16 || !nframes)
 		return -1;
 	/* no store past the buffer: the last frame's fields lie below nbytes */
 	if ((nframes - 1) * fstride + off + (f1 > f2 ? f1 : f2) + 2 > nbytes)
 		return -1;
-	hipLaunchKernelGGL(stream_read_inplace, dim3(blocks), dim3(256), 0, (hipStream_t)stream,
-			   (uint8_t *)p, nbytes / 16, fstride, off, nframes, f1, f2, 1.0 / (double)fstride,
-			   out);
+#define L(U_) hipLaunchKernelGGL((stream_read_inplace<U_>), dim3(blocks), dim3(256), 0,           \
+				    (hipStream_t)stream, (uint8_t *)p, nbytes / 16, fstride, off, nframes, \
+				    f1, f2, 1.0 / (double)fstride, out)
+	if (unroll >= 4)
+		L(4);
+	else if (unroll >= 2)
+		L(2);
+	else
+		L(1);
+#undef L
 	return hipGetLastError() == hipSuccess ? 0 : -1;
 }
