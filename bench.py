@@ -190,12 +190,17 @@ def cpu_baseline(cfg, seconds=15.0):
     res, secs = {}, {}
     t_start = time.perf_counter()
     for th, share in legs:
-        timed(th, 1)                       # warm: threads, page faults, caches
-        t1 = timed(th, 1)
-        reps = max(1, int(seconds * share / max(t1, 1e-6)))
-        t = timed(th, reps)
+        # warm (threads, page faults, caches), then grow the repetition count
+        # until one timed run fills the leg's share: sizing from a single short
+        # run undershot by 10x on the box (thread start-up, cgroup quota)
+        timed(th, 1)
+        target = seconds * share
+        reps, t = 1, timed(th, 1)
+        while t < 0.8 * target and reps < (1 << 24):
+            reps = max(reps + 1, int(reps * target / max(t, 1e-4)) if t >= 0.05 else reps * 10)
+            t = timed(th, reps)
         res[th] = alg * reps / t / 2**30
-        secs[th] = round(t + 2 * t1, 3)
+        secs[th] = round(t, 3)
     total = time.perf_counter() - t_start
     exp = oracle.ref_batch(umem, desc, mode) if kind == "reference" else oracle.batch(umem, desc,
                                                                                         mode)
@@ -210,8 +215,8 @@ def cpu_baseline(cfg, seconds=15.0):
             "value_1core": round(res[1], 3), **facts,
             "sample": f"{m} frames of the same config ({alg / 1e6:.1f} MB algorithmic), "
                       f"xudp/checksum.h {'udp_csum6' if mode == 2 else 'udp_checksum'} compiled "
-                      f"-O2 from the reference, static frame partition; legs: {legs_txt} "
-                      f"({total:.1f} s in all, warm-up repetitions included); "
+                      f"-O2 from the reference, static frame partition; timed legs: {legs_txt} "
+                      f"({total:.1f} s in all with the warm-up and sizing runs); "
                       f"{usable:g} CPUs usable by this job (affinity / cgroup quota), so "
                       f"thread counts above that time-slice; value = the fastest leg"}
 
