@@ -624,18 +624,6 @@ static inline uint64_t stage_off(uint64_t pos, uint64_t addr)
 	return ((pos + 15) & ~(uint64_t)15) + (addr & 15);
 }
 
-/* The source of a host-to-device copy of caller memory [p, p + n): the
- * memory itself when it lies in a registered region (page-locked by
- * xcsum_register_umem: the DMA reads it in place), else a copy in the slot's
- * pinned stage.  Unregistered (pageable) caller memory is never handed to
- * the copy engine: for copies of 1 MiB and more the HIP runtime pins such
- * memory in place and keeps that pinning for later copies
- * (tools/diag_pinning.py: "HSA Copy Using Pinned resource" from 1.5 MB up),
- * and a caller that frees the buffer and gets the same addresses back for
- * another one would have a later copy go through the stale pinning -- the
- * likely cause of the illegal-address faults of DESIGN.md 6.  The slot's
- * previous copy has completed (its event was waited for) before the stage
- * is overwritten. */
 /* memcpy into a pinned stage, split over up to STAGE_THREADS threads from
  * 4 MiB up: one thread copies ~25 GB/s here, under the ~57 GB/s PCIe moves
  * (config 2 frames, pageable, tools/bench_e2e.py: 23.0 GiB/s with one thread) */
@@ -672,6 +660,17 @@ static void stage_copy(uint8_t *dst, const uint8_t *src, uint64_t n)
 			th[t].join();
 }
 
+/* The source of a host-to-device copy of caller memory [p, p + n): the
+ * memory itself when it lies in a registered region (page-locked by
+ * xcsum_register_umem: the DMA reads it in place), else a copy in the slot's
+ * pinned stage.  Unregistered (pageable) caller memory is never handed to
+ * the copy engine: for copies of 1 MiB and more the HIP runtime pins such
+ * memory in place (tools/diag_pinning.py: "HSA Copy Using Pinned resource"
+ * from 1.5 MB up), and a pinning that outlives the caller's buffer -- freed,
+ * its addresses handed to another buffer -- is the likely cause of the
+ * illegal-address faults of DESIGN.md 6.  The slot's
+ * previous copy has completed (its event was waited for) before the stage
+ * is overwritten. */
 static const void *host_dma_src(xcsum_ctx *c, int slot, const uint8_t *p, uint64_t n)
 {
 	if (find_region(c, p, p + n))
