@@ -83,12 +83,38 @@ def alg_bytes_flags(desc, family, flags, with_out):
     return read + 2 * len(desc) * ((1 if with_out else 0) + fields)
 
 
+def elf_section(path, name):
+    """Bytes of one section of an ELF64 little-endian file (None if absent)."""
+    import struct
+    with open(path, "rb") as f:
+        data = f.read()
+    if data[:4] != b"\x7fELF" or data[4] != 2:
+        return None
+    shoff, = struct.unpack_from("<Q", data, 0x28)
+    shentsize, shnum, shstrndx = struct.unpack_from("<HHH", data, 0x3A)
+    def sect(i):
+        # sh_name, sh_type, sh_flags, sh_addr, sh_offset, sh_size
+        return struct.unpack_from("<IIQQQQ", data, shoff + i * shentsize)
+    stroff = sect(shstrndx)[4]
+    for i in range(shnum):
+        nm, _, _, _, off, size = sect(i)
+        end = data.index(b"\0", stroff + nm)
+        if data[stroff + nm:end].decode() == name:
+            return data[off:off + size]
+    return None
+
+
 def lib_sha16():
-    """SHA-256 prefix of the loaded libxcsum.so: ties committed PMC counters
-    to the binary that was timed"""
+    """SHA-256 prefix of the loaded libxcsum.so's device code (its
+    .hip_fatbin section, every gfx950 kernel): ties committed PMC counters to
+    the kernels that were timed.  Host-code edits (error-line numbers
+    included) leave it unchanged; falls back to the whole file."""
     import hashlib
-    with open(X.LIB_PATH, "rb") as f:
-        return hashlib.sha256(f.read()).hexdigest()[:16]
+    sec = elf_section(X.LIB_PATH, ".hip_fatbin")
+    if sec is None:
+        with open(X.LIB_PATH, "rb") as f:
+            sec = f.read()
+    return hashlib.sha256(sec).hexdigest()[:16]
 
 
 def dist_env():
@@ -707,7 +733,7 @@ def main():
                                                                              per_rank])), 4),
                                                       round(slow[0], 4)],
                          "frac_from": "the slowest rank's kernel"},
-            "lib_sha16": sha,
+            "lib_sha16": sha,   # of the kernels (.hip_fatbin), see lib_sha16()
             "kernel_ms_reps": [round(x, 4) for x in kms],
             "wall_ms_reps": [round(x * 1e3, 4) for x in walls_max],
             "timing": (f"median of {reps} repetitions of the K steps "

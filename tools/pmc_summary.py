@@ -49,8 +49,9 @@ def main():
     ap.add_argument("--flags", type=lambda v: int(v, 0), default=0,
                     help="the bench's XCSUM_F_* flags (file name tag _f<hex>)")
     ap.add_argument("--lib-sha", default="",
-                    help="SHA-256 prefix of the profiled libxcsum.so (bench.py lib_sha16); "
-                         "bench.py reports the counters only for that very build")
+                    help="SHA-256 prefix of the profiled libxcsum.so's device code "
+                         "(bench.py lib_sha16: its .hip_fatbin section); bench.py reports the "
+                         "counters only for those very kernels")
     args = ap.parse_args()
     fetch = counter_values(args.fetch, "FETCH_SIZE")
     write = counter_values(args.write, "WRITE_SIZE")
