@@ -234,8 +234,10 @@ int xcsum_rx_host(xcsum_ctx *ctx, const uint8_t *h_umem, const struct xcsum_desc
 
 /* ---- host-resident batch (frames in the AF_XDP UMEM) ----------------------
  * Same semantics with host pointers.  Synchronous.  Frames are moved with
- * chunked, double-buffered hipMemcpyAsync (pinned when the UMEM range is
- * registered) -> kernel -> the 2-byte results back; with XCSUM_F_INPLACE the
+ * chunked, double-buffered hipMemcpyAsync -> kernel -> the 2-byte results
+ * back: DMA'd in place from a registered UMEM, copied into the context's
+ * pinned stages first from pageable memory (never handed to the runtime's
+ * own pinning: DESIGN.md 6); with XCSUM_F_INPLACE the
  * results are also written into the host frames' udp->check (and iph->check
  * with XCSUM_F_IPHDR).  With XCSUM_F_ZEROCOPY and a registered UMEM the
  * kernel reads the frames in place over PCIe instead.  Frames spread over
