@@ -255,6 +255,23 @@ int xcsum_batch_host(xcsum_ctx *ctx, uint8_t *h_umem, const struct xcsum_desc *h
 int xcsum_register_umem(xcsum_ctx *ctx, void *base, size_t size);
 int xcsum_unregister_umem(xcsum_ctx *ctx, void *base);
 
+/* Resident workgroups for small host batches (libxudp sends in batches of
+ * tx_batch_num = 100 frames, xudp/xudp.c:74; tx.c:673-734 is one batch).
+ * `workgroups` (1-64) checksum workgroups stay on the device and poll a
+ * doorbell in pinned host memory: a host batch of at most 4096 frames whose
+ * frames lie in a registered UMEM (read in place) or fit the pinned stage
+ * (256 KiB) then costs a doorbell store and a spin on the answer instead of a
+ * kernel launch and its completion.  Results are the same bytes.  The
+ * workgroups leave after `idle_us` (0: 20000) without a batch, and come back
+ * with the next one.  0 workgroups: off (the default; env XCSUM_RESIDENT=
+ * "W[,idle_us[,max_frames]]" sets it at context creation).
+ * While they are resident, a device-wide synchronisation by others
+ * (hipDeviceSynchronize, torch.cuda.synchronize) waits until they leave, i.e.
+ * up to idle_us after this context's last batch; the library's own
+ * device-wide waits (xcsum_ctx_take_errors, xcsum_unregister_umem,
+ * xcsum_ctx_destroy) stop them first. */
+int xcsum_ctx_set_resident(xcsum_ctx *ctx, int workgroups, uint32_t idle_us);
+
 /* Number of the context's host-path slots with copies or kernels still in
  * flight.  Always 0 after xcsum_batch_host / xcsum_rx_host return, on error
  * returns too: no work of a finished call touches the caller's memory. */

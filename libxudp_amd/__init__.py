@@ -138,6 +138,7 @@ _SIGS = {
                                               ctypes.c_int]),
     "xcsum_ctx_set_launch": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     "xcsum_ctx_set_order": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int]),
+    "xcsum_ctx_set_resident": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_uint32]),
     "xcsum_batch_device": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                           ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint32,
                                           ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p]),
@@ -321,6 +322,11 @@ class Engine:
     def set_order(self, region_log2=-1, tile_log2=0):
         _check(lib().xcsum_ctx_set_order(self._ctx, region_log2, tile_log2),
                "xcsum_ctx_set_order")
+
+    def set_resident(self, workgroups=0, idle_us=0):
+        """Resident workgroups for small host batches (0: off), see xcsum.h."""
+        _check(lib().xcsum_ctx_set_resident(self._ctx, workgroups, idle_us),
+               "xcsum_ctx_set_resident")
 
     def take_errors(self):
         c = ctypes.c_uint64(0)

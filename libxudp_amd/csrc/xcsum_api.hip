@@ -9,6 +9,7 @@
 #include <stdlib.h>
 #include <string.h>
 #include <new>
+#include <chrono>
 #include <thread>
 
 #include "xcsum_internal.h"
@@ -37,6 +38,11 @@ extern "C" int xcsum_last_hip_error(int *line, const char **name)
 		*name = t_hip_err ? hipGetErrorName((hipError_t)t_hip_err) : "hipSuccess";
 	return t_hip_err;
 }
+
+/* resident server defaults (xcsum_ctx_set_resident) */
+static constexpr uint32_t RES_IDLE_US = 20000;     /* workgroups leave after 20 ms idle */
+static constexpr uint32_t RES_MAX_FRAMES = 4096;   /* larger batches are launched */
+static constexpr int RES_TIMEOUT_S = 30;           /* no answer: the call fails */
 
 #ifdef XCSUM_DEBUG_BOUNDS
 namespace xcsum {
@@ -101,6 +107,181 @@ static void env_order(xcsum_ctx *c)
 	}
 }
 
+/* XCSUM_RESIDENT="W[,idle_us[,max_frames]]": resident workgroups for every
+ * new context (xcsum_ctx_set_resident), e.g. for the packet.c mirror's
+ * default context */
+static void env_resident(xcsum_ctx *c)
+{
+	c->res_wg = 0;
+	c->res_idle_us = RES_IDLE_US;
+	c->res_max_frames = RES_MAX_FRAMES;
+	c->res_bell = nullptr;
+	c->res_vbell = nullptr;
+	c->res_stream = nullptr;
+	c->res_live = false;
+	c->res_seq = 0;
+	const char *e = getenv("XCSUM_RESIDENT");
+	int w = 0;
+	unsigned idle = RES_IDLE_US, maxf = RES_MAX_FRAMES;
+	if (e && sscanf(e, "%d,%u,%u", &w, &idle, &maxf) >= 1 && w >= 0 && w <= RB_MAX_WG) {
+		c->res_wg = w;
+		c->res_idle_us = idle;
+		c->res_max_frames = maxf;
+	}
+}
+
+/* ---- resident server (xcsum_resident.hip) ----------------------------------
+ * W workgroups poll a doorbell in pinned host memory; a small host batch is a
+ * request written there and a spin on the workgroups' done words instead of
+ * a launch and its completion. */
+
+/* Ask the workgroups to leave and wait until they have (a no-op when none
+ * run).  Every path that synchronises the whole device calls this first:
+ * resident workgroups end only on `stop` or after res_idle_us without work. */
+static int resident_stop(xcsum_ctx *c)
+{
+	if (!c->res_bell || !c->res_stream)
+		return 0;
+	__atomic_store_n(&c->res_bell->stop, 1u, __ATOMIC_RELEASE);
+	const hipError_t e = hipStreamSynchronize(c->res_stream);
+	__atomic_store_n(&c->res_bell->stop, 0u, __ATOMIC_RELEASE);
+	c->res_live = false;
+	if (e != hipSuccess) {
+		t_hip_err = (int)e;
+		t_hip_line = __LINE__;
+		return -XCSUM_ERR_HIP;
+	}
+	return 0;
+}
+
+static void resident_free(xcsum_ctx *c)
+{
+	if (c->res_stream)
+		(void)hipStreamDestroy(c->res_stream);
+	if (c->res_bell)
+		(void)hipHostFree(c->res_bell);
+	c->res_stream = nullptr;
+	c->res_bell = nullptr;
+	c->res_vbell = nullptr;
+	c->res_live = false;
+}
+
+static int resident_ensure(xcsum_ctx *c)
+{
+	if (c->res_bell)
+		return 0;
+	void *b = nullptr, *v = nullptr;
+	if (hipHostMalloc(&b, sizeof(ResidentBell), hipHostMallocCoherent | hipHostMallocMapped) !=
+	    hipSuccess)
+		return -XCSUM_ERR_NOMEM;
+	memset(b, 0, sizeof(ResidentBell));
+	if (hipHostGetDevicePointer(&v, b, 0) != hipSuccess ||
+	    hipStreamCreateWithFlags(&c->res_stream, hipStreamNonBlocking) != hipSuccess) {
+		(void)hipHostFree(b);
+		c->res_stream = nullptr;
+		return -XCSUM_ERR_HIP;
+	}
+	c->res_bell = (ResidentBell *)b;
+	c->res_vbell = (ResidentBell *)v;
+	c->res_seq = 0;
+	return 0;
+}
+
+extern "C" int xcsum_ctx_set_resident(xcsum_ctx *c, int workgroups, uint32_t idle_us)
+{
+	if (!c || workgroups < 0 || workgroups > RB_MAX_WG)
+		return -XCSUM_ERR_INVAL;
+	HIPCHK(hipSetDevice(c->device));
+	/* the running workgroups leave; the next batch launches the new count */
+	const int rc = resident_stop(c);
+	c->res_wg = workgroups;
+	c->res_idle_us = idle_us ? idle_us : RES_IDLE_US;
+	if (!workgroups)
+		resident_free(c);
+	return rc;
+}
+
+/* One request: the batch `a` describes (device addresses of the frames,
+ * descriptors and result slots) served by the resident workgroups.  Returns
+ * when every workgroup has answered.  A workgroup that left at its idle
+ * deadline while the request was on its way is relaunched with the mask of
+ * those that did answer (they skip it), so every frame is served once. */
+static int resident_call(xcsum_ctx *c, const CsumArgs &a)
+{
+	int rc = resident_ensure(c);
+	if (rc)
+		return rc;
+	ResidentBell *b = c->res_bell;
+	const int W = c->res_wg;
+	const uint32_t prev = c->res_seq;
+	const uint32_t seq = prev + 1u ? prev + 1u : 1u;
+	auto put64 = [&](int k, uint64_t v) {
+		b->req[k] = (uint32_t)v;
+		b->req[k + 1] = (uint32_t)(v >> 32);
+	};
+	put64(RB_UMEM, (uint64_t)(uintptr_t)a.umem);
+	put64(RB_DESC, (uint64_t)(uintptr_t)a.desc);
+	put64(RB_OUT, (uint64_t)(uintptr_t)a.out);
+	put64(RB_OUT_IP, (uint64_t)(uintptr_t)a.out_ip);
+	put64(RB_BIAS, a.bias);
+	b->req[RB_N] = a.n;
+	b->req[RB_MODE] = a.mode;
+	b->req[RB_FLAGS] = a.flags;
+	if (c->res_live && hipStreamQuery(c->res_stream) != hipErrorNotReady)
+		c->res_live = false;   /* left idle (or failed: the launch below reports it) */
+	if (!c->res_live) {
+		HIPCHK(launch_resident(c->res_vbell, c->d_err, W, prev, 0u, 0ull, c->res_idle_us,
+				       c->res_stream));
+		c->res_live = true;
+	}
+	__atomic_store_n(&b->seq, seq, __ATOMIC_RELEASE);
+	c->res_seq = seq;
+
+	const uint64_t all = W == 64 ? ~0ull : (1ull << W) - 1;
+	uint64_t pending = all;
+	const auto t0 = std::chrono::steady_clock::now();
+	for (uint64_t spin = 1;; spin++) {
+		for (int w = 0; w < W; w++)
+			if (((pending >> w) & 1ull) &&
+			    __atomic_load_n(&b->done[RB_DONE_STRIDE * w], __ATOMIC_ACQUIRE) == seq)
+				pending &= ~(1ull << w);
+		if (!pending)
+			return 0;
+		__builtin_ia32_pause();
+		if (spin % 4096 == 0) {
+			const hipError_t q = hipStreamQuery(c->res_stream);
+			if (q == hipErrorNotReady) {
+				/* a device that stopped answering: give up after
+				 * RES_TIMEOUT_S rather than spin forever */
+				if (std::chrono::steady_clock::now() - t0 >
+				    std::chrono::seconds(RES_TIMEOUT_S)) {
+					(void)resident_stop(c);
+					t_hip_err = (int)hipErrorLaunchTimeOut;
+					t_hip_line = __LINE__;
+					return -XCSUM_ERR_HIP;
+				}
+				continue;
+			}
+			if (q != hipSuccess) {
+				c->res_live = false;
+				t_hip_err = (int)q;
+				t_hip_line = __LINE__;
+				return -XCSUM_ERR_HIP;
+			}
+			/* every workgroup left; re-read done[] before relaunching:
+			 * the last ones may have answered just before leaving */
+			for (int w = 0; w < W; w++)
+				if (((pending >> w) & 1ull) &&
+				    __atomic_load_n(&b->done[RB_DONE_STRIDE * w], __ATOMIC_ACQUIRE) == seq)
+					pending &= ~(1ull << w);
+			if (!pending)
+				return 0;
+			HIPCHK(launch_resident(c->res_vbell, c->d_err, W, prev, seq, all & ~pending,
+					       c->res_idle_us, c->res_stream));
+		}
+	}
+}
+
 extern "C" int xcsum_ctx_create(int device, xcsum_ctx **out)
 {
 	int count = 0;
@@ -158,6 +339,7 @@ extern "C" int xcsum_ctx_create(int device, xcsum_ctx **out)
 	c->geom = env_geometry();
 	c->blocks_per_cu = 0;
 	env_order(c);
+	env_resident(c);
 	*out = c;
 	return 0;
 }
@@ -199,7 +381,9 @@ extern "C" void xcsum_ctx_destroy(xcsum_ctx *c)
 	if (!c)
 		return;
 	(void)hipSetDevice(c->device);
+	(void)resident_stop(c);
 	(void)hipDeviceSynchronize();
+	resident_free(c);
 	free_staging(c);
 	for (auto &r : c->regions)
 		(void)hipHostUnregister(r.host);
@@ -221,6 +405,11 @@ extern "C" int xcsum_ctx_take_errors(xcsum_ctx *c, uint64_t *count)
 	if (!c || !count)
 		return -XCSUM_ERR_INVAL;
 	HIPCHK(hipSetDevice(c->device));
+	{
+		const int rc = resident_stop(c);   /* or the device sync waits for it */
+		if (rc)
+			return rc;
+	}
 	HIPCHK(hipDeviceSynchronize());
 	HIPCHK(hipMemcpy(&v, c->d_err, sizeof(v), hipMemcpyDeviceToHost));
 	HIPCHK(hipMemset(c->d_err, 0, sizeof(v)));
@@ -485,8 +674,10 @@ extern "C" int xcsum_unregister_umem(xcsum_ctx *c, void *base)
 		if (c->regions[i].host == (uint8_t *)base) {
 			HIPCHK(hipSetDevice(c->device));
 			/* no kernel or copy may still read or write the region once
-			 * it is unmapped: this context's host-path streams and any
-			 * stream a caller launched on its device alias */
+			 * it is unmapped: this context's resident workgroups, its
+			 * host-path streams and any stream a caller launched on its
+			 * device alias */
+			(void)resident_stop(c);
 			(void)hipDeviceSynchronize();
 			(void)hipHostUnregister(base);
 			c->regions.erase(c->regions.begin() + i);
@@ -765,6 +956,85 @@ extern "C" int xcsum_ctx_pending(xcsum_ctx *c)
 	return busy;
 }
 
+/* A host batch through the resident workgroups (xcsum_ctx_set_resident):
+ * the frames are read where the kernel can reach them without a copy
+ *   - in a registered UMEM: in place through its device alias (in-place
+ *     writes land in the frames directly);
+ *   - else staged into the pinned stage of slot 0 (gathered frame by frame,
+ *     or the 16-byte aligned range), up to XCSUM_DIRECT_MAX bytes;
+ * descriptors go to the pinned descriptor stage, results come back in the
+ * pinned result slot.  Returns RES_DECLINE when the batch does not fit (the
+ * launched path takes it). */
+static constexpr int RES_DECLINE = 1;
+
+static int batch_host_resident(xcsum_ctx *c, uint8_t *h_umem, const struct xcsum_desc *h_desc,
+			       uint32_t n, uint16_t *h_out, uint16_t *h_out_ip, uint32_t mode,
+			       uint32_t flags, const Region *zc, bool gather)
+{
+	if (n > c->res_max_frames || n > c->desc_cap || !c->v_stage[0])
+		return RES_DECLINE;
+	uint64_t lo = UINT64_MAX, hi = 0;
+	for (uint32_t i = 0; i < n; i++) {
+		if (h_desc[i].addr < lo) lo = h_desc[i].addr;
+		if (h_desc[i].addr + h_desc[i].len > hi) hi = h_desc[i].addr + h_desc[i].len;
+	}
+	if (!zc)
+		zc = find_region(c, h_umem + lo, h_umem + hi);   /* dense, registered */
+	const bool want_ip = (flags & XCSUM_F_IPHDR) != 0;
+	struct xcsum_desc *ds = c->h_dstage[0];
+	CsumArgs a;
+	a.desc = c->v_dstage[0];
+	a.n = n;
+	a.out = c->v_out[0];
+	a.out_ip = want_ip ? c->v_out[0] + n : nullptr;
+	a.mode = mode;
+	a.err = c->d_err;
+	a.bias = 0;
+	a.ord = order_identity(n);
+	a.dense = a.ord;
+	if (zc) {
+		memcpy(ds, h_desc, (size_t)n * sizeof(*ds));
+		a.umem = zc->dev + (h_umem - zc->host);
+		a.flags = flags & (XCSUM_F_INPLACE | XCSUM_F_IPHDR | XCSUM_F_V4_RFC | XCSUM_F_VERIFY);
+	} else if (gather) {
+		uint64_t pos = 0;
+		for (uint32_t k = 0; k < n; k++)
+			pos = stage_off(pos, h_desc[k].addr) + h_desc[k].len;
+		if (pos > DIRECT_MAX)
+			return RES_DECLINE;
+		pos = 0;
+		for (uint32_t k = 0; k < n; k++) {
+			const struct xcsum_desc &d = h_desc[k];
+			const uint64_t off = stage_off(pos, d.addr);
+			memcpy(c->h_stage[0] + off, h_umem + d.addr, d.len);
+			ds[k] = xcsum_desc{off, d.len, 0};
+			pos = off + d.len;
+		}
+		a.umem = c->v_stage[0];
+		a.flags = flags & (XCSUM_F_IPHDR | XCSUM_F_V4_RFC | XCSUM_F_VERIFY);
+	} else {
+		/* 16-byte aligned copy of [lo, hi): every frame keeps its address
+		 * parity and phase */
+		const uint64_t alo = lo & ~(uint64_t)15;
+		if (hi - alo > DIRECT_MAX)
+			return RES_DECLINE;
+		memcpy(c->h_stage[0], h_umem + alo, hi - alo);
+		memcpy(ds, h_desc, (size_t)n * sizeof(*ds));
+		a.umem = c->v_stage[0];
+		a.bias = alo;
+		a.flags = flags & (XCSUM_F_IPHDR | XCSUM_F_V4_RFC | XCSUM_F_VERIFY);
+	}
+	const int rc = resident_call(c, a);
+	if (rc)
+		return rc;
+	Pending pd;
+	pd.first = 0;
+	pd.count = n;
+	retire(pd, c->h_out[0], h_umem, h_desc, h_out, h_out_ip, mode,
+	       zc ? (flags & ~XCSUM_F_INPLACE) : flags);
+	return 0;
+}
+
 static int batch_host_run(xcsum_ctx *c, uint8_t *h_umem, const struct xcsum_desc *h_desc,
 			  uint32_t n, uint16_t *h_out, uint16_t *h_out_ip, uint32_t mode,
 			  uint32_t flags, bool gather)
@@ -804,6 +1074,14 @@ static int batch_host_run(xcsum_ctx *c, uint8_t *h_umem, const struct xcsum_desc
 	 * caller memory goes through them (see host_dma_src) */
 	if ((rc = ensure_gather(c)))
 		return rc;
+
+	/* small batches: the resident workgroups, if the context has them */
+	if (c->res_wg > 0) {
+		rc = batch_host_resident(c, h_umem, h_desc, n, h_out, h_out_ip, mode, flags, zc,
+					 gather);
+		if (rc != RES_DECLINE)
+			return rc;
+	}
 
 	/* zero-copy + INPLACE: the kernel already wrote the host frames */
 	const uint32_t rflags = zc ? (flags & ~XCSUM_F_INPLACE) : flags;

@@ -6,6 +6,7 @@
 #include <stdint.h>
 #include <vector>
 #include "xcsum.h"
+#include "xcsum_resident.h"
 
 namespace xcsum {
 
@@ -214,6 +215,17 @@ struct Ctx {
 	uint16_t *v_out[NSLOT];
 	size_t frame_cap;              /* bytes per slot */
 	uint32_t desc_cap;             /* frames per slot */
+
+	/* resident server for small host batches (xcsum_ctx_set_resident,
+	 * xcsum_resident.hip): res_wg workgroups, 0 = off */
+	int res_wg;
+	uint32_t res_idle_us;
+	uint32_t res_max_frames;       /* larger batches take the launched path */
+	ResidentBell *res_bell;        /* pinned, coherent (lazy) */
+	ResidentBell *res_vbell;       /* its device alias */
+	hipStream_t res_stream;
+	bool res_live;                 /* launched, not yet seen gone */
+	uint32_t res_seq;              /* last sequence number issued (0: none) */
 };
 
 } /* namespace xcsum */

@@ -1,0 +1,140 @@
+/*
+ * xcsum_resident.hip -- resident checksum workgroups for small host batches.
+ *
+ * libxudp sends in batches of tx_batch_num = 100 frames (xudp/xudp.c:74); each
+ * batch is one trip through xudp_frame_send (tx.c:673-734).  As a kernel
+ * launch per batch, a call costs a launch and a completion (~17-20 us,
+ * DESIGN.md 5.8) for microseconds of work.  A resident server removes both:
+ * W workgroups stay on the device and poll a doorbell in pinned host memory;
+ * a batch is the request written there, a sequence number stored after it,
+ * and a host spin on one "done" word per workgroup.
+ *
+ * The work is the frame-group checksum loop itself (csum_loop<16, 2, 6, 2>
+ * of xcsum_csum.h: every mode and flag, bit-exact with the launched kernels),
+ * over frames the kernel reads in place through a device alias: a registered
+ * UMEM, or the context's pinned stage.
+ *
+ * Memory ordering (all vector memory operations):
+ *   - wave 0 of a workgroup polls `seq` with system-scope acquire loads; the
+ *     acquire invalidates the CU's L1 and the L2's non-coherent lines, so the
+ *     request, descriptors and frame bytes the host wrote before `seq` are
+ *     read fresh by every wave after the workgroup barrier that follows;
+ *   - every wave ends a request with a system-scope release fence (its
+ *     results and in-place stores written back to host memory), then the
+ *     workgroup barrier, then thread 0 stores done[w] = seq;
+ *   - descriptor and frame loads are vector loads (G = 16: one descriptor per
+ *     lane), never through the scalar cache, which the acquire does not
+ *     invalidate.
+ *
+ * Lifetime: a workgroup leaves when the host sets `stop`, or after idle_ticks
+ * of the 100 MHz wall clock without a request, so the grid always drains on
+ * its own.  The host relaunches on the next batch (see resident_call in
+ * xcsum_api.hip, which also covers a workgroup that left at the idle deadline
+ * while a request was on its way: it is relaunched with a mask of the
+ * workgroups that already served that request, so no frame is done twice --
+ * an in-place frame summed twice would sum its own check field).
+ */
+#include "xcsum_csum.h"
+#include "xcsum_resident.h"
+
+namespace xcsum {
+
+static __device__ __forceinline__ uint32_t ld_acquire_sys(const uint32_t *p)
+{
+	return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+static __device__ __forceinline__ uint32_t ld_relaxed_sys(const uint32_t *p)
+{
+	return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+static __device__ __forceinline__ uint64_t u64_of(uint32_t lo, uint32_t hi)
+{
+	return ((uint64_t)hi << 32) | lo;
+}
+
+/* served0: the sequence number every workgroup has served at launch, except
+ * the workgroups of skip_mask (bit w), which served skip_seq already
+ * (relaunch after a partial service, see the file comment) */
+template <int G, int U, int K>
+__global__ void __launch_bounds__(256) resident_kernel(ResidentBell *bell, unsigned long long *err,
+						       uint32_t served0, uint32_t skip_seq,
+						       uint64_t skip_mask, uint64_t idle_ticks)
+{
+	__shared__ uint32_t cmd[RB_REQ_WORDS + 1];
+	const uint32_t lane = threadIdx.x & 63;
+	uint32_t served = served0;
+	if (blockIdx.x < 64 && ((skip_mask >> blockIdx.x) & 1ull))
+		served = skip_seq;
+	uint64_t last = wall_clock64();
+	for (;;) {
+		if (threadIdx.x < 64) {
+			uint32_t s = served, go = 0;
+			for (;;) {
+				s = __builtin_amdgcn_readfirstlane(ld_acquire_sys(&bell->seq));
+				if (ld_acquire_sys(&bell->stop))
+					break;
+				if (s != served) {
+					go = 1;
+					break;
+				}
+				if (wall_clock64() - last > idle_ticks)
+					break;
+				__builtin_amdgcn_s_sleep(1);
+			}
+			/* the request, read after the acquire of its sequence number */
+			uint32_t v = 0;
+			if (go && lane < RB_REQ_WORDS)
+				v = ld_relaxed_sys(&bell->req[lane]);
+			if (lane < RB_REQ_WORDS)
+				cmd[1 + lane] = v;
+			if (lane == 0)
+				cmd[0] = go ? s : 0u;
+		}
+		__syncthreads();
+		const uint32_t s = __builtin_amdgcn_readfirstlane(cmd[0]);
+		if (s == 0u)
+			break;   /* stop or idle: the whole workgroup leaves (sequence
+				    numbers skip 0) */
+		uint32_t r[RB_REQ_WORDS];
+#pragma unroll
+		for (int k = 0; k < RB_REQ_WORDS; k++)
+			r[k] = __builtin_amdgcn_readfirstlane(cmd[1 + k]);
+		CsumArgs a;
+		a.umem = (uint8_t *)(uintptr_t)u64_of(r[RB_UMEM], r[RB_UMEM + 1]);
+		a.desc = (const struct xcsum_desc *)(uintptr_t)u64_of(r[RB_DESC], r[RB_DESC + 1]);
+		a.out = (uint16_t *)(uintptr_t)u64_of(r[RB_OUT], r[RB_OUT + 1]);
+		a.out_ip = (uint16_t *)(uintptr_t)u64_of(r[RB_OUT_IP], r[RB_OUT_IP + 1]);
+		a.bias = u64_of(r[RB_BIAS], r[RB_BIAS + 1]);
+		a.n = r[RB_N];
+		a.mode = r[RB_MODE];
+		a.flags = r[RB_FLAGS];
+		a.err = err;
+		a.ord = order_identity(a.n);
+		a.dense = a.ord;
+		csum_loop<G, U, K, false, 2>(a);
+		/* this wave's results and in-place stores reach host memory ... */
+		__builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+		/* ... for every wave, before done[w] says so */
+		__syncthreads();
+		if (threadIdx.x == 0)
+			__hip_atomic_store(&bell->done[RB_DONE_STRIDE * blockIdx.x], s, __ATOMIC_RELEASE,
+					   __HIP_MEMORY_SCOPE_SYSTEM);
+		served = s;
+		last = wall_clock64();
+	}
+}
+
+hipError_t launch_resident(ResidentBell *v_bell, unsigned long long *err, int wg, uint32_t served0,
+			   uint32_t skip_seq, uint64_t skip_mask, uint32_t idle_us, hipStream_t s)
+{
+	if (wg <= 0 || wg > RB_MAX_WG)
+		return hipErrorInvalidValue;
+	(void)hipGetLastError();
+	hipLaunchKernelGGL((resident_kernel<16, 2, 6>), dim3((unsigned)wg), dim3(256), 0, s, v_bell, err,
+			   served0, skip_seq, skip_mask, (uint64_t)idle_us * 100ull);
+	return hipGetLastError();
+}
+
+} /* namespace xcsum */

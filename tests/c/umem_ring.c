@@ -26,7 +26,8 @@
  * Variants: the UMEM unregistered (frames gathered and staged), registered
  * (pinned DMA), registered + zero-copy (the kernel reads the UMEM over
  * PCIe); IPv4 (udp->check 0 as packet.c:125), IPv4 with the opt-in RFC UDP
- * checksum, IPv6 (udp_csum6); and the batch-host hook with in-place writes.
+ * checksum, IPv6 (udp_csum6); the batch-host hook with in-place writes; and
+ * the same calls served by resident workgroups (xcsum_ctx_set_resident).
  *
  * usage: umem_ring [--bench [B1,B2,...]]     exit 0 ok, 1 failure, 77 no GPU
  *   --bench: MTU frames per variant in batches of B (default 4096; 1M frames
@@ -77,6 +78,7 @@ struct variant {
 	int registered;
 	int zerocopy;
 	int batch_host;        /* header build + xcsum_batch_host(INPLACE|IPHDR) */
+	int resident;          /* xcsum_ctx_set_resident workgroups (0: launches) */
 };
 
 struct run {
@@ -333,24 +335,32 @@ int main(int argc, char **argv)
 	printf("umem_ring: UMEM %zu bytes by anon_map (MAP_LOCKED %s)\n", bytes,
 	       locked ? "granted" : "refused, mapped without it");
 	static const struct variant vars[] = {
-		{"v4 staged", 4, 0, 0, 0, 0},
-		{"v4 registered", 4, 0, 1, 0, 0},
-		{"v4 zero-copy", 4, 0, 1, 1, 0},
-		{"v4+rfc staged", 4, XCSUM_F_V4_RFC, 0, 0, 0},
-		{"v4+rfc registered", 4, XCSUM_F_V4_RFC, 1, 0, 0},
-		{"v4+rfc zero-copy", 4, XCSUM_F_V4_RFC, 1, 1, 0},
-		{"v6 staged", 6, 0, 0, 0, 0},
-		{"v6 registered", 6, 0, 1, 0, 0},
-		{"v6 zero-copy", 6, 0, 1, 1, 0},
-		{"v4 batch_host in place, registered", 4, XCSUM_F_V4_RFC, 1, 0, 1},
-		{"v4 batch_host in place, zero-copy", 4, XCSUM_F_V4_RFC, 1, 1, 1},
-		{"v6 batch_host in place, zero-copy", 6, 0, 1, 1, 1},
+		{"v4 staged", 4, 0, 0, 0, 0, 0},
+		{"v4 registered", 4, 0, 1, 0, 0, 0},
+		{"v4 zero-copy", 4, 0, 1, 1, 0, 0},
+		{"v4+rfc staged", 4, XCSUM_F_V4_RFC, 0, 0, 0, 0},
+		{"v4+rfc registered", 4, XCSUM_F_V4_RFC, 1, 0, 0, 0},
+		{"v4+rfc zero-copy", 4, XCSUM_F_V4_RFC, 1, 1, 0, 0},
+		{"v6 staged", 6, 0, 0, 0, 0, 0},
+		{"v6 registered", 6, 0, 1, 0, 0, 0},
+		{"v6 zero-copy", 6, 0, 1, 1, 0, 0},
+		{"v4 batch_host in place, registered", 4, XCSUM_F_V4_RFC, 1, 0, 1, 0},
+		{"v4 batch_host in place, zero-copy", 4, XCSUM_F_V4_RFC, 1, 1, 1, 0},
+		{"v6 batch_host in place, zero-copy", 6, 0, 1, 1, 1, 0},
+		/* resident workgroups instead of a launch per batch */
+		{"v4 registered, resident", 4, 0, 1, 0, 0, 8},
+		{"v4+rfc registered, resident", 4, XCSUM_F_V4_RFC, 1, 0, 0, 8},
+		{"v6 staged, resident", 6, 0, 0, 0, 0, 8},
+		{"v6 registered, resident", 6, 0, 1, 0, 0, 8},
+		{"v4 batch_host in place, registered, resident", 4, XCSUM_F_V4_RFC, 1, 0, 1, 8},
+		{"v6 batch_host in place, registered, resident", 6, 0, 1, 0, 1, 8},
 	};
 	struct run *r = calloc(1, sizeof(*r));
 	for (size_t k = 0; k < sizeof(vars) / sizeof(vars[0]); k++) {
 		const struct variant *v = &vars[k];
 		if (v->registered)
 			CHECK(xcsum_register_umem(ctx, umem, bytes) == 0, "%s: register", v->name);
+		CHECK(xcsum_ctx_set_resident(ctx, v->resident, 0) == 0, "%s: resident", v->name);
 		for (int pass = bench; pass < (bench ? 1 + nbatch : 1); pass++) {
 			/* tx_batch_num is 100 (xudp.c:74); the bench batches as asked */
 			const uint32_t batch = pass ? batches[pass - 1] : 100u;

@@ -1,0 +1,215 @@
+"""GPU: host batches served by resident workgroups (xcsum_ctx_set_resident,
+csrc/xcsum_resident.hip) against the reference fixtures and the oracle.  The
+resident path must give the same bytes as the launched one in every mode,
+flag and transport (registered UMEM read in place, pageable frames staged),
+stay correct when the same UMEM changes between calls (no stale cache
+lines), and serve every frame exactly once when its workgroups leave and
+come back between calls (an in-place frame served twice would sum its own
+check field)."""
+import time
+
+import numpy as np
+import pytest
+
+import libxudp_amd as X
+import oracle
+from conftest import golden_desc
+from test_gpu_host_path import check_inplace, host_batch
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture
+def res_engine():
+    e = X.Engine(0)
+    e.set_resident(8)
+    yield e
+    e.close()
+
+
+@pytest.mark.parametrize("mode,col,fam", [(X.MODE_V4_LEGACY, "exp_legacy", 4),
+                                          (X.MODE_V4_RFC, "exp_rfc", 4),
+                                          (X.MODE_V6, "exp_v6", 6)])
+@pytest.mark.parametrize("register", [False, True])
+def test_resident_golden(res_engine, golden, mode, col, fam, register):
+    sel = np.nonzero(golden["family"] == fam)[0]
+    umem = golden["umem"].copy()
+    if register:
+        res_engine.register_umem(umem)
+    try:
+        for lo in range(0, len(sel), 300):       # batches the resident path takes
+            s = sel[lo:lo + 300]
+            got = host_batch(res_engine, umem, golden_desc(golden, s), mode)
+            assert np.array_equal(got, golden[col][s])
+    finally:
+        if register:
+            res_engine.unregister_umem(umem)
+
+
+@pytest.mark.parametrize("how", ["pageable", "registered", "zerocopy"])
+def test_resident_inplace(res_engine, golden, how):
+    umem = golden["umem"].copy()
+    desc = golden_desc(golden)
+    flags = X.F_INPLACE | X.F_IPHDR
+    if how != "pageable":
+        res_engine.register_umem(umem)
+    if how == "zerocopy":
+        flags |= X.F_ZEROCOPY
+    try:
+        got = host_batch(res_engine, umem, desc, X.MODE_AUTO, flags)
+    finally:
+        if how != "pageable":
+            res_engine.unregister_umem(umem)
+    fam = golden["family"]
+    assert np.array_equal(got, np.where(fam == 6, golden["exp_v6"], golden["exp_legacy"]))
+    check_inplace(golden, umem, desc)
+
+
+def test_resident_verify(res_engine, golden):
+    """VERIFY through the resident workgroups: frames with their reference
+    checksum in place verify (0); a corrupted payload byte does not."""
+    sel = np.nonzero(golden["family"] == 6)[0][:200]
+    desc = golden_desc(golden, sel)
+    umem = golden["umem"].copy()
+    for i, d in zip(sel, desc):
+        a = int(d["addr"])
+        umem[a + 60:a + 62] = np.array([golden["exp_v6"][i]], dtype="<u2").view(np.uint8)
+    assert not host_batch(res_engine, umem, desc, X.MODE_V6, X.F_VERIFY).any()
+    a = int(desc["addr"][7])
+    umem[a + int(desc["len"][7]) - 1] ^= 0x40
+    got = host_batch(res_engine, umem, desc, X.MODE_V6, X.F_VERIFY)
+    assert got[7] != 0 and np.count_nonzero(got) == 1
+
+
+@pytest.mark.parametrize("fam", [4, 6])
+@pytest.mark.parametrize("register", [False, True])
+def test_resident_slots(res_engine, fam, register):
+    """xudp's TX layout (one frame per 4096-byte chunk): gathered from a
+    pageable UMEM, read in place from a registered one; in place + IP header."""
+    umem, desc = X.gen_frames_host(100, fam, 0, 1458, seed=77 + fam, stride=4096,
+                                   offset=322 if fam == 6 else 342)
+    mode = X.MODE_V6 if fam == 6 else X.MODE_V4_RFC
+    exp = oracle.batch(umem, desc, mode)
+    if register:
+        res_engine.register_umem(umem)
+    try:
+        assert np.array_equal(host_batch(res_engine, umem, desc, mode), exp)
+        got = host_batch(res_engine, umem, desc, mode,
+                         X.F_INPLACE | (X.F_IPHDR if fam == 4 else 0))
+        assert np.array_equal(got, exp)
+    finally:
+        if register:
+            res_engine.unregister_umem(umem)
+    a = desc["addr"].astype(np.int64)
+    chk = 60 if fam == 6 else 40
+    assert np.array_equal(umem[a[:, None] + np.array([chk, chk + 1])].copy().view("<u2").ravel(),
+                          exp)
+
+
+@pytest.mark.parametrize("n", [1, 2, 99, 100, 1024, 4096, 4097, 20000])
+def test_resident_sizes(res_engine, n):
+    """Batch sizes around the resident limit (4096 frames): larger batches
+    and staged ranges over 256 KiB take the launched path; same results."""
+    umem, desc = X.gen_frames_host(n, 4, 0, 1472, seed=n, align=8)
+    exp = oracle.batch(umem, desc, X.MODE_V4_LEGACY)
+    assert np.array_equal(host_batch(res_engine, umem, desc, X.MODE_V4_LEGACY), exp)
+    res_engine.register_umem(umem)
+    try:
+        assert np.array_equal(host_batch(res_engine, umem, desc, X.MODE_V4_LEGACY), exp)
+    finally:
+        res_engine.unregister_umem(umem)
+    assert res_engine.pending() == 0
+
+
+def test_resident_fresh_bytes_every_call(res_engine):
+    """The same registered UMEM rewritten between calls: every call must read
+    the new bytes (the workgroups' acquire drops cached lines)."""
+    umem, desc = X.gen_frames_host(100, 6, 0, 1400, seed=5, stride=4096, offset=322)
+    res_engine.register_umem(umem)
+    rng = np.random.default_rng(1)
+    a = desc["addr"].astype(np.int64)
+    try:
+        for it in range(200):
+            k = int(rng.integers(0, 100))
+            pos = a[k] + 62 + int(rng.integers(0, int(desc["len"][k]) - 62))
+            umem[pos] = rng.integers(0, 256)
+            got = host_batch(res_engine, umem, desc, X.MODE_V6)
+            assert np.array_equal(got, oracle.batch(umem, desc, X.MODE_V6)), it
+    finally:
+        res_engine.unregister_umem(umem)
+
+
+@pytest.mark.parametrize("idle_us", [1, 3, 30, 1000])
+def test_resident_leave_and_return(idle_us):
+    """Workgroups that leave after idle_us come back with the next batch; with
+    a 1-30 us idle time they leave between (and during) calls, so relaunches
+    after a partial service happen too.  In place on a registered UMEM: a
+    frame served twice would sum its own, already written check field."""
+    e = X.Engine(0)
+    e.set_resident(16, idle_us)
+    umem, desc = X.gen_frames_host(300, 6, 0, 1400, seed=9, stride=4096, offset=322)
+    a = desc["addr"].astype(np.int64)
+    chk = a[:, None] + np.array([60, 61])
+    exp = oracle.batch(umem, desc, X.MODE_V6)
+    e.register_umem(umem)
+    try:
+        for it in range(300):
+            umem[chk] = 0
+            got = host_batch(e, umem, desc, X.MODE_V6, X.F_INPLACE)
+            assert np.array_equal(got, exp), it
+            assert np.array_equal(umem[chk].copy().view("<u2").ravel(), exp), it
+            if it % 50 == 49:
+                time.sleep(0.002)
+    finally:
+        e.unregister_umem(umem)
+        e.close()
+
+
+def test_resident_errors_and_switch(res_engine, golden):
+    """Malformed frames are counted with resident workgroups live
+    (take_errors stops them first); set_resident(0) falls back to launches,
+    a new count takes effect on the next batch."""
+    umem, desc = X.gen_frames_host(50, 4, 10, 200, seed=2, align=8)
+    d = desc.copy()
+    d["len"][3] = 20            # too short for the headers
+    exp = oracle.batch(umem, d, X.MODE_V4_RFC)
+    res_engine.take_errors()
+    assert np.array_equal(host_batch(res_engine, umem, d, X.MODE_V4_RFC), exp)
+    assert res_engine.take_errors() == 1
+    for w in (0, 1, 64, 3):
+        res_engine.set_resident(w)
+        assert np.array_equal(host_batch(res_engine, umem, d, X.MODE_V4_RFC), exp)
+    with pytest.raises(X.XcsumError):
+        res_engine.set_resident(65)
+
+
+def test_resident_packet_mirror(res_engine):
+    """xudp_packet_udp_batch (the packet.c mirror) through a resident
+    context: headers on the host, checksums from the resident workgroups."""
+    from test_gpu_host_path import MAC1, MAC2
+    rng = np.random.default_rng(4)
+    umem = np.zeros(4096 * 100, dtype=np.uint8)
+    pas = []
+    for i in range(100):
+        fam = 6 if i % 2 else 4
+        L = int(rng.integers(0, 1439))
+        alen = 16 if fam == 6 else 4
+        pa = X.PacketArgs(fam, rng.integers(0, 256, L, dtype=np.uint8).tobytes(), MAC1, MAC2,
+                          rng.integers(0, 256, alen, dtype=np.uint8).tobytes(), 1000 + i,
+                          rng.integers(0, 256, alen, dtype=np.uint8).tobytes(), 2000 + i,
+                          buf=umem, offset=4096 * i + 320)
+        umem[4096 * i + 320 + 64:4096 * i + 320 + 64 + L] = pa.payload[:L]
+        pas.append(pa)
+    X.packet_udp_batch(res_engine, pas, X.F_V4_RFC)
+    for pa in pas:
+        f = pa.frame()
+        z = f.copy()
+        desc = np.zeros(1, dtype=X.DESC_DTYPE)
+        desc["len"] = len(f)
+        if pa.family == 6:
+            z[60:62] = 0
+            assert int(f[60:62].view("<u2")[0]) == oracle.batch(z, desc, X.MODE_V6)[0]
+        else:
+            assert int(f[24:26].view("<u2")[0]) == oracle.ip_header_rfc(f)
+            z[40:42] = 0
+            assert int(f[40:42].view("<u2")[0]) == oracle.batch(z, desc, X.MODE_V4_RFC)[0]
