@@ -8,8 +8,10 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <unistd.h>
 #include <new>
 #include <chrono>
+#include <mutex>
 #include <thread>
 
 #include "xcsum_internal.h"
@@ -117,16 +119,21 @@ static void env_resident(xcsum_ctx *c)
 	c->res_max_frames = RES_MAX_FRAMES;
 	c->res_bell = nullptr;
 	c->res_vbell = nullptr;
+	c->res_bell_dev = false;
+	c->res_bell_forced_host = false;
+	c->res_done = nullptr;
+	c->res_vdone = nullptr;
 	c->res_stream = nullptr;
 	c->res_live = false;
 	c->res_seq = 0;
+	c->res_gen = 0;
 	const char *e = getenv("XCSUM_RESIDENT");
 	int w = 0;
 	unsigned idle = RES_IDLE_US, maxf = RES_MAX_FRAMES;
 	if (e && sscanf(e, "%d,%u,%u", &w, &idle, &maxf) >= 1 && w >= 0 && w <= RB_MAX_WG) {
 		c->res_wg = w;
-		c->res_idle_us = idle;
-		c->res_max_frames = maxf;
+		c->res_idle_us = idle ? idle : RES_IDLE_US;
+		c->res_max_frames = maxf < RB_DESC_CAP ? maxf : RB_DESC_CAP;
 	}
 }
 
@@ -135,6 +142,17 @@ static void env_resident(xcsum_ctx *c)
  * request written there and a spin on the workgroups' done words instead of
  * a launch and its completion. */
 
+/* A doorbell word, visible to the device at once and after everything
+ * written before it: the BAR mapping is write-combining, whose stores x86
+ * does not order with later stores, so a store fence drains the request and
+ * descriptors first, and another pushes the word itself out. */
+static inline void bell_store(uint32_t *p, uint32_t v)
+{
+	__builtin_ia32_sfence();
+	__atomic_store_n(p, v, __ATOMIC_RELEASE);
+	__builtin_ia32_sfence();
+}
+
 /* Ask the workgroups to leave and wait until they have (a no-op when none
  * run).  Every path that synchronises the whole device calls this first:
  * resident workgroups end only on `stop` or after res_idle_us without work. */
@@ -142,9 +160,9 @@ static int resident_stop(xcsum_ctx *c)
 {
 	if (!c->res_bell || !c->res_stream)
 		return 0;
-	__atomic_store_n(&c->res_bell->stop, 1u, __ATOMIC_RELEASE);
+	bell_store(&c->res_bell->stop, 1u);
 	const hipError_t e = hipStreamSynchronize(c->res_stream);
-	__atomic_store_n(&c->res_bell->stop, 0u, __ATOMIC_RELEASE);
+	bell_store(&c->res_bell->stop, 0u);
 	c->res_live = false;
 	if (e != hipSuccess) {
 		t_hip_err = (int)e;
@@ -154,15 +172,102 @@ static int resident_stop(xcsum_ctx *c)
 	return 0;
 }
 
+/* Does the CPU map this address (fine-grained VRAM behind a large PCIe BAR
+ * shares the GPU's virtual address)?  Asked of the kernel: write() from an
+ * unmapped address fails with EFAULT instead of faulting the process. */
+static bool cpu_maps(const void *p)
+{
+	int fd[2];
+	if (pipe(fd) != 0)
+		return false;
+	const bool ok = write(fd[1], p, 8) == 8;
+	close(fd[0]);
+	close(fd[1]);
+	return ok;
+}
+
+/* Doorbell memory: the doorbell in UNCACHED device memory the host writes
+ * through the BAR (uncached: host stores land in HBM behind the L2's back, so
+ * no L2 line of it may ever be served -- not even one left by an earlier use
+ * of the same addresses), or in pinned host memory where the CPU does not
+ * map device memory; the done words in pinned host memory.  Allocated once
+ * per process and device and kept for later contexts: contexts come and go
+ * (one per test), the memory a resident kernel polls is never freed and
+ * reallocated under another mapping. */
+struct BellMem {
+	int device;
+	bool forced_host;        /* XCSUM_RESIDENT_BELL=host asked for it */
+	bool dev;                /* the doorbell is device memory */
+	ResidentBell *h, *d;     /* as the host writes it, as the kernel reads it */
+	ResidentDone *done_h, *done_d;
+	uint32_t seq, gen;       /* last sequence number / generation issued on it:
+				    a later owner continues from there, so no
+				    stale view of seq can announce a request */
+};
+static std::mutex g_bell_mu;
+static std::vector<BellMem> g_bell_pool;   /* free doorbells */
+
+static int bell_alloc(int device, bool force_host, BellMem *m)
+{
+	void *d = nullptr, *h = nullptr, *v = nullptr;
+	m->device = device;
+	m->forced_host = force_host;
+	m->dev = false;
+	if (!force_host &&
+	    hipExtMallocWithFlags(&d, sizeof(ResidentBell), hipDeviceMallocUncached) == hipSuccess) {
+		if (cpu_maps(d)) {
+			h = d;   /* one virtual address for CPU and GPU */
+			m->dev = true;
+		} else {
+			(void)hipFree(d);
+			d = nullptr;
+		}
+	}
+	if (!m->dev) {
+		if (hipHostMalloc(&h, sizeof(ResidentBell), hipHostMallocCoherent | hipHostMallocMapped) !=
+			    hipSuccess)
+			return -XCSUM_ERR_NOMEM;
+		if (hipHostGetDevicePointer(&d, h, 0) != hipSuccess) {
+			(void)hipHostFree(h);
+			return -XCSUM_ERR_HIP;
+		}
+	}
+	m->h = (ResidentBell *)h;
+	m->d = (ResidentBell *)d;
+	h = nullptr;
+	if (hipHostMalloc(&h, sizeof(ResidentDone), hipHostMallocCoherent | hipHostMallocMapped) !=
+		    hipSuccess ||
+	    hipHostGetDevicePointer(&v, h, 0) != hipSuccess) {
+		if (h)
+			(void)hipHostFree(h);
+		(void)(m->dev ? hipFree(m->d) : hipHostFree(m->h));
+		return -XCSUM_ERR_NOMEM;
+	}
+	m->done_h = (ResidentDone *)h;
+	m->done_d = (ResidentDone *)v;
+	m->seq = 0;
+	m->gen = 0;
+	bell_store(&m->h->stop, 0u);
+	bell_store(&m->h->seq, 0u);
+	return 0;
+}
+
 static void resident_free(xcsum_ctx *c)
 {
 	if (c->res_stream)
 		(void)hipStreamDestroy(c->res_stream);
-	if (c->res_bell)
-		(void)hipHostFree(c->res_bell);
+	if (c->res_bell) {
+		/* back to the pool; its kernel has left (resident_stop first) */
+		std::lock_guard<std::mutex> g(g_bell_mu);
+		g_bell_pool.push_back(BellMem{c->device, c->res_bell_forced_host, c->res_bell_dev,
+					      c->res_bell, c->res_vbell, c->res_done, c->res_vdone,
+					      c->res_seq, c->res_gen});
+	}
 	c->res_stream = nullptr;
 	c->res_bell = nullptr;
 	c->res_vbell = nullptr;
+	c->res_done = nullptr;
+	c->res_vdone = nullptr;
 	c->res_live = false;
 }
 
@@ -170,20 +275,43 @@ static int resident_ensure(xcsum_ctx *c)
 {
 	if (c->res_bell)
 		return 0;
-	void *b = nullptr, *v = nullptr;
-	if (hipHostMalloc(&b, sizeof(ResidentBell), hipHostMallocCoherent | hipHostMallocMapped) !=
-	    hipSuccess)
-		return -XCSUM_ERR_NOMEM;
-	memset(b, 0, sizeof(ResidentBell));
-	if (hipHostGetDevicePointer(&v, b, 0) != hipSuccess ||
-	    hipStreamCreateWithFlags(&c->res_stream, hipStreamNonBlocking) != hipSuccess) {
-		(void)hipHostFree(b);
+	const char *where = getenv("XCSUM_RESIDENT_BELL");   /* "host": force pinned memory */
+	const bool force_host = where && strcmp(where, "host") == 0;
+	BellMem m;
+	bool have = false;
+	{
+		std::lock_guard<std::mutex> g(g_bell_mu);
+		for (size_t i = 0; i < g_bell_pool.size(); i++)
+			if (g_bell_pool[i].device == c->device && g_bell_pool[i].forced_host == force_host) {
+				m = g_bell_pool[i];
+				g_bell_pool.erase(g_bell_pool.begin() + (long)i);
+				have = true;
+				break;
+			}
+	}
+	if (!have) {
+		const int rc = bell_alloc(c->device, force_host, &m);
+		if (rc)
+			return rc;
+	}
+	if (hipStreamCreateWithFlags(&c->res_stream, hipStreamNonBlocking) != hipSuccess) {
 		c->res_stream = nullptr;
+		std::lock_guard<std::mutex> g(g_bell_mu);
+		g_bell_pool.push_back(m);
 		return -XCSUM_ERR_HIP;
 	}
-	c->res_bell = (ResidentBell *)b;
-	c->res_vbell = (ResidentBell *)v;
-	c->res_seq = 0;
+	c->res_bell = m.h;
+	c->res_vbell = m.d;
+	c->res_bell_dev = m.dev;
+	c->res_bell_forced_host = m.forced_host;
+	c->res_done = m.done_h;
+	c->res_vdone = m.done_d;
+	/* no answers or left words of the previous owner (its kernel has
+	 * left); sequence numbers and generations continue from its last */
+	memset(c->res_done, 0, sizeof(ResidentDone));
+	c->res_seq = m.seq;
+	c->res_gen = m.gen;
+	c->res_live = false;
 	return 0;
 }
 
@@ -206,11 +334,24 @@ extern "C" int xcsum_ctx_set_resident(xcsum_ctx *c, int workgroups, uint32_t idl
  * when every workgroup has answered.  A workgroup that left at its idle
  * deadline while the request was on its way is relaunched with the mask of
  * those that did answer (they skip it), so every frame is served once. */
+static hipError_t resident_launch(xcsum_ctx *c, uint32_t served0, uint32_t skip_seq,
+				  uint64_t skip_mask)
+{
+	c->res_gen = c->res_gen + 1u ? c->res_gen + 1u : 1u;
+	const hipError_t e = launch_resident(c->res_vbell, c->res_vdone, c->d_err, c->res_wg,
+					     c->res_gen, served0, skip_seq, skip_mask, c->res_idle_us,
+					     c->res_stream);
+	c->res_live = e == hipSuccess;
+	return e;
+}
+
+static inline uint32_t done_word(const xcsum_ctx *c, int w, int k)
+{
+	return __atomic_load_n(&c->res_done->done[RB_DONE_STRIDE * w + k], __ATOMIC_ACQUIRE);
+}
+
 static int resident_call(xcsum_ctx *c, const CsumArgs &a)
 {
-	int rc = resident_ensure(c);
-	if (rc)
-		return rc;
 	ResidentBell *b = c->res_bell;
 	const int W = c->res_wg;
 	const uint32_t prev = c->res_seq;
@@ -227,57 +368,67 @@ static int resident_call(xcsum_ctx *c, const CsumArgs &a)
 	b->req[RB_N] = a.n;
 	b->req[RB_MODE] = a.mode;
 	b->req[RB_FLAGS] = a.flags;
-	if (c->res_live && hipStreamQuery(c->res_stream) != hipErrorNotReady)
-		c->res_live = false;   /* left idle (or failed: the launch below reports it) */
-	if (!c->res_live) {
-		HIPCHK(launch_resident(c->res_vbell, c->d_err, W, prev, 0u, 0ull, c->res_idle_us,
-				       c->res_stream));
-		c->res_live = true;
-	}
-	__atomic_store_n(&b->seq, seq, __ATOMIC_RELEASE);
+	b->req[RB_SEQ] = seq;
+	/* a workgroup that left after its idle time says so in its left word:
+	 * the others leave at about the same moment -- wait for them, then a
+	 * fresh launch (no HIP call while they stay) */
+	if (c->res_live)
+		for (int w = 0; w < W; w++)
+			if (done_word(c, w, RB_LEFT) == c->res_gen) {
+				HIPCHK(hipStreamSynchronize(c->res_stream));
+				c->res_live = false;
+				break;
+			}
+	if (!c->res_live)
+		HIPCHK(resident_launch(c, prev, 0u, 0ull));
+	bell_store(&b->seq, seq);
 	c->res_seq = seq;
 
 	const uint64_t all = W == 64 ? ~0ull : (1ull << W) - 1;
 	uint64_t pending = all;
 	const auto t0 = std::chrono::steady_clock::now();
 	for (uint64_t spin = 1;; spin++) {
-		for (int w = 0; w < W; w++)
-			if (((pending >> w) & 1ull) &&
-			    __atomic_load_n(&b->done[RB_DONE_STRIDE * w], __ATOMIC_ACQUIRE) == seq)
+		uint64_t gone = 0;
+		for (int w = 0; w < W; w++) {
+			if (!((pending >> w) & 1ull))
+				continue;
+			if (done_word(c, w, 0) == seq)
 				pending &= ~(1ull << w);
+			else if (done_word(c, w, RB_LEFT) == c->res_gen)
+				gone |= 1ull << w;
+		}
 		if (!pending)
 			return 0;
+		if (gone == pending) {
+			/* every workgroup still owing an answer left before it saw
+			 * the request: once all are gone (and done[] is final),
+			 * relaunch; those that answered skip it */
+			HIPCHK(hipStreamSynchronize(c->res_stream));
+			for (int w = 0; w < W; w++)
+				if (((pending >> w) & 1ull) && done_word(c, w, 0) == seq)
+					pending &= ~(1ull << w);
+			if (!pending)
+				return 0;
+			HIPCHK(resident_launch(c, prev, seq, all & ~pending));
+			continue;
+		}
 		__builtin_ia32_pause();
-		if (spin % 4096 == 0) {
+		if (spin % 65536 == 0) {
+			/* a fault, or a device that stopped answering: give up after
+			 * RES_TIMEOUT_S rather than spin forever */
 			const hipError_t q = hipStreamQuery(c->res_stream);
-			if (q == hipErrorNotReady) {
-				/* a device that stopped answering: give up after
-				 * RES_TIMEOUT_S rather than spin forever */
-				if (std::chrono::steady_clock::now() - t0 >
-				    std::chrono::seconds(RES_TIMEOUT_S)) {
-					(void)resident_stop(c);
-					t_hip_err = (int)hipErrorLaunchTimeOut;
-					t_hip_line = __LINE__;
-					return -XCSUM_ERR_HIP;
-				}
-				continue;
-			}
-			if (q != hipSuccess) {
+			if (q != hipErrorNotReady && q != hipSuccess) {
 				c->res_live = false;
 				t_hip_err = (int)q;
 				t_hip_line = __LINE__;
 				return -XCSUM_ERR_HIP;
 			}
-			/* every workgroup left; re-read done[] before relaunching:
-			 * the last ones may have answered just before leaving */
-			for (int w = 0; w < W; w++)
-				if (((pending >> w) & 1ull) &&
-				    __atomic_load_n(&b->done[RB_DONE_STRIDE * w], __ATOMIC_ACQUIRE) == seq)
-					pending &= ~(1ull << w);
-			if (!pending)
-				return 0;
-			HIPCHK(launch_resident(c->res_vbell, c->d_err, W, prev, seq, all & ~pending,
-					       c->res_idle_us, c->res_stream));
+			if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(RES_TIMEOUT_S)) {
+				(void)resident_stop(c);
+				t_hip_err = (int)hipErrorLaunchTimeOut;
+				t_hip_line = __LINE__;
+				return -XCSUM_ERR_HIP;
+			}
 		}
 	}
 }
@@ -971,7 +1122,7 @@ static int batch_host_resident(xcsum_ctx *c, uint8_t *h_umem, const struct xcsum
 			       uint32_t n, uint16_t *h_out, uint16_t *h_out_ip, uint32_t mode,
 			       uint32_t flags, const Region *zc, bool gather)
 {
-	if (n > c->res_max_frames || n > c->desc_cap || !c->v_stage[0])
+	if (n > c->res_max_frames || n > RB_DESC_CAP || !c->v_stage[0])
 		return RES_DECLINE;
 	uint64_t lo = UINT64_MAX, hi = 0;
 	for (uint32_t i = 0; i < n; i++) {
@@ -981,9 +1132,14 @@ static int batch_host_resident(xcsum_ctx *c, uint8_t *h_umem, const struct xcsum
 	if (!zc)
 		zc = find_region(c, h_umem + lo, h_umem + hi);   /* dense, registered */
 	const bool want_ip = (flags & XCSUM_F_IPHDR) != 0;
-	struct xcsum_desc *ds = c->h_dstage[0];
+	int rc = resident_ensure(c);
+	if (rc)
+		return rc;
+	/* the descriptors go into the doorbell (device memory: the kernel reads
+	 * them without a PCIe round trip) */
+	struct xcsum_desc *ds = c->res_bell->desc;
 	CsumArgs a;
-	a.desc = c->v_dstage[0];
+	a.desc = c->res_vbell->desc;
 	a.n = n;
 	a.out = c->v_out[0];
 	a.out_ip = want_ip ? c->v_out[0] + n : nullptr;
@@ -1024,7 +1180,7 @@ static int batch_host_resident(xcsum_ctx *c, uint8_t *h_umem, const struct xcsum
 		a.bias = alo;
 		a.flags = flags & (XCSUM_F_IPHDR | XCSUM_F_V4_RFC | XCSUM_F_VERIFY);
 	}
-	const int rc = resident_call(c, a);
+	rc = resident_call(c, a);
 	if (rc)
 		return rc;
 	Pending pd;

@@ -221,11 +221,16 @@ struct Ctx {
 	int res_wg;
 	uint32_t res_idle_us;
 	uint32_t res_max_frames;       /* larger batches take the launched path */
-	ResidentBell *res_bell;        /* pinned, coherent (lazy) */
-	ResidentBell *res_vbell;       /* its device alias */
+	ResidentBell *res_bell;        /* the doorbell as the host writes it (lazy) */
+	ResidentBell *res_vbell;       /* ... and as the kernel reads it */
+	bool res_bell_dev;             /* in device memory (else pinned host) */
+	bool res_bell_forced_host;     /* XCSUM_RESIDENT_BELL=host */
+	ResidentDone *res_done;        /* pinned, coherent */
+	ResidentDone *res_vdone;       /* its device alias */
 	hipStream_t res_stream;
 	bool res_live;                 /* launched, not yet seen gone */
 	uint32_t res_seq;              /* last sequence number issued (0: none) */
+	uint32_t res_gen;              /* generation of the last launch (skips 0) */
 };
 
 } /* namespace xcsum */

@@ -5,32 +5,51 @@
 
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include "xcsum.h"
 
 namespace xcsum {
 
 constexpr int RB_MAX_WG = 64;          /* workgroups (one bit each in a skip mask) */
 constexpr int RB_DONE_STRIDE = 16;     /* one 64-byte line per workgroup's done word */
+constexpr uint32_t RB_DESC_CAP = 4096; /* descriptors the doorbell holds */
 
 /* request words: device addresses as (lo, hi) pairs */
 enum {
 	RB_UMEM = 0, RB_DESC = 2, RB_OUT = 4, RB_OUT_IP = 6, RB_BIAS = 8,
 	RB_N = 10, RB_MODE = 11, RB_FLAGS = 12,
-	RB_REQ_WORDS = 13
+	RB_SEQ = 13,                   /* the request's own sequence number: a
+					  request whose echo differs from seq is
+					  not (yet) the one announced */
+	RB_REQ_WORDS = 14
 };
 
-/* In pinned, coherent host memory; the kernel sees it through its device
- * alias.  The host writes req[] and then seq (release); a workgroup answers
- * with done[RB_DONE_STRIDE * w] = seq.  Sequence numbers skip 0. */
-struct ResidentBell {
+/* The doorbell: fine-grained DEVICE memory the host writes through the PCIe
+ * BAR, so the workgroups poll their own HBM (tools/latency_probe: 1.5-2 us
+ * less per request than polling host memory over PCIe); pinned host memory
+ * where the device memory is not host-writable.  The host writes desc[] and
+ * req[], then seq; `stop` asks the workgroups to leave.  Sequence numbers
+ * skip 0. */
+struct alignas(64) ResidentBell {
 	uint32_t seq;
-	uint32_t stop;
+	uint32_t stop;                 /* next to seq: one 8-byte poll reads both */
 	uint32_t pad0[14];
 	uint32_t req[16];
+	struct xcsum_desc desc[RB_DESC_CAP];
+};
+
+/* The answers, in pinned host memory (the host spins on them locally):
+ * workgroup w stores done[RB_DONE_STRIDE * w] = seq when its part of request
+ * seq is done, and done[RB_DONE_STRIDE * w + 1] = gen (its launch's
+ * generation) as it leaves -- so the host learns that the workgroups are gone
+ * without asking the HIP runtime on every call. */
+constexpr int RB_LEFT = 1;
+struct alignas(64) ResidentDone {
 	uint32_t done[RB_MAX_WG * RB_DONE_STRIDE];
 };
 
-hipError_t launch_resident(ResidentBell *v_bell, unsigned long long *err, int wg, uint32_t served0,
-			   uint32_t skip_seq, uint64_t skip_mask, uint32_t idle_us, hipStream_t s);
+hipError_t launch_resident(ResidentBell *v_bell, ResidentDone *v_done, unsigned long long *err,
+			   int wg, uint32_t gen, uint32_t served0, uint32_t skip_seq,
+			   uint64_t skip_mask, uint32_t idle_us, hipStream_t s);
 
 } /* namespace xcsum */
 

@@ -5,9 +5,10 @@
  * batch is one trip through xudp_frame_send (tx.c:673-734).  As a kernel
  * launch per batch, a call costs a launch and a completion (~17-20 us,
  * DESIGN.md 5.8) for microseconds of work.  A resident server removes both:
- * W workgroups stay on the device and poll a doorbell in pinned host memory;
- * a batch is the request written there, a sequence number stored after it,
- * and a host spin on one "done" word per workgroup.
+ * W workgroups stay on the device and poll a doorbell (xcsum_resident.h:
+ * device memory the host writes through the BAR); a batch is the request and
+ * its descriptors written there, a sequence number stored after them, and a
+ * host spin on one "done" word per workgroup in pinned host memory.
  *
  * The work is the frame-group checksum loop itself (csum_loop<16, 2, 6, 2>
  * of xcsum_csum.h: every mode and flag, bit-exact with the launched kernels),
@@ -15,10 +16,12 @@
  * UMEM, or the context's pinned stage.
  *
  * Memory ordering (all vector memory operations):
- *   - wave 0 of a workgroup polls `seq` with system-scope acquire loads; the
- *     acquire invalidates the CU's L1 and the L2's non-coherent lines, so the
- *     request, descriptors and frame bytes the host wrote before `seq` are
- *     read fresh by every wave after the workgroup barrier that follows;
+ *   - wave 0 of a workgroup polls `seq` (and `stop`, the same 8 bytes) with
+ *     relaxed system-scope loads, then, once per request, a system-scope
+ *     acquire fence: it invalidates the CU's L1 and the L2's non-coherent
+ *     lines, so the request, descriptors and frame bytes the host wrote
+ *     before `seq` are read fresh by every wave after the workgroup barrier
+ *     that follows;
  *   - every wave ends a request with a system-scope release fence (its
  *     results and in-place stores written back to host memory), then the
  *     workgroup barrier, then thread 0 stores done[w] = seq;
@@ -39,11 +42,6 @@
 
 namespace xcsum {
 
-static __device__ __forceinline__ uint32_t ld_acquire_sys(const uint32_t *p)
-{
-	return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-
 static __device__ __forceinline__ uint32_t ld_relaxed_sys(const uint32_t *p)
 {
 	return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -58,7 +56,8 @@ static __device__ __forceinline__ uint64_t u64_of(uint32_t lo, uint32_t hi)
  * the workgroups of skip_mask (bit w), which served skip_seq already
  * (relaunch after a partial service, see the file comment) */
 template <int G, int U, int K>
-__global__ void __launch_bounds__(256) resident_kernel(ResidentBell *bell, unsigned long long *err,
+__global__ void __launch_bounds__(256) resident_kernel(const ResidentBell *bell, ResidentDone *done,
+						       unsigned long long *err, uint32_t gen,
 						       uint32_t served0, uint32_t skip_seq,
 						       uint64_t skip_mask, uint64_t idle_ticks)
 {
@@ -72,9 +71,15 @@ __global__ void __launch_bounds__(256) resident_kernel(ResidentBell *bell, unsig
 		if (threadIdx.x < 64) {
 			uint32_t s = served, go = 0;
 			for (;;) {
-				s = __builtin_amdgcn_readfirstlane(ld_acquire_sys(&bell->seq));
-				if (ld_acquire_sys(&bell->stop))
-					break;
+				/* seq and stop in one relaxed load: no cache maintenance
+				 * per poll (an acquire load here invalidated the L2 on
+				 * every poll: 12-55 us per request, tools/latency_probe) */
+				const uint64_t w = __hip_atomic_load(
+					(const uint64_t *)__builtin_assume_aligned(&bell->seq, 8),
+					__ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+				s = __builtin_amdgcn_readfirstlane((uint32_t)w);
+				if (__builtin_amdgcn_readfirstlane((uint32_t)(w >> 32)))
+					break;   /* stop */
 				if (s != served) {
 					go = 1;
 					break;
@@ -83,6 +88,10 @@ __global__ void __launch_bounds__(256) resident_kernel(ResidentBell *bell, unsig
 					break;
 				__builtin_amdgcn_s_sleep(1);
 			}
+			/* one acquire per request: the request, descriptors and frames
+			 * the host wrote before seq are read fresh from here on */
+			if (go)
+				__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
 			/* the request, read after the acquire of its sequence number */
 			uint32_t v = 0;
 			if (go && lane < RB_REQ_WORDS)
@@ -94,9 +103,20 @@ __global__ void __launch_bounds__(256) resident_kernel(ResidentBell *bell, unsig
 		}
 		__syncthreads();
 		const uint32_t s = __builtin_amdgcn_readfirstlane(cmd[0]);
-		if (s == 0u)
-			break;   /* stop or idle: the whole workgroup leaves (sequence
-				    numbers skip 0) */
+		if (s != 0u && __builtin_amdgcn_readfirstlane(cmd[1 + RB_SEQ]) != s) {
+			/* the request read is not the one announced (never seen; a
+			 * guard against serving stale words): poll again */
+			__syncthreads();
+			continue;
+		}
+		if (s == 0u) {
+			/* stop or idle: the whole workgroup leaves (sequence numbers
+			 * skip 0), and says so */
+			if (threadIdx.x == 0)
+				__hip_atomic_store(&done->done[RB_DONE_STRIDE * blockIdx.x + RB_LEFT], gen,
+						   __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+			break;
+		}
 		uint32_t r[RB_REQ_WORDS];
 #pragma unroll
 		for (int k = 0; k < RB_REQ_WORDS; k++)
@@ -119,21 +139,22 @@ __global__ void __launch_bounds__(256) resident_kernel(ResidentBell *bell, unsig
 		/* ... for every wave, before done[w] says so */
 		__syncthreads();
 		if (threadIdx.x == 0)
-			__hip_atomic_store(&bell->done[RB_DONE_STRIDE * blockIdx.x], s, __ATOMIC_RELEASE,
+			__hip_atomic_store(&done->done[RB_DONE_STRIDE * blockIdx.x], s, __ATOMIC_RELEASE,
 					   __HIP_MEMORY_SCOPE_SYSTEM);
 		served = s;
 		last = wall_clock64();
 	}
 }
 
-hipError_t launch_resident(ResidentBell *v_bell, unsigned long long *err, int wg, uint32_t served0,
-			   uint32_t skip_seq, uint64_t skip_mask, uint32_t idle_us, hipStream_t s)
+hipError_t launch_resident(ResidentBell *v_bell, ResidentDone *v_done, unsigned long long *err,
+			   int wg, uint32_t gen, uint32_t served0, uint32_t skip_seq,
+			   uint64_t skip_mask, uint32_t idle_us, hipStream_t s)
 {
 	if (wg <= 0 || wg > RB_MAX_WG)
 		return hipErrorInvalidValue;
 	(void)hipGetLastError();
-	hipLaunchKernelGGL((resident_kernel<16, 2, 6>), dim3((unsigned)wg), dim3(256), 0, s, v_bell, err,
-			   served0, skip_seq, skip_mask, (uint64_t)idle_us * 100ull);
+	hipLaunchKernelGGL((resident_kernel<16, 2, 6>), dim3((unsigned)wg), dim3(256), 0, s, v_bell, v_done,
+			   err, gen, served0, skip_seq, skip_mask, (uint64_t)idle_us * 100ull);
 	return hipGetLastError();
 }
 

@@ -9,7 +9,8 @@
  *   - fork() before any HIP call (the master/worker model forks its workers,
  *     test/case/lib.c:169); each child initialises HIP lazily through its own
  *     context and checks a batch;
- *   - two host threads, each with its own context and stream on device 0,
+ *   - two host threads, each with its own context and stream on device 0
+ *     (and later its own resident workgroups),
  *     running concurrently (one TX channel per thread, xudp/xsk.c:303-304);
  *   - the UMEM allocated exactly as xudp does (anon_map, include/common.h:37-41,
  *     xudp/xsk.c:234), registered, checksummed staged / zero-copy / in place.
@@ -342,6 +343,20 @@ static void *thread_main(void *arg)
 		memset(got, 0, 2 * n);
 		j->err |= xcsum_batch_host(c, umem, desc, n, got, mode, 0) != 0;
 		j->bad += count_diff(got, exp, n) != 0;
+	}
+	/* resident workgroups (xcsum_ctx_set_resident): both threads' servers
+	 * live at once, libxudp-sized batches from different places, device
+	 * batches on the thread's stream in between */
+	j->err |= xcsum_ctx_set_resident(c, 8, 0) != 0;
+	for (int it = 0; it < 4 * j->iters && !j->err; it++) {
+		const uint32_t first = (uint32_t)(it * 997u) % (n - 100);
+		memset(got, 0, 2 * 100);
+		j->err |= xcsum_batch_host(c, umem, desc + first, 100, got, mode, 0) != 0;
+		j->bad += count_diff(got, exp + first, 100) != 0;
+		if (it % 8 == 7) {
+			j->err |= xcsum_batch_device(c, d_umem, d_desc, n, d_out, mode, 0, 0, st) != 0;
+			j->err |= xcsum_sync(c, st) != 0;
+		}
 	}
 	(void)hipFree(d_umem);
 	(void)hipFree(d_desc);

@@ -360,7 +360,10 @@ int main(int argc, char **argv)
 		const struct variant *v = &vars[k];
 		if (v->registered)
 			CHECK(xcsum_register_umem(ctx, umem, bytes) == 0, "%s: register", v->name);
-		CHECK(xcsum_ctx_set_resident(ctx, v->resident, 0) == 0, "%s: resident", v->name);
+		/* $RING_RESIDENT_WG overrides the resident variants' workgroup count */
+		const char *rw = getenv("RING_RESIDENT_WG");
+		const int wg = v->resident && rw ? atoi(rw) : v->resident;
+		CHECK(xcsum_ctx_set_resident(ctx, wg, 0) == 0, "%s: resident", v->name);
 		for (int pass = bench; pass < (bench ? 1 + nbatch : 1); pass++) {
 			/* tx_batch_num is 100 (xudp.c:74); the bench batches as asked */
 			const uint32_t batch = pass ? batches[pass - 1] : 100u;

@@ -139,6 +139,22 @@ def test_resident_fresh_bytes_every_call(res_engine):
         res_engine.unregister_umem(umem)
 
 
+def test_resident_fresh_descriptors_every_call(res_engine):
+    """A different batch every call (size, frames, order) from one registered
+    UMEM: the descriptors the host wrote into the doorbell are the ones read."""
+    umem, desc = X.gen_frames_host(2000, 4, 0, 1472, seed=12, stride=2048, offset=64)
+    res_engine.register_umem(umem)
+    rng = np.random.default_rng(3)
+    try:
+        for it in range(300):
+            n = int(rng.integers(1, 400))
+            d = desc[rng.choice(len(desc), n, replace=False)]
+            got = host_batch(res_engine, umem, d, X.MODE_V4_RFC)
+            assert np.array_equal(got, oracle.batch(umem, d, X.MODE_V4_RFC)), it
+    finally:
+        res_engine.unregister_umem(umem)
+
+
 @pytest.mark.parametrize("idle_us", [1, 3, 30, 1000])
 def test_resident_leave_and_return(idle_us):
     """Workgroups that leave after idle_us come back with the next batch; with
@@ -213,3 +229,26 @@ def test_resident_packet_mirror(res_engine):
             assert int(f[24:26].view("<u2")[0]) == oracle.ip_header_rfc(f)
             z[40:42] = 0
             assert int(f[40:42].view("<u2")[0]) == oracle.batch(z, desc, X.MODE_V4_RFC)[0]
+
+
+def test_resident_host_doorbell(golden, monkeypatch):
+    """The fallback doorbell in pinned host memory (used where the CPU does
+    not map the device memory; XCSUM_RESIDENT_BELL=host forces it): same
+    results, in place included."""
+    monkeypatch.setenv("XCSUM_RESIDENT_BELL", "host")
+    e = X.Engine(0)
+    e.set_resident(4)
+    umem = golden["umem"].copy()
+    desc = golden_desc(golden)
+    e.register_umem(umem)
+    try:
+        for lo in range(0, len(desc), 250):
+            d = desc[lo:lo + 250]
+            got = host_batch(e, umem, d, X.MODE_AUTO, X.F_INPLACE | X.F_IPHDR)
+            fam = golden["family"][lo:lo + 250]
+            assert np.array_equal(got, np.where(fam == 6, golden["exp_v6"][lo:lo + 250],
+                                                golden["exp_legacy"][lo:lo + 250]))
+    finally:
+        e.unregister_umem(umem)
+        e.close()
+    check_inplace(golden, umem, desc)

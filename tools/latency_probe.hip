@@ -108,40 +108,88 @@ __global__ void __launch_bounds__(256) call_kernel(const uint8_t *umem, const De
 	}
 }
 
-struct Doorbell {
+struct alignas(64) Doorbell {
 	uint32_t seq;           /* host: request number */
+	uint32_t stop;          /* next to seq: one 8-byte poll reads both */
 	uint32_t n;
-	uint32_t stop;
 	uint32_t pad[29];
 	uint32_t done[64 * 32]; /* workgroup w: done[32 * w] = seq served */
 };
 
-/* W resident workgroups; every wave polls, so no barrier is needed */
+/* W resident workgroups; wave 0 of each polls, the workgroup follows.
+ * MODE 0: every poll a system-scope acquire load (L2 invalidate per poll);
+ * MODE 1: relaxed system-scope polls (no cache maintenance), one acquire
+ *         fence per request, release store of done;
+ * MODE 2: relaxed polls, no cache maintenance at all (fine-grained memory
+ *         only: nothing of it is cached), relaxed store of done after the
+ *         workgroup's stores have completed;
+ * MODE 3: MODE 1 with the doorbell (seq, stop, n) in fine-grained DEVICE
+ *         memory the host writes through the BAR: polls stay on the card. */
+template <int MODE>
 __global__ void __launch_bounds__(256) server_kernel(const uint8_t *umem, const Desc *desc,
-						     uint16_t *out, Doorbell *db, uint32_t idle_ms)
+						     uint16_t *out, Doorbell *db, uint32_t idle_ms,
+						     Doorbell *bell)
 {
+	__shared__ uint32_t cmd[2];
 	const uint32_t wave = blockIdx.x * 4 + (threadIdx.x >> 6), nwaves = gridDim.x * 4;
 	uint32_t served = 0;
 	uint64_t last = wall_clock64();
 	const uint64_t idle = (uint64_t)idle_ms * 100000ull;  /* 100 MHz */
 	for (;;) {
-		const uint32_t seq = __builtin_amdgcn_readfirstlane(ld_sys(&db->seq));
-		if (ld_sys(&db->stop))
-			break;
-		if (seq == served) {
-			if (wall_clock64() - last > idle)
-				break;
-			__builtin_amdgcn_s_sleep(2);
-			continue;
+		if (threadIdx.x < 64) {
+			uint32_t seq = served, go = 0;
+			for (;;) {
+				uint64_t w;
+				if (MODE == 0) {
+					seq = ld_sys(&bell->seq);
+					w = ((uint64_t)ld_sys(&bell->stop) << 32) | seq;
+				} else {
+					w = __hip_atomic_load((const uint64_t *)__builtin_assume_aligned(&bell->seq, 8), __ATOMIC_RELAXED,
+							      __HIP_MEMORY_SCOPE_SYSTEM);
+				}
+				w = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(w >> 32)) << 32) |
+				    __builtin_amdgcn_readfirstlane((uint32_t)w);
+				seq = (uint32_t)w;
+				if (w >> 32)
+					break;
+				if (seq != served) {
+					go = 1;
+					break;
+				}
+				if (wall_clock64() - last > idle)
+					break;
+				__builtin_amdgcn_s_sleep(1);
+			}
+			if ((MODE == 1 || MODE == 3) && go)
+				__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+			uint32_t n = 0;
+			if (go)
+				n = __hip_atomic_load(&bell->n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+			if (threadIdx.x == 0) {
+				cmd[0] = go ? seq : 0u;
+				cmd[1] = n;
+			}
 		}
-		const uint32_t n = __builtin_amdgcn_readfirstlane(ld_sys(&db->n));
+		__syncthreads();
+		const uint32_t seq = __builtin_amdgcn_readfirstlane(cmd[0]);
+		const uint32_t n = __builtin_amdgcn_readfirstlane(cmd[1]);
+		if (!seq)
+			break;
 		work(umem, desc, n, out, wave, nwaves);
+		if (MODE == 2)
+			__builtin_amdgcn_s_waitcnt(0);   /* this wave's stores done */
+		else
+			__builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+		__syncthreads();
+		if (threadIdx.x == 0) {
+			if (MODE == 2)
+				__hip_atomic_store(&db->done[32 * blockIdx.x], seq, __ATOMIC_RELAXED,
+						   __HIP_MEMORY_SCOPE_SYSTEM);
+			else
+				st_sys(&db->done[32 * blockIdx.x], seq);
+		}
 		served = seq;
 		last = wall_clock64();
-		/* every wave of the workgroup done, then one system-scope release */
-		__syncthreads();
-		if (threadIdx.x == 0)
-			st_sys(&db->done[32 * blockIdx.x], seq);
 	}
 }
 
@@ -170,6 +218,31 @@ int main(int argc, char **argv)
 	CHK(hipHostMalloc((void **)&flag, 256, hipHostMallocCoherent | hipHostMallocMapped));
 	CHK(hipHostMalloc((void **)&db, sizeof(Doorbell), hipHostMallocCoherent | hipHostMallocMapped));
 	CHK(hipMalloc((void **)&dcount, 4));
+	Doorbell *dbell = nullptr;   /* fine-grained device memory, host-writable */
+	CHK(hipExtMallocWithFlags((void **)&dbell, sizeof(Doorbell) + (64u << 10), hipDeviceMallocFinegrained));
+	{
+		hipPointerAttribute_t at;
+		memset(&at, 0, sizeof at);
+		const hipError_t e = hipPointerGetAttributes(&at, dbell);
+		printf("{\"probe\": \"finegrained_device_attr\", \"rc\": %d, \"type\": %d, "
+		       "\"host_ptr_is_dev_ptr\": %d, \"host_ptr_null\": %d}\n", (int)e, (int)at.type,
+		       at.hostPointer == (void *)dbell, at.hostPointer == nullptr);
+		/* host stores into it through the BAR: descriptor-sized copies */
+		static uint8_t src[64u << 10];
+		memset(src, 7, sizeof src);
+		for (uint32_t bytes : {1600u, 16384u, 65536u}) {
+			uint8_t *dst = (uint8_t *)(dbell + 1);
+			memcpy(dst, src, bytes);
+			_mm_sfence();
+			const double t = now_us();
+			for (int k = 0; k < 200; k++) {
+				memcpy(dst, src, bytes);
+				_mm_sfence();
+			}
+			printf("{\"probe\": \"host_memcpy_to_finegrained_device\", \"bytes\": %u, "
+			       "\"us\": %.2f}\n", bytes, (now_us() - t) / 200);
+		}
+	}
 	CHK(hipMemset(dcount, 0, 4));
 	memset(db, 0, sizeof(Doorbell));
 	for (uint32_t i = 0; i < NMAX * SLOT; i++)
@@ -273,20 +346,29 @@ int main(int argc, char **argv)
 	}
 
 	/* ---- resident workgroups polling a doorbell ---- */
-	const int wgs[] = {1, 8, 32};
+	const int wgs[] = {1, 4, 8, 16};
+	for (int mode = 0; mode < 4; mode++)
 	for (int W : wgs) {
 		for (int hbm = 0; hbm < 2; hbm++) {
 			memset(db, 0, sizeof(Doorbell));
-			hipLaunchKernelGGL(server_kernel, dim3(W), dim3(256), 0, s, hbm ? d_umem : umem,
-					   hbm ? d_desc : desc, hbm ? d_out : out, db, 500u);
+			Doorbell *bell = mode == 3 ? dbell : db;
+			if (mode == 3) {
+				CHK(hipMemset(dbell, 0, sizeof(Doorbell)));
+				CHK(hipDeviceSynchronize());
+			}
+#define SRV(M) hipLaunchKernelGGL(server_kernel<M>, dim3(W), dim3(256), 0, s, hbm ? d_umem : umem, \
+				  hbm ? d_desc : desc, hbm ? d_out : out, db, 500u, bell)
+			if (mode == 0) SRV(0); else if (mode == 1) SRV(1); else if (mode == 2) SRV(2); else SRV(3);
+#undef SRV
 			CHK(hipGetLastError());
 			uint32_t seq = 0;
 			bool dead = false;
 			for (uint32_t n : sizes) {
 				auto one = [&]() {
 					seq++;
-					db->n = n;
-					__atomic_store_n(&db->seq, seq, __ATOMIC_RELEASE);
+					bell->n = n;
+					__atomic_store_n(&bell->seq, seq, __ATOMIC_RELEASE);
+					_mm_sfence();
 					const double tw = now_us();
 					for (int w = 0; w < W; w++)
 						while (vload(&db->done[32 * w]) != seq) {
@@ -302,7 +384,8 @@ int main(int argc, char **argv)
 				for (int k = 0; k < iters && !dead; k++)
 					dead = !one();
 				char name[96];
-				snprintf(name, sizeof name, "resident_%s(%d wg)", hbm ? "hbm_frames" : "host_frames", W);
+				snprintf(name, sizeof name, "resident_m%d_%s(%d wg)", mode,
+					 hbm ? "hbm_frames" : "host_frames", W);
 				if (dead) {
 					printf("{\"probe\": \"%s\", \"frames\": %u, \"error\": \"no answer in 200 ms\"}\n",
 					       name, n);
@@ -310,7 +393,8 @@ int main(int argc, char **argv)
 				}
 				report(name, n, (now_us() - t0) / iters);
 			}
-			__atomic_store_n(&db->stop, 1u, __ATOMIC_RELEASE);
+			__atomic_store_n(&bell->stop, 1u, __ATOMIC_RELEASE);
+			_mm_sfence();
 			CHK(hipStreamSynchronize(s));
 			if (dead)
 				return 1;
