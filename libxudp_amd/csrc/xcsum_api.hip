@@ -127,6 +127,9 @@ static void env_resident(xcsum_ctx *c)
 	c->res_live = false;
 	c->res_seq = 0;
 	c->res_gen = 0;
+	c->res_trace = getenv("XCSUM_RESIDENT_TRACE") != nullptr;
+	c->res_calls = 0;
+	c->res_spin_us = c->res_call_us = 0;
 	const char *e = getenv("XCSUM_RESIDENT");
 	int w = 0;
 	unsigned idle = RES_IDLE_US, maxf = RES_MAX_FRAMES;
@@ -206,6 +209,18 @@ struct BellMem {
 };
 static std::mutex g_bell_mu;
 static std::vector<BellMem> g_bell_pool;   /* free doorbells */
+static std::vector<ResidentBell *> g_bell_all;   /* every doorbell (host view) */
+
+/* At process exit, every resident workgroup still polling is told to leave
+ * (they would anyway, after their idle time): no kernel outlives the
+ * process's last call by more than one poll.  Registered after HIP's own
+ * initialisation (at the first doorbell), so it runs before HIP's teardown. */
+static void bells_stop_at_exit()
+{
+	std::lock_guard<std::mutex> g(g_bell_mu);
+	for (ResidentBell *b : g_bell_all)
+		bell_store(&b->stop, 1u);
+}
 
 static int bell_alloc(int device, bool force_host, BellMem *m)
 {
@@ -249,6 +264,10 @@ static int bell_alloc(int device, bool force_host, BellMem *m)
 	m->gen = 0;
 	bell_store(&m->h->stop, 0u);
 	bell_store(&m->h->seq, 0u);
+	std::lock_guard<std::mutex> g(g_bell_mu);
+	if (g_bell_all.empty())
+		(void)atexit(bells_stop_at_exit);
+	g_bell_all.push_back(m->h);
 	return 0;
 }
 
@@ -368,7 +387,10 @@ static int resident_call(xcsum_ctx *c, const CsumArgs &a)
 	b->req[RB_N] = a.n;
 	b->req[RB_MODE] = a.mode;
 	b->req[RB_FLAGS] = a.flags;
-	b->req[RB_SEQ] = seq;
+	/* the echo last, after everything else of the request has left the
+	 * write-combining buffers: a workgroup that reads the echo equal to seq
+	 * has the whole request in the same 64-byte read */
+	bell_store(&b->req[RB_SEQ], seq);
 	/* a workgroup that left after its idle time says so in its left word:
 	 * the others leave at about the same moment -- wait for them, then a
 	 * fresh launch (no HIP call while they stay) */
@@ -383,6 +405,17 @@ static int resident_call(xcsum_ctx *c, const CsumArgs &a)
 		HIPCHK(resident_launch(c, prev, 0u, 0ull));
 	bell_store(&b->seq, seq);
 	c->res_seq = seq;
+	struct SpinTimer {   /* XCSUM_RESIDENT_TRACE */
+		xcsum_ctx *c;
+		std::chrono::steady_clock::time_point t;
+		~SpinTimer()
+		{
+			if (c->res_trace)
+				c->res_spin_us += std::chrono::duration<double, std::micro>(
+							  std::chrono::steady_clock::now() - t).count();
+		}
+	} spin_timer{c, c->res_trace ? std::chrono::steady_clock::now()
+				     : std::chrono::steady_clock::time_point()};
 
 	const uint64_t all = W == 64 ? ~0ull : (1ull << W) - 1;
 	uint64_t pending = all;
@@ -533,6 +566,11 @@ extern "C" void xcsum_ctx_destroy(xcsum_ctx *c)
 		return;
 	(void)hipSetDevice(c->device);
 	(void)resident_stop(c);
+	if (c->res_trace && c->res_calls)
+		fprintf(stderr, "xcsum resident: %llu calls, %.2f us per call, %.2f us of it "
+			"from the doorbell store to the last answer\n",
+			(unsigned long long)c->res_calls, c->res_call_us / c->res_calls,
+			c->res_spin_us / c->res_calls);
 	(void)hipDeviceSynchronize();
 	resident_free(c);
 	free_staging(c);
@@ -1124,6 +1162,8 @@ static int batch_host_resident(xcsum_ctx *c, uint8_t *h_umem, const struct xcsum
 {
 	if (n > c->res_max_frames || n > RB_DESC_CAP || !c->v_stage[0])
 		return RES_DECLINE;
+	const auto t_call = c->res_trace ? std::chrono::steady_clock::now()
+					 : std::chrono::steady_clock::time_point();
 	uint64_t lo = UINT64_MAX, hi = 0;
 	for (uint32_t i = 0; i < n; i++) {
 		if (h_desc[i].addr < lo) lo = h_desc[i].addr;
@@ -1188,6 +1228,11 @@ static int batch_host_resident(xcsum_ctx *c, uint8_t *h_umem, const struct xcsum
 	pd.count = n;
 	retire(pd, c->h_out[0], h_umem, h_desc, h_out, h_out_ip, mode,
 	       zc ? (flags & ~XCSUM_F_INPLACE) : flags);
+	if (c->res_trace) {
+		c->res_calls++;
+		c->res_call_us += std::chrono::duration<double, std::micro>(
+					  std::chrono::steady_clock::now() - t_call).count();
+	}
 	return 0;
 }
 

@@ -457,7 +457,8 @@ static hipError_t launch_t(const CsumArgs &a, int cus, int bpc, hipStream_t s)
 /* extra geometries for tuning sweeps only (make variant DEFS=-DXCSUM_SWEEP_GEOMS):
  * plain instantiation, not in the tested table */
 #ifdef XCSUM_SWEEP_GEOMS
-#define XCSUM_SWEEP_GEOMETRIES(X) X(16, 3, 6) X(16, 4, 6) X(32, 2, 3) X(32, 3, 3) X(16, 3, 5) X(8, 4, 12)
+#define XCSUM_SWEEP_GEOMETRIES(X) X(16, 3, 6) X(16, 4, 6) X(32, 2, 3) X(32, 3, 3) X(16, 3, 5) X(8, 4, 12) \
+	X(64, 2, 9) X(64, 1, 12) X(64, 2, 6) X(32, 2, 9) X(64, 3, 6)
 #else
 #define XCSUM_SWEEP_GEOMETRIES(X)
 #endif

@@ -231,6 +231,10 @@ struct Ctx {
 	bool res_live;                 /* launched, not yet seen gone */
 	uint32_t res_seq;              /* last sequence number issued (0: none) */
 	uint32_t res_gen;              /* generation of the last launch (skips 0) */
+	/* XCSUM_RESIDENT_TRACE=1: per-call timing, printed by xcsum_ctx_destroy */
+	bool res_trace;
+	uint64_t res_calls;
+	double res_spin_us, res_call_us;
 };
 
 } /* namespace xcsum */

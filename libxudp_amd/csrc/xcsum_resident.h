@@ -30,10 +30,10 @@ enum {
  * req[], then seq; `stop` asks the workgroups to leave.  Sequence numbers
  * skip 0. */
 struct alignas(64) ResidentBell {
-	uint32_t seq;
-	uint32_t stop;                 /* next to seq: one 8-byte poll reads both */
+	uint32_t seq;                  /* words 0-31 are read by one load per poll */
+	uint32_t stop;
 	uint32_t pad0[14];
-	uint32_t req[16];
+	uint32_t req[16];              /* word 16 on */
 	struct xcsum_desc desc[RB_DESC_CAP];
 };
 

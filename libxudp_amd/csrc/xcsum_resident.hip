@@ -69,18 +69,21 @@ __global__ void __launch_bounds__(256) resident_kernel(const ResidentBell *bell,
 	uint64_t last = wall_clock64();
 	for (;;) {
 		if (threadIdx.x < 64) {
-			uint32_t s = served, go = 0;
+			/* one load of the doorbell's first 128 bytes per poll: lane i
+			 * reads word i -- seq (0), stop (1) and the request (16...),
+			 * whose own echo of its sequence number (written after the
+			 * other request words, xcsum_api.hip resident_call) says the
+			 * words read with it belong to that request.  Relaxed: no cache
+			 * maintenance per poll (an acquire load per poll invalidated the
+			 * L2 every time: 12-55 us per request, tools/latency_probe). */
+			const uint32_t *words = (const uint32_t *)bell;
+			uint32_t s = served, go = 0, v = 0;
 			for (;;) {
-				/* seq and stop in one relaxed load: no cache maintenance
-				 * per poll (an acquire load here invalidated the L2 on
-				 * every poll: 12-55 us per request, tools/latency_probe) */
-				const uint64_t w = __hip_atomic_load(
-					(const uint64_t *)__builtin_assume_aligned(&bell->seq, 8),
-					__ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-				s = __builtin_amdgcn_readfirstlane((uint32_t)w);
-				if (__builtin_amdgcn_readfirstlane((uint32_t)(w >> 32)))
+				v = lane < 32 ? ld_relaxed_sys(words + lane) : 0u;
+				s = __builtin_amdgcn_readlane(v, 0);
+				if (__builtin_amdgcn_readlane(v, 1))
 					break;   /* stop */
-				if (s != served) {
+				if (s != served && __builtin_amdgcn_readlane(v, 16 + RB_SEQ) == s) {
 					go = 1;
 					break;
 				}
@@ -88,16 +91,12 @@ __global__ void __launch_bounds__(256) resident_kernel(const ResidentBell *bell,
 					break;
 				__builtin_amdgcn_s_sleep(1);
 			}
-			/* one acquire per request: the request, descriptors and frames
-			 * the host wrote before seq are read fresh from here on */
+			/* one acquire per request: the descriptors and frames the host
+			 * wrote before seq are read fresh from here on */
 			if (go)
 				__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
-			/* the request, read after the acquire of its sequence number */
-			uint32_t v = 0;
-			if (go && lane < RB_REQ_WORDS)
-				v = ld_relaxed_sys(&bell->req[lane]);
-			if (lane < RB_REQ_WORDS)
-				cmd[1 + lane] = v;
+			if (lane >= 16 && lane < 16 + RB_REQ_WORDS)
+				cmd[1 + lane - 16] = v;
 			if (lane == 0)
 				cmd[0] = go ? s : 0u;
 		}
