@@ -106,15 +106,83 @@ def elf_section(path, name):
 
 def lib_sha16():
     """SHA-256 prefix of the loaded libxcsum.so's device code (its
-    .hip_fatbin section, every gfx950 kernel): ties committed PMC counters to
-    the kernels that were timed.  Host-code edits (error-line numbers
-    included) leave it unchanged; falls back to the whole file."""
+    .hip_fatbin section, every gfx950 kernel).  Host-code edits (error-line
+    numbers included) leave it unchanged; falls back to the whole file."""
     import hashlib
     sec = elf_section(X.LIB_PATH, ".hip_fatbin")
     if sec is None:
         with open(X.LIB_PATH, "rb") as f:
             sec = f.read()
     return hashlib.sha256(sec).hexdigest()[:16]
+
+
+def _code_objects(sec):
+    """The gfx950 code objects in a .hip_fatbin section: one clang offload
+    bundle per translation unit ('__CLANG_OFFLOAD_BUNDLE__', entry count,
+    then per entry: offset, size, triple length, triple)."""
+    import struct
+    magic = b"__CLANG_OFFLOAD_BUNDLE__"
+    i = sec.find(magic)
+    while i >= 0:
+        n, = struct.unpack_from("<Q", sec, i + len(magic))
+        p = i + len(magic) + 8
+        for _ in range(n):
+            off, size, tlen = struct.unpack_from("<QQQ", sec, p)
+            triple = sec[p + 24:p + 24 + tlen]
+            p += 24 + tlen
+            if b"gfx950" in triple:
+                yield sec[i + off:i + off + size]
+        i = sec.find(magic, i + 1)
+
+
+def _elf_symbol_bytes(co, want):
+    """{symbol name: bytes} of the defined symbols of ELF code object `co`
+    whose names satisfy want(name)."""
+    import struct
+    shoff, = struct.unpack_from("<Q", co, 0x28)
+    shentsize, shnum = struct.unpack_from("<HH", co, 0x3A)
+    sh = [struct.unpack_from("<IIQQQQIIQQ", co, shoff + k * shentsize) for k in range(shnum)]
+    out = {}
+    for s_ in sh:
+        if s_[1] != 2:                      # SHT_SYMTAB
+            continue
+        strtab = sh[s_[6]]                  # sh_link
+        for e in range(s_[5] // 24):
+            nm, info, other, shndx, value, size = struct.unpack_from("<IBBHQQ", co, s_[4] + 24 * e)
+            if not shndx or shndx >= shnum or not size:
+                continue
+            name = co[strtab[4] + nm:co.index(b"\0", strtab[4] + nm)].decode()
+            if want(name):
+                sec_ = sh[shndx]
+                o = sec_[4] + (value - sec_[3])
+                out[name] = co[o:o + size]
+    return out
+
+
+def kernel_sha16(demangled):
+    """SHA-256 prefix of ONE kernel's gfx950 machine code and kernel
+    descriptor in the loaded libxcsum.so, named as rocprofv3 names it (e.g.
+    'void xcsum::csum_kernel<16, 2, 6, 0>(xcsum::CsumArgs)').  Ties PMC
+    counters to the kernel that was measured: other kernels, host code and
+    new translation units leave it unchanged.  None if not found."""
+    import hashlib
+    import re
+    m = re.search(r"xcsum::(\w+)<([^>]*)>", demangled or "")
+    if not m:
+        return None
+    args = [a.strip() for a in m.group(2).split(",")]
+    mangled = (f"{len(m.group(1))}{m.group(1)}I" + "".join(f"Li{a}E" for a in args) + "E")
+    sec = elf_section(X.LIB_PATH, ".hip_fatbin")
+    if sec is None:
+        return None
+    for co in _code_objects(sec):
+        syms = _elf_symbol_bytes(co, lambda n: mangled in n)
+        if syms:
+            h = hashlib.sha256()
+            for k in sorted(syms):          # the function and its .kd
+                h.update(k.encode() + b"\0" + syms[k])
+            return h.hexdigest()[:16]
+    return None
 
 
 def dist_env():
@@ -251,8 +319,12 @@ def pmc_traffic(cid, layout, flags, sha):
     """HBM bytes per launch from the rocprofv3 PMC summary committed under
     profiles/ (FETCH_SIZE + WRITE_SIZE passes of this bench, tools/pmc_summary.py);
     counters cannot be read inside the timed process itself.  Only counters
-    taken on this very library (same SHA-256 prefix) are reported; otherwise
-    traffic is null and the reason says which binary they came from."""
+    taken on this very kernel are reported: the summary records the kernel
+    rocprofv3 measured and the SHA-256 prefix of its machine code
+    (kernel_sha16), which must equal the loaded library's; older summaries
+    without it are matched on the whole device code (lib_sha16).  Otherwise
+    traffic is null and the reason says which code the counters came from.
+    Returns (bytes, source, reason, kernel hash)."""
     tag = f"{'_umem' if layout == 'umem' else ''}{'_f%x' % flags if flags else ''}"
     for rnd in ("r03", "r02", "r01", ""):
         path = os.path.join(ROOT, "profiles", rnd, f"pmc_config{cid}{tag}.json")
@@ -263,11 +335,18 @@ def pmc_traffic(cid, layout, flags, sha):
         except Exception:
             continue
         src = os.path.relpath(path, ROOT)
+        if j.get("kernel_sha16"):
+            kern = (j.get("kernel") or [None])[0]
+            mine = kernel_sha16(kern)
+            if mine != j["kernel_sha16"]:
+                return None, src, (f"counters in {src} were taken on {kern} with code "
+                                   f"{j['kernel_sha16']}, this build's is {mine}"), mine
+            return j.get("hbm_bytes_per_launch"), src, None, mine
         if j.get("lib_sha16") != sha:
             return None, src, (f"counters in {src} were taken on libxcsum.so "
-                               f"{j.get('lib_sha16') or '(unrecorded)'}, not this build {sha}")
-        return j.get("hbm_bytes_per_launch"), src, None
-    return None, None, "no PMC summary for this workload under profiles/"
+                               f"{j.get('lib_sha16') or '(unrecorded)'}, not this build {sha}"), None
+        return j.get("hbm_bytes_per_launch"), src, None, None
+    return None, None, "no PMC summary for this workload under profiles/", None
 
 
 def gpu_clocks(dev):
@@ -669,10 +748,12 @@ def main():
         slow = max(per_rank, key=lambda r: r[0])
         achieved = slow[1] / (slow[0] * 1e-3) / 1e9  # GB/s
         sha = lib_sha16()
-        traffic, traffic_src, why = pmc_traffic(args.config, args.layout, flags, sha)
+        traffic, traffic_src, why, ksha = pmc_traffic(args.config, args.layout, flags, sha)
         roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                 "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": traffic, "traffic_source": traffic_src}
+        if ksha:
+            roof["traffic_kernel_sha16"] = ksha   # the counted kernel's code, this build
         if why:
             roof["traffic_note"] = why
         # bytes the kernel must move per launch (every 64-byte line holding a

@@ -114,7 +114,9 @@ def test_bench_flags_and_algorithmic_bytes():
 
 def test_pmc_traffic_only_from_the_same_library(tmp_path, monkeypatch):
     """roofline.traffic comes from a committed PMC summary only when it was
-    taken on this very library (SHA-256 prefix); otherwise null + reason."""
+    taken on this very code: the counted kernel's machine-code hash
+    (kernel_sha16) when the summary has one, else the whole device code
+    (lib_sha16); otherwise null + reason."""
     import json
     import bench
     monkeypatch.setattr(bench, "ROOT", str(tmp_path))
@@ -123,13 +125,41 @@ def test_pmc_traffic_only_from_the_same_library(tmp_path, monkeypatch):
     (d / "pmc_config2.json").write_text(json.dumps({"hbm_bytes_per_launch": 123,
                                                     "lib_sha16": "aaaa"}))
     assert bench.pmc_traffic(2, "packed", 0, "aaaa")[0] == 123
-    t, src, why = bench.pmc_traffic(2, "packed", 0, "bbbb")
+    t, src, why, _ = bench.pmc_traffic(2, "packed", 0, "bbbb")
     assert t is None and src.endswith("pmc_config2.json") and "aaaa" in why
-    t, src, why = bench.pmc_traffic(3, "packed", 0, "aaaa")
+    t, src, why, _ = bench.pmc_traffic(3, "packed", 0, "aaaa")
     assert t is None and src is None and why
     (d / "pmc_config2_f3.json").write_text(json.dumps({"hbm_bytes_per_launch": 7,
                                                        "lib_sha16": "aaaa"}))
     assert bench.pmc_traffic(2, "packed", X.F_INPLACE | X.F_IPHDR, "aaaa")[0] == 7
+    # kernel-keyed: the library's own csum_kernel<16, 2, 6, 0> code decides,
+    # whatever the whole-library hash says
+    kern = "void xcsum::csum_kernel<16, 2, 6, 0>(xcsum::CsumArgs)"
+    ksha = bench.kernel_sha16(kern)
+    assert ksha and ksha != bench.kernel_sha16(
+        "void xcsum::csum_kernel<16, 2, 6, 2>(xcsum::CsumArgs)")
+    (d / "pmc_config4.json").write_text(json.dumps({"hbm_bytes_per_launch": 9, "kernel": [kern],
+                                                    "kernel_sha16": ksha,
+                                                    "lib_sha16": "zzzz"}))
+    t, _, why, got = bench.pmc_traffic(4, "packed", 0, "aaaa")
+    assert t == 9 and why is None and got == ksha
+    (d / "pmc_config4.json").write_text(json.dumps({"hbm_bytes_per_launch": 9, "kernel": [kern],
+                                                    "kernel_sha16": "0000"}))
+    t, _, why, got = bench.pmc_traffic(4, "packed", 0, "aaaa")
+    assert t is None and "0000" in why and got == ksha
+
+
+def test_kernel_sha16_reads_the_fatbin():
+    """kernel_sha16 finds every product checksum kernel in libxcsum.so's
+    gfx950 code objects (no GPU needed) and tells them apart."""
+    import bench
+    names = ["void xcsum::csum_kernel<16, 2, 6, 0>(xcsum::CsumArgs)",
+             "void xcsum::csum_kernel<16, 2, 6, 2>(xcsum::CsumArgs)",
+             "void xcsum::csum_kernel<64, 1, 9, 0>(xcsum::CsumArgs)",
+             "void xcsum::csum_stream_kernel<8>(xcsum::CsumArgs)"]
+    hs = [bench.kernel_sha16(n) for n in names]
+    assert all(hs) and len(set(hs)) == len(hs)
+    assert bench.kernel_sha16("void xcsum::no_such_kernel<1>(xcsum::CsumArgs)") is None
 
 
 def test_cpu_baseline_legs_report_their_seconds():
