@@ -252,3 +252,53 @@ def test_resident_host_doorbell(golden, monkeypatch):
         e.unregister_umem(umem)
         e.close()
     check_inplace(golden, umem, desc)
+
+
+@pytest.mark.parametrize("how", ["pageable", "registered"])
+def test_resident_inplace_skips_truncated_frame(res_engine, how):
+    """As test_gpu_host_path::test_inplace_skips_truncated_frame, through the
+    resident workgroups: a 20-byte runt before a valid frame is counted as
+    malformed and nothing outside the valid frames' check fields changes."""
+    umem, desc = X.gen_frames_host(2, 4, 50, 50, seed=3, align=1)
+    runt = np.zeros(1, dtype=X.DESC_DTYPE)
+    big = np.zeros(len(umem) + 20, dtype=np.uint8)
+    big[20:] = umem
+    big[:20] = 0x33
+    d = np.concatenate([runt, desc])
+    d["addr"][1:] += 20
+    d["len"][0] = 20
+    exp = oracle.batch(big, d, X.MODE_V4_RFC)
+    before = big.copy()
+    res_engine.take_errors()
+    if how == "registered":
+        res_engine.register_umem(big)
+    try:
+        got = host_batch(res_engine, big, d, X.MODE_V4_RFC, X.F_INPLACE)
+    finally:
+        if how == "registered":
+            res_engine.unregister_umem(big)
+    assert np.array_equal(got, exp) and got[0] == 0
+    assert res_engine.take_errors() == 1
+    changed = set(np.nonzero(big != before)[0].tolist())
+    assert changed <= {int(a) + k for a in d["addr"][1:] for k in (40, 41)}
+
+
+def test_resident_auto_mixed_families_verify_iphdr(res_engine, golden):
+    """AUTO mode over mixed IPv4/IPv6 fixtures with V4_RFC, then VERIFY +
+    IPHDR on the frames the first call completed in place."""
+    umem = golden["umem"].copy()
+    desc = golden_desc(golden)
+    fam = golden["family"]
+    res_engine.register_umem(umem)
+    try:
+        for lo in range(0, len(desc), 400):
+            d = desc[lo:lo + 400]
+            got = host_batch(res_engine, umem, d, X.MODE_AUTO,
+                             X.F_V4_RFC | X.F_INPLACE | X.F_IPHDR)
+            f = fam[lo:lo + 400]
+            assert np.array_equal(got, np.where(f == 6, golden["exp_v6"][lo:lo + 400],
+                                                golden["exp_rfc"][lo:lo + 400]))
+            assert not host_batch(res_engine, umem, d, X.MODE_AUTO,
+                                  X.F_VERIFY | X.F_IPHDR).any()
+    finally:
+        res_engine.unregister_umem(umem)
