@@ -217,9 +217,13 @@ static std::vector<ResidentBell *> g_bell_all;   /* every doorbell (host view) *
  * initialisation (at the first doorbell), so it runs before HIP's teardown. */
 static void bells_stop_at_exit()
 {
-	std::lock_guard<std::mutex> g(g_bell_mu);
+	/* a thread still inside resident_ensure at exit holds the lock: skip
+	 * rather than wait (the workgroups leave after their idle time anyway) */
+	if (!g_bell_mu.try_lock())
+		return;
 	for (ResidentBell *b : g_bell_all)
 		bell_store(&b->stop, 1u);
+	g_bell_mu.unlock();
 }
 
 static int bell_alloc(int device, bool force_host, BellMem *m)
