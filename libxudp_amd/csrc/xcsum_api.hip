@@ -45,6 +45,7 @@ extern "C" int xcsum_last_hip_error(int *line, const char **name)
 static constexpr uint32_t RES_IDLE_US = 20000;     /* workgroups leave after 20 ms idle */
 static constexpr uint32_t RES_MAX_FRAMES = 4096;   /* larger batches are launched */
 static constexpr int RES_TIMEOUT_S = 30;           /* no answer: the call fails */
+static constexpr uint32_t RES_PUSH_MAX = 64u << 10; /* batches the CPU pushes (bytes) */
 
 #ifdef XCSUM_DEBUG_BOUNDS
 namespace xcsum {
@@ -128,6 +129,13 @@ static void env_resident(xcsum_ctx *c)
 	c->res_seq = 0;
 	c->res_gen = 0;
 	c->res_trace = getenv("XCSUM_RESIDENT_TRACE") != nullptr;
+	c->res_push = nullptr;
+	{
+		/* XCSUM_RESIDENT_PUSH=bytes: largest batch pushed (0: never) */
+		const char *pe = getenv("XCSUM_RESIDENT_PUSH");
+		const unsigned long v = pe ? strtoul(pe, nullptr, 0) : RES_PUSH_MAX;
+		c->res_push_max = v < RB_PUSH_CAP ? (uint32_t)v : RB_PUSH_CAP;
+	}
 	c->res_calls = 0;
 	c->res_spin_us = c->res_call_us = 0;
 	const char *e = getenv("XCSUM_RESIDENT");
@@ -203,6 +211,8 @@ struct BellMem {
 	bool dev;                /* the doorbell is device memory */
 	ResidentBell *h, *d;     /* as the host writes it, as the kernel reads it */
 	ResidentDone *done_h, *done_d;
+	uint8_t *push;           /* device-memory stage for pushed frames (CPU and GPU
+				    address; null with a host doorbell) */
 	uint32_t seq, gen;       /* last sequence number / generation issued on it:
 				    a later owner continues from there, so no
 				    stale view of seq can announce a request */
@@ -264,6 +274,16 @@ static int bell_alloc(int device, bool force_host, BellMem *m)
 	}
 	m->done_h = (ResidentDone *)h;
 	m->done_d = (ResidentDone *)v;
+	/* the push stage: uncached device memory the CPU writes, like the
+	 * doorbell (optional: without it small batches are read over PCIe) */
+	m->push = nullptr;
+	void *ps = nullptr;
+	if (m->dev && hipExtMallocWithFlags(&ps, RB_PUSH_CAP, hipDeviceMallocUncached) == hipSuccess) {
+		if (cpu_maps(ps))
+			m->push = (uint8_t *)ps;
+		else
+			(void)hipFree(ps);
+	}
 	m->seq = 0;
 	m->gen = 0;
 	bell_store(&m->h->stop, 0u);
@@ -284,13 +304,14 @@ static void resident_free(xcsum_ctx *c)
 		std::lock_guard<std::mutex> g(g_bell_mu);
 		g_bell_pool.push_back(BellMem{c->device, c->res_bell_forced_host, c->res_bell_dev,
 					      c->res_bell, c->res_vbell, c->res_done, c->res_vdone,
-					      c->res_seq, c->res_gen});
+					      c->res_push, c->res_seq, c->res_gen});
 	}
 	c->res_stream = nullptr;
 	c->res_bell = nullptr;
 	c->res_vbell = nullptr;
 	c->res_done = nullptr;
 	c->res_vdone = nullptr;
+	c->res_push = nullptr;
 	c->res_live = false;
 }
 
@@ -329,6 +350,7 @@ static int resident_ensure(xcsum_ctx *c)
 	c->res_bell_forced_host = m.forced_host;
 	c->res_done = m.done_h;
 	c->res_vdone = m.done_d;
+	c->res_push = m.push;
 	/* no answers or left words of the previous owner (its kernel has
 	 * left); sequence numbers and generations continue from its last */
 	memset(c->res_done, 0, sizeof(ResidentDone));
@@ -1192,24 +1214,38 @@ static int batch_host_resident(xcsum_ctx *c, uint8_t *h_umem, const struct xcsum
 	a.bias = 0;
 	a.ord = order_identity(n);
 	a.dense = a.ord;
-	if (zc) {
-		memcpy(ds, h_desc, (size_t)n * sizeof(*ds));
-		a.umem = zc->dev + (h_umem - zc->host);
-		a.flags = flags & (XCSUM_F_INPLACE | XCSUM_F_IPHDR | XCSUM_F_V4_RFC | XCSUM_F_VERIFY);
-	} else if (gather) {
+	/* the frames' bytes gathered, each at its 16-byte phase (stage_off) */
+	uint64_t gbytes = 0;
+	for (uint32_t k = 0; k < n; k++)
+		gbytes = stage_off(gbytes, h_desc[k].addr) + h_desc[k].len;
+	bool kernel_inplace = false;   /* the kernel writes the host frames itself */
+	auto gather_into = [&](uint8_t *stage) {
 		uint64_t pos = 0;
-		for (uint32_t k = 0; k < n; k++)
-			pos = stage_off(pos, h_desc[k].addr) + h_desc[k].len;
-		if (pos > DIRECT_MAX)
-			return RES_DECLINE;
-		pos = 0;
 		for (uint32_t k = 0; k < n; k++) {
 			const struct xcsum_desc &d = h_desc[k];
 			const uint64_t off = stage_off(pos, d.addr);
-			memcpy(c->h_stage[0] + off, h_umem + d.addr, d.len);
+			memcpy(stage + off, h_umem + d.addr, d.len);
 			ds[k] = xcsum_desc{off, d.len, 0};
 			pos = off + d.len;
 		}
+	};
+	if (c->res_push && gbytes <= c->res_push_max) {
+		/* small batch: the CPU pushes the frame bytes into device memory
+		 * through the BAR (one write burst), so the kernel reads HBM
+		 * instead of waiting a PCIe round trip for them; in-place fields
+		 * are written on the host (retire) */
+		gather_into(c->res_push);
+		a.umem = c->res_push;
+		a.flags = flags & (XCSUM_F_IPHDR | XCSUM_F_V4_RFC | XCSUM_F_VERIFY);
+	} else if (zc) {
+		memcpy(ds, h_desc, (size_t)n * sizeof(*ds));
+		a.umem = zc->dev + (h_umem - zc->host);
+		a.flags = flags & (XCSUM_F_INPLACE | XCSUM_F_IPHDR | XCSUM_F_V4_RFC | XCSUM_F_VERIFY);
+		kernel_inplace = true;
+	} else if (gather) {
+		if (gbytes > DIRECT_MAX)
+			return RES_DECLINE;
+		gather_into(c->h_stage[0]);
 		a.umem = c->v_stage[0];
 		a.flags = flags & (XCSUM_F_IPHDR | XCSUM_F_V4_RFC | XCSUM_F_VERIFY);
 	} else {
@@ -1231,7 +1267,7 @@ static int batch_host_resident(xcsum_ctx *c, uint8_t *h_umem, const struct xcsum
 	pd.first = 0;
 	pd.count = n;
 	retire(pd, c->h_out[0], h_umem, h_desc, h_out, h_out_ip, mode,
-	       zc ? (flags & ~XCSUM_F_INPLACE) : flags);
+	       kernel_inplace ? (flags & ~XCSUM_F_INPLACE) : flags);
 	if (c->res_trace) {
 		c->res_calls++;
 		c->res_call_us += std::chrono::duration<double, std::micro>(

@@ -227,6 +227,8 @@ struct Ctx {
 	bool res_bell_forced_host;     /* XCSUM_RESIDENT_BELL=host */
 	ResidentDone *res_done;        /* pinned, coherent */
 	ResidentDone *res_vdone;       /* its device alias */
+	uint8_t *res_push;             /* device-memory stage for pushed batches */
+	uint32_t res_push_max;         /* largest pushed batch (bytes) */
 	hipStream_t res_stream;
 	bool res_live;                 /* launched, not yet seen gone */
 	uint32_t res_seq;              /* last sequence number issued (0: none) */

@@ -12,6 +12,7 @@ namespace xcsum {
 constexpr int RB_MAX_WG = 64;          /* workgroups (one bit each in a skip mask) */
 constexpr int RB_DONE_STRIDE = 16;     /* one 64-byte line per workgroup's done word */
 constexpr uint32_t RB_DESC_CAP = 4096; /* descriptors the doorbell holds */
+constexpr uint32_t RB_PUSH_CAP = 128u << 10;   /* push stage bytes (xcsum_api.hip) */
 
 /* request words: device addresses as (lo, hi) pairs */
 enum {

@@ -19,8 +19,13 @@ from test_gpu_host_path import check_inplace, host_batch
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture
-def res_engine():
+@pytest.fixture(params=["push", "nopush"])
+def res_engine(request, monkeypatch):
+    """A context with 8 resident workgroups; batches up to 64 KiB of frame
+    bytes are pushed into device memory by the CPU ("push", the default) or,
+    with XCSUM_RESIDENT_PUSH=0, read by the kernel where they are."""
+    if request.param == "nopush":
+        monkeypatch.setenv("XCSUM_RESIDENT_PUSH", "0")
     e = X.Engine(0)
     e.set_resident(8)
     yield e
