@@ -258,15 +258,14 @@ int xcsum_unregister_umem(xcsum_ctx *ctx, void *base);
 /* Resident workgroups for small host batches (libxudp sends in batches of
  * tx_batch_num = 100 frames, xudp/xudp.c:74; tx.c:673-734 is one batch).
  * `workgroups` (1-64; 16 is a good start) checksum workgroups stay on the
- * device and poll a doorbell in device memory that the host writes through
- * the PCIe BAR (pinned host memory where the CPU does not map it): a host
- * batch of at most 4096 frames whose frames lie in a registered UMEM (read
- * in place) or fit the pinned stage (256 KiB) then costs a doorbell store and
- * a spin on the answer instead of a kernel launch and its completion (TX
- * loop, 100 MTU frames per call: 11-16 us instead of 23-32 us).  Results are
- * the same bytes.  The workgroups leave after `idle_us` (0: 20000) without a
- * batch and come back with the next one.  0 workgroups: off (the default;
- * env XCSUM_RESIDENT="W[,idle_us[,max_frames]]" sets it at context creation).
+ * device and poll a doorbell in pinned host memory: a host batch of at most
+ * 4096 frames whose frames lie in a registered UMEM (read in place) or fit
+ * the pinned stage (256 KiB) then costs a doorbell store and a spin on the
+ * answer instead of a kernel launch and its completion (TX loop, 100 MTU
+ * frames per call: 12-18 us instead of 23-32 us).  Results are the same
+ * bytes.  The workgroups leave after `idle_us` (0: 20000) without a batch and
+ * come back with the next one.  0 workgroups: off (the default; env
+ * XCSUM_RESIDENT="W[,idle_us[,max_frames]]" sets it at context creation).
  * While they are resident, a device-wide synchronisation by others
  * (hipDeviceSynchronize, torch.cuda.synchronize) waits until they leave, i.e.
  * up to idle_us after this context's last batch; the library's own

@@ -8,7 +8,6 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
-#include <unistd.h>
 #include <new>
 #include <chrono>
 #include <mutex>
@@ -45,7 +44,6 @@ extern "C" int xcsum_last_hip_error(int *line, const char **name)
 static constexpr uint32_t RES_IDLE_US = 20000;     /* workgroups leave after 20 ms idle */
 static constexpr uint32_t RES_MAX_FRAMES = 4096;   /* larger batches are launched */
 static constexpr int RES_TIMEOUT_S = 30;           /* no answer: the call fails */
-static constexpr uint32_t RES_PUSH_MAX = 64u << 10; /* batches the CPU pushes (bytes) */
 
 #ifdef XCSUM_DEBUG_BOUNDS
 namespace xcsum {
@@ -120,8 +118,6 @@ static void env_resident(xcsum_ctx *c)
 	c->res_max_frames = RES_MAX_FRAMES;
 	c->res_bell = nullptr;
 	c->res_vbell = nullptr;
-	c->res_bell_dev = false;
-	c->res_bell_forced_host = false;
 	c->res_done = nullptr;
 	c->res_vdone = nullptr;
 	c->res_stream = nullptr;
@@ -129,13 +125,6 @@ static void env_resident(xcsum_ctx *c)
 	c->res_seq = 0;
 	c->res_gen = 0;
 	c->res_trace = getenv("XCSUM_RESIDENT_TRACE") != nullptr;
-	c->res_push = nullptr;
-	{
-		/* XCSUM_RESIDENT_PUSH=bytes: largest batch pushed (0: never) */
-		const char *pe = getenv("XCSUM_RESIDENT_PUSH");
-		const unsigned long v = pe ? strtoul(pe, nullptr, 0) : RES_PUSH_MAX;
-		c->res_push_max = v < RB_PUSH_CAP ? (uint32_t)v : RB_PUSH_CAP;
-	}
 	c->res_calls = 0;
 	c->res_spin_us = c->res_call_us = 0;
 	const char *e = getenv("XCSUM_RESIDENT");
@@ -153,10 +142,8 @@ static void env_resident(xcsum_ctx *c)
  * request written there and a spin on the workgroups' done words instead of
  * a launch and its completion. */
 
-/* A doorbell word, visible to the device at once and after everything
- * written before it: the BAR mapping is write-combining, whose stores x86
- * does not order with later stores, so a store fence drains the request and
- * descriptors first, and another pushes the word itself out. */
+/* A doorbell word, visible to the device after everything written before it
+ * (the request and the descriptors): a release store between store fences. */
 static inline void bell_store(uint32_t *p, uint32_t v)
 {
 	__builtin_ia32_sfence();
@@ -183,36 +170,16 @@ static int resident_stop(xcsum_ctx *c)
 	return 0;
 }
 
-/* Does the CPU map this address (fine-grained VRAM behind a large PCIe BAR
- * shares the GPU's virtual address)?  Asked of the kernel: write() from an
- * unmapped address fails with EFAULT instead of faulting the process. */
-static bool cpu_maps(const void *p)
-{
-	int fd[2];
-	if (pipe(fd) != 0)
-		return false;
-	const bool ok = write(fd[1], p, 8) == 8;
-	close(fd[0]);
-	close(fd[1]);
-	return ok;
-}
-
-/* Doorbell memory: the doorbell in UNCACHED device memory the host writes
- * through the BAR (uncached: host stores land in HBM behind the L2's back, so
- * no L2 line of it may ever be served -- not even one left by an earlier use
- * of the same addresses), or in pinned host memory where the CPU does not
- * map device memory; the done words in pinned host memory.  Allocated once
- * per process and device and kept for later contexts: contexts come and go
- * (one per test), the memory a resident kernel polls is never freed and
- * reallocated under another mapping. */
+/* Doorbell memory: the doorbell (request + descriptors) and the done words in
+ * pinned, coherent host memory, which the workgroups read over PCIe.  (A
+ * doorbell in device memory written through the BAR was measured and
+ * dropped: DESIGN.md 5.10.)  Allocated once per process and device and kept
+ * for later contexts: contexts come and go (one per test), the memory a
+ * resident kernel polls is never freed and reallocated under it. */
 struct BellMem {
 	int device;
-	bool forced_host;        /* XCSUM_RESIDENT_BELL=host asked for it */
-	bool dev;                /* the doorbell is device memory */
 	ResidentBell *h, *d;     /* as the host writes it, as the kernel reads it */
 	ResidentDone *done_h, *done_d;
-	uint8_t *push;           /* device-memory stage for pushed frames (CPU and GPU
-				    address; null with a host doorbell) */
 	uint32_t seq, gen;       /* last sequence number / generation issued on it:
 				    a later owner continues from there, so no
 				    stale view of seq can announce a request */
@@ -236,30 +203,16 @@ static void bells_stop_at_exit()
 	g_bell_mu.unlock();
 }
 
-static int bell_alloc(int device, bool force_host, BellMem *m)
+static int bell_alloc(int device, BellMem *m)
 {
 	void *d = nullptr, *h = nullptr, *v = nullptr;
 	m->device = device;
-	m->forced_host = force_host;
-	m->dev = false;
-	if (!force_host &&
-	    hipExtMallocWithFlags(&d, sizeof(ResidentBell), hipDeviceMallocUncached) == hipSuccess) {
-		if (cpu_maps(d)) {
-			h = d;   /* one virtual address for CPU and GPU */
-			m->dev = true;
-		} else {
-			(void)hipFree(d);
-			d = nullptr;
-		}
-	}
-	if (!m->dev) {
-		if (hipHostMalloc(&h, sizeof(ResidentBell), hipHostMallocCoherent | hipHostMallocMapped) !=
-			    hipSuccess)
-			return -XCSUM_ERR_NOMEM;
-		if (hipHostGetDevicePointer(&d, h, 0) != hipSuccess) {
-			(void)hipHostFree(h);
-			return -XCSUM_ERR_HIP;
-		}
+	if (hipHostMalloc(&h, sizeof(ResidentBell), hipHostMallocCoherent | hipHostMallocMapped) !=
+		    hipSuccess)
+		return -XCSUM_ERR_NOMEM;
+	if (hipHostGetDevicePointer(&d, h, 0) != hipSuccess) {
+		(void)hipHostFree(h);
+		return -XCSUM_ERR_HIP;
 	}
 	m->h = (ResidentBell *)h;
 	m->d = (ResidentBell *)d;
@@ -269,25 +222,14 @@ static int bell_alloc(int device, bool force_host, BellMem *m)
 	    hipHostGetDevicePointer(&v, h, 0) != hipSuccess) {
 		if (h)
 			(void)hipHostFree(h);
-		(void)(m->dev ? hipFree(m->d) : hipHostFree(m->h));
+		(void)hipHostFree(m->h);
 		return -XCSUM_ERR_NOMEM;
 	}
 	m->done_h = (ResidentDone *)h;
 	m->done_d = (ResidentDone *)v;
-	/* the push stage: uncached device memory the CPU writes, like the
-	 * doorbell (optional: without it small batches are read over PCIe) */
-	m->push = nullptr;
-	void *ps = nullptr;
-	if (m->dev && hipExtMallocWithFlags(&ps, RB_PUSH_CAP, hipDeviceMallocUncached) == hipSuccess) {
-		if (cpu_maps(ps))
-			m->push = (uint8_t *)ps;
-		else
-			(void)hipFree(ps);
-	}
 	m->seq = 0;
 	m->gen = 0;
-	bell_store(&m->h->stop, 0u);
-	bell_store(&m->h->seq, 0u);
+	memset(m->h, 0, sizeof(ResidentBell));
 	std::lock_guard<std::mutex> g(g_bell_mu);
 	if (g_bell_all.empty())
 		(void)atexit(bells_stop_at_exit);
@@ -302,16 +244,14 @@ static void resident_free(xcsum_ctx *c)
 	if (c->res_bell) {
 		/* back to the pool; its kernel has left (resident_stop first) */
 		std::lock_guard<std::mutex> g(g_bell_mu);
-		g_bell_pool.push_back(BellMem{c->device, c->res_bell_forced_host, c->res_bell_dev,
-					      c->res_bell, c->res_vbell, c->res_done, c->res_vdone,
-					      c->res_push, c->res_seq, c->res_gen});
+		g_bell_pool.push_back(BellMem{c->device, c->res_bell, c->res_vbell, c->res_done,
+					      c->res_vdone, c->res_seq, c->res_gen});
 	}
 	c->res_stream = nullptr;
 	c->res_bell = nullptr;
 	c->res_vbell = nullptr;
 	c->res_done = nullptr;
 	c->res_vdone = nullptr;
-	c->res_push = nullptr;
 	c->res_live = false;
 }
 
@@ -319,14 +259,12 @@ static int resident_ensure(xcsum_ctx *c)
 {
 	if (c->res_bell)
 		return 0;
-	const char *where = getenv("XCSUM_RESIDENT_BELL");   /* "host": force pinned memory */
-	const bool force_host = where && strcmp(where, "host") == 0;
 	BellMem m;
 	bool have = false;
 	{
 		std::lock_guard<std::mutex> g(g_bell_mu);
 		for (size_t i = 0; i < g_bell_pool.size(); i++)
-			if (g_bell_pool[i].device == c->device && g_bell_pool[i].forced_host == force_host) {
+			if (g_bell_pool[i].device == c->device) {
 				m = g_bell_pool[i];
 				g_bell_pool.erase(g_bell_pool.begin() + (long)i);
 				have = true;
@@ -334,7 +272,7 @@ static int resident_ensure(xcsum_ctx *c)
 			}
 	}
 	if (!have) {
-		const int rc = bell_alloc(c->device, force_host, &m);
+		const int rc = bell_alloc(c->device, &m);
 		if (rc)
 			return rc;
 	}
@@ -346,11 +284,8 @@ static int resident_ensure(xcsum_ctx *c)
 	}
 	c->res_bell = m.h;
 	c->res_vbell = m.d;
-	c->res_bell_dev = m.dev;
-	c->res_bell_forced_host = m.forced_host;
 	c->res_done = m.done_h;
 	c->res_vdone = m.done_d;
-	c->res_push = m.push;
 	/* no answers or left words of the previous owner (its kernel has
 	 * left); sequence numbers and generations continue from its last */
 	memset(c->res_done, 0, sizeof(ResidentDone));
@@ -395,7 +330,25 @@ static inline uint32_t done_word(const xcsum_ctx *c, int w, int k)
 	return __atomic_load_n(&c->res_done->done[RB_DONE_STRIDE * w + k], __ATOMIC_ACQUIRE);
 }
 
-static int resident_call(xcsum_ctx *c, const CsumArgs &a)
+/* After every workgroup answered request seq: did one refuse it (a
+ * descriptor outside the request's limit, RB_BAD)?  Then the call fails --
+ * -XCSUM_ERR_INVAL, the frames' descriptors are the caller's -- and says
+ * which on stderr. */
+static int resident_bad(const xcsum_ctx *c, uint32_t seq)
+{
+	for (int w = 0; w < c->res_wg; w++) {
+		const uint32_t *o = &c->res_done->done[RB_DONE_STRIDE * w + RB_BAD];
+		if (__atomic_load_n(&o[0], __ATOMIC_ACQUIRE) == seq) {
+			fprintf(stderr, "xcsum resident: request %u: descriptor %u {addr %#llx, len %u} "
+				"outside the frames' buffer\n", seq, o[1],
+				(unsigned long long)(((uint64_t)o[3] << 32) | o[2]), o[4]);
+			return -XCSUM_ERR_INVAL;
+		}
+	}
+	return 0;
+}
+
+static int resident_call(xcsum_ctx *c, const CsumArgs &a, uint64_t limit)
 {
 	ResidentBell *b = c->res_bell;
 	const int W = c->res_wg;
@@ -413,6 +366,7 @@ static int resident_call(xcsum_ctx *c, const CsumArgs &a)
 	b->req[RB_N] = a.n;
 	b->req[RB_MODE] = a.mode;
 	b->req[RB_FLAGS] = a.flags;
+	put64(RB_LIMIT, limit);
 	/* the echo last, after everything else of the request has left the
 	 * write-combining buffers: a workgroup that reads the echo equal to seq
 	 * has the whole request in the same 64-byte read */
@@ -457,7 +411,7 @@ static int resident_call(xcsum_ctx *c, const CsumArgs &a)
 				gone |= 1ull << w;
 		}
 		if (!pending)
-			return 0;
+			return resident_bad(c, seq);
 		if (gone == pending) {
 			/* every workgroup still owing an answer left before it saw
 			 * the request: once all are gone (and done[] is final),
@@ -467,7 +421,7 @@ static int resident_call(xcsum_ctx *c, const CsumArgs &a)
 				if (((pending >> w) & 1ull) && done_word(c, w, 0) == seq)
 					pending &= ~(1ull << w);
 			if (!pending)
-				return 0;
+				return resident_bad(c, seq);
 			HIPCHK(resident_launch(c, prev, seq, all & ~pending));
 			continue;
 		}
@@ -1201,8 +1155,7 @@ static int batch_host_resident(xcsum_ctx *c, uint8_t *h_umem, const struct xcsum
 	int rc = resident_ensure(c);
 	if (rc)
 		return rc;
-	/* the descriptors go into the doorbell (device memory: the kernel reads
-	 * them without a PCIe round trip) */
+	/* the descriptors go into the doorbell */
 	struct xcsum_desc *ds = c->res_bell->desc;
 	CsumArgs a;
 	a.desc = c->res_vbell->desc;
@@ -1214,39 +1167,33 @@ static int batch_host_resident(xcsum_ctx *c, uint8_t *h_umem, const struct xcsum
 	a.bias = 0;
 	a.ord = order_identity(n);
 	a.dense = a.ord;
-	/* the frames' bytes gathered, each at its 16-byte phase (stage_off) */
-	uint64_t gbytes = 0;
-	for (uint32_t k = 0; k < n; k++)
-		gbytes = stage_off(gbytes, h_desc[k].addr) + h_desc[k].len;
-	bool kernel_inplace = false;   /* the kernel writes the host frames itself */
-	auto gather_into = [&](uint8_t *stage) {
+	/* The resident kernel reads only the library's own pinned stage, never
+	 * the caller's registered UMEM in place: reading it in place faulted 4 of
+	 * 12 GPU suite runs, always in a test whose resident workgroups read a
+	 * registered UMEM; reading the stage never did.  A
+	 * registered UMEM's frames are gathered like a sparse pageable one's. */
+	if (zc)
+		gather = true;
+	const bool kernel_inplace = false;   /* in-place fields: written on the host */
+	uint64_t limit = 0;            /* bytes readable from a.umem (+ bias) */
+	if (gather) {
+		/* each frame copied on its own into the pinned stage, at its
+		 * 16-byte phase (stage_off) */
 		uint64_t pos = 0;
+		for (uint32_t k = 0; k < n; k++)
+			pos = stage_off(pos, h_desc[k].addr) + h_desc[k].len;
+		if (pos > DIRECT_MAX)
+			return RES_DECLINE;
+		pos = 0;
 		for (uint32_t k = 0; k < n; k++) {
 			const struct xcsum_desc &d = h_desc[k];
 			const uint64_t off = stage_off(pos, d.addr);
-			memcpy(stage + off, h_umem + d.addr, d.len);
+			memcpy(c->h_stage[0] + off, h_umem + d.addr, d.len);
 			ds[k] = xcsum_desc{off, d.len, 0};
 			pos = off + d.len;
 		}
-	};
-	if (c->res_push && gbytes <= c->res_push_max) {
-		/* small batch: the CPU pushes the frame bytes into device memory
-		 * through the BAR (one write burst), so the kernel reads HBM
-		 * instead of waiting a PCIe round trip for them; in-place fields
-		 * are written on the host (retire) */
-		gather_into(c->res_push);
-		a.umem = c->res_push;
-		a.flags = flags & (XCSUM_F_IPHDR | XCSUM_F_V4_RFC | XCSUM_F_VERIFY);
-	} else if (zc) {
-		memcpy(ds, h_desc, (size_t)n * sizeof(*ds));
-		a.umem = zc->dev + (h_umem - zc->host);
-		a.flags = flags & (XCSUM_F_INPLACE | XCSUM_F_IPHDR | XCSUM_F_V4_RFC | XCSUM_F_VERIFY);
-		kernel_inplace = true;
-	} else if (gather) {
-		if (gbytes > DIRECT_MAX)
-			return RES_DECLINE;
-		gather_into(c->h_stage[0]);
 		a.umem = c->v_stage[0];
+		limit = pos;
 		a.flags = flags & (XCSUM_F_IPHDR | XCSUM_F_V4_RFC | XCSUM_F_VERIFY);
 	} else {
 		/* 16-byte aligned copy of [lo, hi): every frame keeps its address
@@ -1258,9 +1205,10 @@ static int batch_host_resident(xcsum_ctx *c, uint8_t *h_umem, const struct xcsum
 		memcpy(ds, h_desc, (size_t)n * sizeof(*ds));
 		a.umem = c->v_stage[0];
 		a.bias = alo;
+		limit = hi - alo;
 		a.flags = flags & (XCSUM_F_IPHDR | XCSUM_F_V4_RFC | XCSUM_F_VERIFY);
 	}
-	rc = resident_call(c, a);
+	rc = resident_call(c, a, limit);
 	if (rc)
 		return rc;
 	Pending pd;

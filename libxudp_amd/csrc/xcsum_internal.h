@@ -221,14 +221,10 @@ struct Ctx {
 	int res_wg;
 	uint32_t res_idle_us;
 	uint32_t res_max_frames;       /* larger batches take the launched path */
-	ResidentBell *res_bell;        /* the doorbell as the host writes it (lazy) */
-	ResidentBell *res_vbell;       /* ... and as the kernel reads it */
-	bool res_bell_dev;             /* in device memory (else pinned host) */
-	bool res_bell_forced_host;     /* XCSUM_RESIDENT_BELL=host */
+	ResidentBell *res_bell;        /* the doorbell, pinned host memory (lazy) */
+	ResidentBell *res_vbell;       /* its device alias */
 	ResidentDone *res_done;        /* pinned, coherent */
 	ResidentDone *res_vdone;       /* its device alias */
-	uint8_t *res_push;             /* device-memory stage for pushed batches */
-	uint32_t res_push_max;         /* largest pushed batch (bytes) */
 	hipStream_t res_stream;
 	bool res_live;                 /* launched, not yet seen gone */
 	uint32_t res_seq;              /* last sequence number issued (0: none) */

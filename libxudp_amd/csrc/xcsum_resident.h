@@ -12,7 +12,6 @@ namespace xcsum {
 constexpr int RB_MAX_WG = 64;          /* workgroups (one bit each in a skip mask) */
 constexpr int RB_DONE_STRIDE = 16;     /* one 64-byte line per workgroup's done word */
 constexpr uint32_t RB_DESC_CAP = 4096; /* descriptors the doorbell holds */
-constexpr uint32_t RB_PUSH_CAP = 128u << 10;   /* push stage bytes (xcsum_api.hip) */
 
 /* request words: device addresses as (lo, hi) pairs */
 enum {
@@ -21,15 +20,14 @@ enum {
 	RB_SEQ = 13,                   /* the request's own sequence number: a
 					  request whose echo differs from seq is
 					  not (yet) the one announced */
-	RB_REQ_WORDS = 14
+	RB_LIMIT = 14,                 /* (lo, hi): bytes readable from umem + 0
+					  (desc.addr - bias + len must not pass it) */
+	RB_REQ_WORDS = 16
 };
 
-/* The doorbell: fine-grained DEVICE memory the host writes through the PCIe
- * BAR, so the workgroups poll their own HBM (tools/latency_probe: 1.5-2 us
- * less per request than polling host memory over PCIe); pinned host memory
- * where the device memory is not host-writable.  The host writes desc[] and
- * req[], then seq; `stop` asks the workgroups to leave.  Sequence numbers
- * skip 0. */
+/* The doorbell, in pinned coherent host memory the workgroups read over
+ * PCIe.  The host writes desc[] and req[], then seq; `stop` asks the
+ * workgroups to leave.  Sequence numbers skip 0. */
 struct alignas(64) ResidentBell {
 	uint32_t seq;                  /* words 0-31 are read by one load per poll */
 	uint32_t stop;
@@ -44,6 +42,10 @@ struct alignas(64) ResidentBell {
  * generation) as it leaves -- so the host learns that the workgroups are gone
  * without asking the HIP runtime on every call. */
 constexpr int RB_LEFT = 1;
+/* a workgroup that finds a descriptor of its frames outside the request's
+ * limit serves none of them and reports it: [2] = seq, [3] = frame index,
+ * [4..5] = desc.addr, [6] = desc.len (a bad request never faults the GPU) */
+constexpr int RB_BAD = 2;
 struct alignas(64) ResidentDone {
 	uint32_t done[RB_MAX_WG * RB_DONE_STRIDE];
 };

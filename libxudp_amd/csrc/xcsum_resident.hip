@@ -5,10 +5,10 @@
  * batch is one trip through xudp_frame_send (tx.c:673-734).  As a kernel
  * launch per batch, a call costs a launch and a completion (~17-20 us,
  * DESIGN.md 5.8) for microseconds of work.  A resident server removes both:
- * W workgroups stay on the device and poll a doorbell (xcsum_resident.h:
- * device memory the host writes through the BAR); a batch is the request and
- * its descriptors written there, a sequence number stored after them, and a
- * host spin on one "done" word per workgroup in pinned host memory.
+ * W workgroups stay on the device and poll a doorbell in pinned host memory
+ * (xcsum_resident.h); a batch is the request and its descriptors written
+ * there, a sequence number stored after them, and a host spin on one "done"
+ * word per workgroup.
  *
  * The work is the frame-group checksum loop itself (csum_loop<16, 2, 6, 2>
  * of xcsum_csum.h: every mode and flag, bit-exact with the launched kernels),
@@ -62,6 +62,7 @@ __global__ void __launch_bounds__(256) resident_kernel(const ResidentBell *bell,
 						       uint64_t skip_mask, uint64_t idle_ticks)
 {
 	__shared__ uint32_t cmd[RB_REQ_WORDS + 1];
+	__shared__ uint32_t first_bad_lds;   /* descriptor check (below) */
 	const uint32_t lane = threadIdx.x & 63;
 	uint32_t served = served0;
 	if (blockIdx.x < 64 && ((skip_mask >> blockIdx.x) & 1ull))
@@ -132,7 +133,39 @@ __global__ void __launch_bounds__(256) resident_kernel(const ResidentBell *bell,
 		a.err = err;
 		a.ord = order_identity(a.n);
 		a.dense = a.ord;
-		csum_loop<G, U, K, false, 2>(a);
+		/* every descriptor of this workgroup's frames inside the request's
+		 * limit, or the workgroup serves none and reports the first bad
+		 * one (csum_loop: segment s = 16 b + j of workgroup b takes frames
+		 * s, s + nseg, ...) */
+		const uint64_t limit = u64_of(r[RB_LIMIT], r[RB_LIMIT + 1]);
+		const uint32_t nseg = gridDim.x * (256u / G);
+		uint32_t bad = ~0u;
+		for (uint32_t p = (256u / G) * blockIdx.x + (threadIdx.x % (256u / G)) +
+				  (threadIdx.x / (256u / G)) * nseg;
+		     p < a.n; p += (256u / G) * nseg) {
+			const u32x4 d = *((gu32x4 *)(a.desc + p));
+			const uint64_t ad = ((uint64_t)d.y << 32) | d.x;
+			if (ad < a.bias || ad - a.bias > limit || d.z > limit - (ad - a.bias))
+				bad = p < bad ? p : bad;
+		}
+		if (threadIdx.x == 0)
+			first_bad_lds = ~0u;
+		__syncthreads();
+		if (bad != ~0u)
+			atomicMin(&first_bad_lds, bad);
+		__syncthreads();
+		const uint32_t first_bad = __builtin_amdgcn_readfirstlane(first_bad_lds);
+		if (first_bad == ~0u) {
+			csum_loop<G, U, K, false, 2>(a);
+		} else if (threadIdx.x == 0) {
+			const u32x4 d = *((gu32x4 *)(a.desc + first_bad));
+			uint32_t *o = &done->done[RB_DONE_STRIDE * blockIdx.x + RB_BAD];
+			o[1] = first_bad;
+			o[2] = d.x;
+			o[3] = d.y;
+			o[4] = d.z;
+			__hip_atomic_store(&o[0], s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+		}
 		/* this wave's results and in-place stores reach host memory ... */
 		__builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
 		/* ... for every wave, before done[w] says so */

@@ -19,13 +19,8 @@ from test_gpu_host_path import check_inplace, host_batch
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(params=["push", "nopush"])
-def res_engine(request, monkeypatch):
-    """A context with 8 resident workgroups; batches up to 64 KiB of frame
-    bytes are pushed into device memory by the CPU ("push", the default) or,
-    with XCSUM_RESIDENT_PUSH=0, read by the kernel where they are."""
-    if request.param == "nopush":
-        monkeypatch.setenv("XCSUM_RESIDENT_PUSH", "0")
+@pytest.fixture
+def res_engine():
     e = X.Engine(0)
     e.set_resident(8)
     yield e
@@ -160,6 +155,39 @@ def test_resident_fresh_descriptors_every_call(res_engine):
         res_engine.unregister_umem(umem)
 
 
+def test_resident_fresh_staged_bytes_every_call(res_engine):
+    """Small frames in a pageable UMEM (gathered into the pinned stage): one
+    payload byte changes before every call, and every call must checksum the
+    new bytes."""
+    umem, desc = X.gen_frames_host(100, 6, 0, 300, seed=15, stride=2048, offset=64)
+    rng = np.random.default_rng(5)
+    a = desc["addr"].astype(np.int64)
+    for it in range(300):
+        k = int(rng.integers(0, 100))
+        pos = a[k] + 62 + int(rng.integers(0, max(1, int(desc["len"][k]) - 62)))
+        umem[pos] = rng.integers(0, 256)
+        got = host_batch(res_engine, umem, desc, X.MODE_V6)
+        assert np.array_equal(got, oracle.batch(umem, desc, X.MODE_V6)), it
+
+
+def test_resident_large_descriptor_batches(res_engine):
+    """4096-frame batches (the doorbell's capacity), a different selection
+    and order every call, read in place from a registered UMEM: all 64 KiB
+    of descriptors must be the ones just written."""
+    umem, desc = X.gen_frames_host(6000, 4, 0, 200, seed=16, stride=512, offset=0)
+    exp_all = oracle.batch(umem, desc, X.MODE_V4_RFC)
+    res_engine.register_umem(umem)
+    rng = np.random.default_rng(6)
+    try:
+        for it in range(60):
+            n = 4096 if it % 2 == 0 else int(rng.integers(1000, 4097))
+            sel = rng.choice(len(desc), n, replace=False)
+            got = host_batch(res_engine, umem, desc[sel], X.MODE_V4_RFC)
+            assert np.array_equal(got, exp_all[sel]), it
+    finally:
+        res_engine.unregister_umem(umem)
+
+
 @pytest.mark.parametrize("idle_us", [1, 3, 30, 1000])
 def test_resident_leave_and_return(idle_us):
     """Workgroups that leave after idle_us come back with the next batch; with
@@ -234,29 +262,6 @@ def test_resident_packet_mirror(res_engine):
             assert int(f[24:26].view("<u2")[0]) == oracle.ip_header_rfc(f)
             z[40:42] = 0
             assert int(f[40:42].view("<u2")[0]) == oracle.batch(z, desc, X.MODE_V4_RFC)[0]
-
-
-def test_resident_host_doorbell(golden, monkeypatch):
-    """The fallback doorbell in pinned host memory (used where the CPU does
-    not map the device memory; XCSUM_RESIDENT_BELL=host forces it): same
-    results, in place included."""
-    monkeypatch.setenv("XCSUM_RESIDENT_BELL", "host")
-    e = X.Engine(0)
-    e.set_resident(4)
-    umem = golden["umem"].copy()
-    desc = golden_desc(golden)
-    e.register_umem(umem)
-    try:
-        for lo in range(0, len(desc), 250):
-            d = desc[lo:lo + 250]
-            got = host_batch(e, umem, d, X.MODE_AUTO, X.F_INPLACE | X.F_IPHDR)
-            fam = golden["family"][lo:lo + 250]
-            assert np.array_equal(got, np.where(fam == 6, golden["exp_v6"][lo:lo + 250],
-                                                golden["exp_legacy"][lo:lo + 250]))
-    finally:
-        e.unregister_umem(umem)
-        e.close()
-    check_inplace(golden, umem, desc)
 
 
 @pytest.mark.parametrize("how", ["pageable", "registered"])
