@@ -259,18 +259,18 @@ int xcsum_unregister_umem(xcsum_ctx *ctx, void *base);
  * tx_batch_num = 100 frames, xudp/xudp.c:74; tx.c:673-734 is one batch).
  * `workgroups` (1-64; 16 is a good start) checksum workgroups stay on the
  * device and poll a doorbell in pinned host memory: a host batch of at most
- * 4096 frames whose frames lie in a registered UMEM (read in place) or fit
- * the pinned stage (256 KiB) then costs a doorbell store and a spin on the
- * answer instead of a kernel launch and its completion (TX loop, 100 MTU
- * frames per call: 12-18 us instead of 23-32 us).  Results are the same
- * bytes.  The workgroups leave after `idle_us` (0: 20000) without a batch and
- * come back with the next one.  0 workgroups: off (the default; env
- * XCSUM_RESIDENT="W[,idle_us[,max_frames]]" sets it at context creation).
- * While they are resident, a device-wide synchronisation by others
- * (hipDeviceSynchronize, torch.cuda.synchronize) waits until they leave, i.e.
- * up to idle_us after this context's last batch; the library's own
- * device-wide waits (xcsum_ctx_take_errors, xcsum_unregister_umem,
- * xcsum_ctx_destroy) stop them first. */
+ * 4096 frames and 256 KiB of frame bytes is gathered into the context's
+ * pinned stage and then costs a doorbell store and a spin on the answer
+ * instead of a kernel launch and its completion (TX loop, 100 MTU frames per
+ * call: 16-21 us instead of 23-31 us; 1 frame 12-14 us instead of 17-29 us).
+ * Results are the same bytes.  The workgroups leave after `idle_us` (0:
+ * 20000) without a batch and come back with the next one.  0 workgroups: off
+ * (the default; env XCSUM_RESIDENT="W[,idle_us[,max_frames]]" sets it at
+ * context creation).  While they are resident, a device-wide
+ * synchronisation by others (hipDeviceSynchronize, torch.cuda.synchronize)
+ * waits until they leave, i.e. up to idle_us after this context's last
+ * batch; the library's own device-wide waits (xcsum_ctx_take_errors,
+ * xcsum_unregister_umem, xcsum_ctx_destroy) stop them first. */
 int xcsum_ctx_set_resident(xcsum_ctx *ctx, int workgroups, uint32_t idle_us);
 
 /* Number of the context's host-path slots with copies or kernels still in
