@@ -1144,47 +1144,43 @@ static int batch_host_resident(xcsum_ctx *c, uint8_t *h_umem, const struct xcsum
 		return RES_DECLINE;
 	const auto t_call = c->res_trace ? std::chrono::steady_clock::now()
 					 : std::chrono::steady_clock::time_point();
-	uint64_t lo = UINT64_MAX, hi = 0;
+	/* The resident kernel reads only the library's own pinned stage, never
+	 * the caller's registered UMEM in place: reading it in place faulted 4 of
+	 * 12 GPU suite runs, always in a test whose resident workgroups read a
+	 * registered UMEM (DESIGN.md 5.10); reading the stage never did.  A
+	 * sparse registered UMEM's frames are gathered like a pageable one's. */
+	if (zc)
+		gather = true;
+	uint64_t lo = UINT64_MAX, hi = 0, staged = 0;
 	for (uint32_t i = 0; i < n; i++) {
 		if (h_desc[i].addr < lo) lo = h_desc[i].addr;
 		if (h_desc[i].addr + h_desc[i].len > hi) hi = h_desc[i].addr + h_desc[i].len;
+		staged = stage_off(staged, h_desc[i].addr) + h_desc[i].len;
 	}
-	if (!zc)
-		zc = find_region(c, h_umem + lo, h_umem + hi);   /* dense, registered */
-	const bool want_ip = (flags & XCSUM_F_IPHDR) != 0;
+	const uint64_t alo = lo & ~(uint64_t)15;
+	if ((gather ? staged : hi - alo) > DIRECT_MAX)
+		return RES_DECLINE;
 	int rc = resident_ensure(c);
 	if (rc)
 		return rc;
 	/* the descriptors go into the doorbell */
 	struct xcsum_desc *ds = c->res_bell->desc;
 	CsumArgs a;
+	a.umem = c->v_stage[0];
 	a.desc = c->res_vbell->desc;
 	a.n = n;
 	a.out = c->v_out[0];
-	a.out_ip = want_ip ? c->v_out[0] + n : nullptr;
+	a.out_ip = (flags & XCSUM_F_IPHDR) ? c->v_out[0] + n : nullptr;
 	a.mode = mode;
+	/* in-place fields are written on the host (retire) */
+	a.flags = flags & (XCSUM_F_IPHDR | XCSUM_F_V4_RFC | XCSUM_F_VERIFY);
 	a.err = c->d_err;
 	a.bias = 0;
 	a.ord = order_identity(n);
 	a.dense = a.ord;
-	/* The resident kernel reads only the library's own pinned stage, never
-	 * the caller's registered UMEM in place: reading it in place faulted 4 of
-	 * 12 GPU suite runs, always in a test whose resident workgroups read a
-	 * registered UMEM (DESIGN.md 5.10); reading the stage never did.  A
-	 * registered UMEM's frames are gathered like a sparse pageable one's. */
-	if (zc)
-		gather = true;
-	const bool kernel_inplace = false;   /* in-place fields: written on the host */
-	uint64_t limit = 0;            /* bytes readable from a.umem (+ bias) */
 	if (gather) {
-		/* each frame copied on its own into the pinned stage, at its
-		 * 16-byte phase (stage_off) */
+		/* each frame copied on its own, at its 16-byte phase (stage_off) */
 		uint64_t pos = 0;
-		for (uint32_t k = 0; k < n; k++)
-			pos = stage_off(pos, h_desc[k].addr) + h_desc[k].len;
-		if (pos > DIRECT_MAX)
-			return RES_DECLINE;
-		pos = 0;
 		for (uint32_t k = 0; k < n; k++) {
 			const struct xcsum_desc &d = h_desc[k];
 			const uint64_t off = stage_off(pos, d.addr);
@@ -1192,30 +1188,20 @@ static int batch_host_resident(xcsum_ctx *c, uint8_t *h_umem, const struct xcsum
 			ds[k] = xcsum_desc{off, d.len, 0};
 			pos = off + d.len;
 		}
-		a.umem = c->v_stage[0];
-		limit = pos;
-		a.flags = flags & (XCSUM_F_IPHDR | XCSUM_F_V4_RFC | XCSUM_F_VERIFY);
 	} else {
 		/* 16-byte aligned copy of [lo, hi): every frame keeps its address
 		 * parity and phase */
-		const uint64_t alo = lo & ~(uint64_t)15;
-		if (hi - alo > DIRECT_MAX)
-			return RES_DECLINE;
 		memcpy(c->h_stage[0], h_umem + alo, hi - alo);
 		memcpy(ds, h_desc, (size_t)n * sizeof(*ds));
-		a.umem = c->v_stage[0];
 		a.bias = alo;
-		limit = hi - alo;
-		a.flags = flags & (XCSUM_F_IPHDR | XCSUM_F_V4_RFC | XCSUM_F_VERIFY);
 	}
-	rc = resident_call(c, a, limit);
+	rc = resident_call(c, a, gather ? staged : hi - alo);
 	if (rc)
 		return rc;
 	Pending pd;
 	pd.first = 0;
 	pd.count = n;
-	retire(pd, c->h_out[0], h_umem, h_desc, h_out, h_out_ip, mode,
-	       kernel_inplace ? (flags & ~XCSUM_F_INPLACE) : flags);
+	retire(pd, c->h_out[0], h_umem, h_desc, h_out, h_out_ip, mode, flags);
 	if (c->res_trace) {
 		c->res_calls++;
 		c->res_call_us += std::chrono::duration<double, std::micro>(
