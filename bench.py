@@ -496,7 +496,7 @@ def digest_check(cfg, out, count, world, rank, dist, sdev):
         return None
     import torch
     mine = out[:count].view(torch.uint8) if count else out[:0].view(torch.uint8)
-    if cfg["shard"] and world > 1:
+    if cfg["shard"] and dist.is_initialized():
         cnt = torch.tensor([count], dtype=torch.int64, device=sdev)
         cnts = [torch.zeros_like(cnt) for _ in range(world)]
         dist.all_gather(cnts, cnt)
@@ -529,6 +529,9 @@ def main():
                          "chunk as in xudp's TX UMEM")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-graph", action="store_true", help="time eager launches")
+    ap.add_argument("--dist-init", action="store_true",
+                    help="form the process group and run every collective even at one rank "
+                         "(exercises the RCCL branch on a one-GPU box)")
     ap.add_argument("--dist-backend", default="nccl",
                     help="process group for the barrier / timing reductions (nccl = RCCL)")
     ap.add_argument("--same-device", action="store_true",
@@ -557,14 +560,15 @@ def main():
         print(f"note: WORLD_SIZE={world} but --gpus {args.gpus}", file=sys.stderr)
     dev = torch.device(f"cuda:{0 if args.same_device else local}")
     torch.cuda.set_device(dev)
-    if world > 1:
+    use_dist = world > 1 or args.dist_init
+    if use_dist:
         if args.dist_backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
         else:
             dist.init_process_group(args.dist_backend)
 
     def barrier():
-        if world > 1:
+        if use_dist:
             dist.barrier()
 
     cfg = dict(CONFIGS[args.config], id=args.config, layout=args.layout)
@@ -683,7 +687,7 @@ def main():
     # per rank: its kernel's median launch time, algorithmic bytes and frames
     mine = torch.tensor([kern_ms, float(alg), float(count)], dtype=torch.float64, device=sdev)
     per_rank = [mine]
-    if world > 1:
+    if use_dist:
         dist.all_reduce(wt, op=dist.ReduceOp.MAX)
         dist.all_reduce(tot, op=dist.ReduceOp.SUM)
         per_rank = [torch.zeros_like(mine) for _ in range(world)]
@@ -833,7 +837,7 @@ def main():
         print(json.dumps(line), flush=True)
 
     eng.close()
-    if world > 1:
+    if use_dist:
         dist.destroy_process_group()
     if rank == 0 and not parity_ok:
         print("bench: the output differs from the reference; value withheld", file=sys.stderr)

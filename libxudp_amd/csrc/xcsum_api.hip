@@ -125,6 +125,11 @@ static void env_resident(xcsum_ctx *c)
 	c->res_seq = 0;
 	c->res_gen = 0;
 	c->res_trace = getenv("XCSUM_RESIDENT_TRACE") != nullptr;
+	/* test hook: requests carry a limit this many bytes short, so the
+	 * workgroups' own descriptor check refuses the frames past it
+	 * (tests/test_gpu_resident.py::test_resident_descriptor_check) */
+	const char *cut = getenv("XCSUM_RESIDENT_LIMIT_CUT");
+	c->res_limit_cut = cut ? strtoull(cut, nullptr, 10) : 0;
 	c->res_calls = 0;
 	c->res_spin_us = c->res_call_us = 0;
 	const char *e = getenv("XCSUM_RESIDENT");
@@ -1195,7 +1200,10 @@ static int batch_host_resident(xcsum_ctx *c, uint8_t *h_umem, const struct xcsum
 		memcpy(ds, h_desc, (size_t)n * sizeof(*ds));
 		a.bias = alo;
 	}
-	rc = resident_call(c, a, gather ? staged : hi - alo);
+	{
+		const uint64_t lim = gather ? staged : hi - alo;
+		rc = resident_call(c, a, lim - (c->res_limit_cut < lim ? c->res_limit_cut : lim));
+	}
 	if (rc)
 		return rc;
 	Pending pd;

@@ -56,6 +56,14 @@ static __device__ __forceinline__ bool dense_batch(const CsumArgs &a)
 	return !(al > a0 && al + dl.z - a0 > 2ull * a.n * mean);
 }
 
+/* descriptor hooks of the plain argument type (never called: kChecked is
+ * false); a checked type brings its own overloads */
+static __device__ __forceinline__ bool desc_ok(const CsumArgs &, u32x4)
+{
+	return true;
+}
+static __device__ __forceinline__ void desc_bad(const CsumArgs &, uint32_t) {}
+
 template <bool UNIFORM>
 static __device__ __forceinline__ u32x4 load_desc(const CsumArgs &a, uint32_t p)
 {
@@ -65,10 +73,17 @@ static __device__ __forceinline__ u32x4 load_desc(const CsumArgs &a, uint32_t p)
 	return *((gu32x4 *)(a.desc + q));
 }
 
-template <bool DW, int FEAT>
-static __device__ __forceinline__ Frame resolve(const CsumArgs &a, u32x4 d, bool present)
+template <bool DW, int FEAT, class A = CsumArgs>
+static __device__ __forceinline__ Frame resolve(const A &a, u32x4 d, bool present)
 {
 	Frame f;
+	/* a checked argument type: a descriptor outside its bounds is an absent
+	 * frame (no load of it) marked -4, reported by consume() */
+	bool bad = false;
+	if constexpr (A::kChecked) {
+		bad = present && !desc_ok(a, d);
+		present = present && !bad;
+	}
 	/* d.w (xdp_desc.options) is unused; keeping it "used" here stops the
 	 * register allocator from recycling that VGPR as a temporary right after
 	 * the prefetch is issued, which would force a full vmcnt(0) drain of the
@@ -100,7 +115,7 @@ static __device__ __forceinline__ Frame resolve(const CsumArgs &a, u32x4 d, bool
 	set_span<DW>(f, lo, lo + (len + pre - hdr));
 	if (mode < 0 || !present)
 		f.nchunks = 0;
-	f.mode = present ? mode : -2;
+	f.mode = present ? mode : bad ? -4 : -2;
 	/* VERIFY needs the check field: load it with this frame's chunks, one
 	 * pipeline step before finalize() reads it (loaded there, it was a
 	 * dependent round trip on every frame).  Unconditional and unused
@@ -296,8 +311,8 @@ static __device__ __forceinline__ uint32_t fidx(const CsumArgs &a, uint32_t p)
 	return ORD ? frame_of(a.ord, p) : p;
 }
 
-template <int G, int U, int K, bool TAIL, bool ORD, int FEAT>
-static __device__ __forceinline__ void consume(const CsumArgs &a, const Frame (&fc)[U],
+template <int G, int U, int K, bool TAIL, bool ORD, int FEAT, class A>
+static __device__ __forceinline__ void consume(const A &a, const Frame (&fc)[U],
 					       const u32x4 (&vc)[U][K], uint32_t lane,
 					       uint32_t p0, uint32_t nseg)
 {
@@ -311,15 +326,23 @@ static __device__ __forceinline__ void consume(const CsumArgs &a, const Frame (&
 			sum_walk<G, Grid<G, K>::DW>(f, lane, E, O);   /* jumbo frame */
 		uint32_t s = f.odd ? (O << 8) + E : (E << 8) + O;
 		s = seg_sum<G>(s);
-		if (lane == 0 && f.mode != -2)
-			finalize<FEAT>(a, f, fidx<ORD>(a, p0 + u * nseg), s);
+		if (lane == 0 && f.mode != -2) {
+			if constexpr (A::kChecked) {
+				if (f.mode == -4)
+					desc_bad(a, fidx<ORD>(a, p0 + u * nseg));
+				else
+					finalize<FEAT>(a, f, fidx<ORD>(a, p0 + u * nseg), s);
+			} else {
+				finalize<FEAT>(a, f, fidx<ORD>(a, p0 + u * nseg), s);
+			}
+		}
 	}
 }
 
 /* wave-uniform split: the jumbo path lives in its own copy of the body, so
  * its drains never merge into the common path's vmcnt bookkeeping */
-template <int G, int U, int K, bool ORD, int FEAT>
-static __device__ __forceinline__ void consume_any(const CsumArgs &a, const Frame (&fc)[U],
+template <int G, int U, int K, bool ORD, int FEAT, class A>
+static __device__ __forceinline__ void consume_any(const A &a, const Frame (&fc)[U],
 						   const u32x4 (&vc)[U][K], uint32_t lane,
 						   uint32_t p0, uint32_t nseg)
 {
@@ -328,9 +351,9 @@ static __device__ __forceinline__ void consume_any(const CsumArgs &a, const Fram
 	for (int u = 0; u < U; u++)
 		big |= fc[u].nchunks > K * G;
 	if (__builtin_amdgcn_ballot_w64(big))
-		consume<G, U, K, true, ORD, FEAT>(a, fc, vc, lane, p0, nseg);
+		consume<G, U, K, true, ORD, FEAT, A>(a, fc, vc, lane, p0, nseg);
 	else
-		consume<G, U, K, false, ORD, FEAT>(a, fc, vc, lane, p0, nseg);
+		consume<G, U, K, false, ORD, FEAT, A>(a, fc, vc, lane, p0, nseg);
 }
 
 /*
@@ -344,8 +367,8 @@ static __device__ __forceinline__ void consume_any(const CsumArgs &a, const Fram
  * at the loop latch, that copy needs the next step's loads to have landed,
  * and the ISA showed a vmcnt(0) there -- one step in flight, not two.
  */
-template <int G, int U, int K, bool ORD, int FEAT>
-static __device__ __forceinline__ void csum_loop(const CsumArgs &a)
+template <int G, int U, int K, bool ORD, int FEAT, class A>
+static __device__ __forceinline__ void csum_loop(const A &a)
 {
 	const uint32_t lane = threadIdx.x & (G - 1);
 	uint32_t seg = (blockIdx.x * 256u + threadIdx.x) / G;
@@ -366,7 +389,7 @@ static __device__ __forceinline__ void csum_loop(const CsumArgs &a)
 		d[u] = load_desc<G == 64>(a, fidx<ORD>(a, seg + u * nseg));
 #pragma unroll
 	for (int u = 0; u < U; u++)
-		fa[u] = resolve<Grid<G, K>::DW, FEAT>(a, d[u], has(seg + u * nseg));
+		fa[u] = resolve<Grid<G, K>::DW, FEAT, A>(a, d[u], has(seg + u * nseg));
 #pragma unroll
 	for (int u = 0; u < U; u++)
 		d[u] = load_desc<G == 64>(a, fidx<ORD>(a, seg + step + u * nseg));
@@ -381,24 +404,24 @@ static __device__ __forceinline__ void csum_loop(const CsumArgs &a)
 	for (uint32_t p0 = seg; p0 < limit; p0 += 2 * step) {
 #pragma unroll
 		for (int u = 0; u < U; u++)
-			fb[u] = resolve<Grid<G, K>::DW, FEAT>(a, d[u], has(p0 + step + u * nseg));
+			fb[u] = resolve<Grid<G, K>::DW, FEAT, A>(a, d[u], has(p0 + step + u * nseg));
 #pragma unroll
 		for (int u = 0; u < U; u++)
 			d[u] = load_desc<G == 64>(a, fidx<ORD>(a, p0 + 2 * step + u * nseg));
 		__builtin_amdgcn_sched_barrier(0);
 		issue<G, U, K>(fb, lane, vb);
-		consume_any<G, U, K, ORD, FEAT>(a, fa, va, lane, p0, nseg);
+		consume_any<G, U, K, ORD, FEAT, A>(a, fa, va, lane, p0, nseg);
 
 #pragma unroll
 		for (int u = 0; u < U; u++)
-			fa[u] = resolve<Grid<G, K>::DW, FEAT>(a, d[u],
+			fa[u] = resolve<Grid<G, K>::DW, FEAT, A>(a, d[u],
 							has(p0 + 2 * step + u * nseg));
 #pragma unroll
 		for (int u = 0; u < U; u++)
 			d[u] = load_desc<G == 64>(a, fidx<ORD>(a, p0 + 3 * step + u * nseg));
 		__builtin_amdgcn_sched_barrier(0);
 		issue<G, U, K>(fa, lane, va);
-		consume_any<G, U, K, ORD, FEAT>(a, fb, vb, lane, p0 + step, nseg);
+		consume_any<G, U, K, ORD, FEAT, A>(a, fb, vb, lane, p0 + step, nseg);
 	}
 }
 

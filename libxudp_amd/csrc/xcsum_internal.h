@@ -108,6 +108,10 @@ struct CsumArgs {
 	Order ord;
 	Order dense;                   /* ord.sparse_only: the order a dense batch
 					  gets instead (resolve_order) */
+	/* the launched kernels trust their descriptors (the host bounded the
+	 * batch); an argument type with kChecked (xcsum_resident.hip) checks
+	 * each one before any load of its frame (desc_ok / desc_bad) */
+	static constexpr bool kChecked = false;
 };
 
 /* Frame-build kernel arguments (xcsum_build.hip). */
@@ -231,6 +235,7 @@ struct Ctx {
 	uint32_t res_gen;              /* generation of the last launch (skips 0) */
 	/* XCSUM_RESIDENT_TRACE=1: per-call timing, printed by xcsum_ctx_destroy */
 	bool res_trace;
+	uint64_t res_limit_cut;        /* test hook: XCSUM_RESIDENT_LIMIT_CUT */
 	uint64_t res_calls;
 	double res_spin_us, res_call_us;
 };

@@ -12,8 +12,8 @@
  *
  * The work is the frame-group checksum loop itself (csum_loop<16, 2, 6, 2>
  * of xcsum_csum.h: every mode and flag, bit-exact with the launched kernels),
- * over frames the kernel reads in place through a device alias: a registered
- * UMEM, or the context's pinned stage.
+ * over frames the host gathered into the context's pinned stage, each
+ * descriptor checked against the request's bounds inside the loop.
  *
  * Memory ordering (all vector memory operations):
  *   - wave 0 of a workgroup polls `seq` (and `stop`, the same 8 bytes) with
@@ -52,6 +52,28 @@ static __device__ __forceinline__ uint64_t u64_of(uint32_t lo, uint32_t hi)
 	return ((uint64_t)hi << 32) | lo;
 }
 
+/* The resident loop's arguments: a request's frames must lie inside
+ * [bias, bias + limit) of its buffer; csum_loop checks every descriptor before
+ * any load of its frame (resolve) and hands a bad one to desc_bad, which keeps
+ * the workgroup's lowest bad index in LDS.  The check rides on the loop's own
+ * descriptor loads, so it costs no round trip of its own. */
+struct ResidentArgs : CsumArgs {
+	static constexpr bool kChecked = true;
+	uint64_t limit;
+	uint32_t *first_bad;   /* LDS */
+};
+
+static __device__ __forceinline__ bool desc_ok(const ResidentArgs &a, u32x4 d)
+{
+	const uint64_t ad = ((uint64_t)d.y << 32) | d.x;
+	return !(ad < a.bias || ad - a.bias > a.limit || d.z > a.limit - (ad - a.bias));
+}
+
+static __device__ __forceinline__ void desc_bad(const ResidentArgs &a, uint32_t p)
+{
+	atomicMin(a.first_bad, p);
+}
+
 /* served0: the sequence number every workgroup has served at launch, except
  * the workgroups of skip_mask (bit w), which served skip_seq already
  * (relaunch after a partial service, see the file comment) */
@@ -62,7 +84,7 @@ __global__ void __launch_bounds__(256) resident_kernel(const ResidentBell *bell,
 						       uint64_t skip_mask, uint64_t idle_ticks)
 {
 	__shared__ uint32_t cmd[RB_REQ_WORDS + 1];
-	__shared__ uint32_t first_bad_lds;   /* descriptor check (below) */
+	__shared__ uint32_t first_bad_lds;   /* ResidentArgs::first_bad */
 	const uint32_t lane = threadIdx.x & 63;
 	uint32_t served = served0;
 	if (blockIdx.x < 64 && ((skip_mask >> blockIdx.x) & 1ull))
@@ -98,8 +120,10 @@ __global__ void __launch_bounds__(256) resident_kernel(const ResidentBell *bell,
 				__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
 			if (lane >= 16 && lane < 16 + RB_REQ_WORDS)
 				cmd[1 + lane - 16] = v;
-			if (lane == 0)
+			if (lane == 0) {
 				cmd[0] = go ? s : 0u;
+				first_bad_lds = ~0u;
+			}
 		}
 		__syncthreads();
 		const uint32_t s = __builtin_amdgcn_readfirstlane(cmd[0]);
@@ -121,7 +145,7 @@ __global__ void __launch_bounds__(256) resident_kernel(const ResidentBell *bell,
 #pragma unroll
 		for (int k = 0; k < RB_REQ_WORDS; k++)
 			r[k] = __builtin_amdgcn_readfirstlane(cmd[1 + k]);
-		CsumArgs a;
+		ResidentArgs a;
 		a.umem = (uint8_t *)(uintptr_t)u64_of(r[RB_UMEM], r[RB_UMEM + 1]);
 		a.desc = (const struct xcsum_desc *)(uintptr_t)u64_of(r[RB_DESC], r[RB_DESC + 1]);
 		a.out = (uint16_t *)(uintptr_t)u64_of(r[RB_OUT], r[RB_OUT + 1]);
@@ -133,31 +157,14 @@ __global__ void __launch_bounds__(256) resident_kernel(const ResidentBell *bell,
 		a.err = err;
 		a.ord = order_identity(a.n);
 		a.dense = a.ord;
-		/* every descriptor of this workgroup's frames inside the request's
-		 * limit, or the workgroup serves none and reports the first bad
-		 * one (csum_loop: segment s = 16 b + j of workgroup b takes frames
-		 * s, s + nseg, ...) */
-		const uint64_t limit = u64_of(r[RB_LIMIT], r[RB_LIMIT + 1]);
-		const uint32_t nseg = gridDim.x * (256u / G);
-		uint32_t bad = ~0u;
-		for (uint32_t p = (256u / G) * blockIdx.x + (threadIdx.x % (256u / G)) +
-				  (threadIdx.x / (256u / G)) * nseg;
-		     p < a.n; p += (256u / G) * nseg) {
-			const u32x4 d = *((gu32x4 *)(a.desc + p));
-			const uint64_t ad = ((uint64_t)d.y << 32) | d.x;
-			if (ad < a.bias || ad - a.bias > limit || d.z > limit - (ad - a.bias))
-				bad = p < bad ? p : bad;
-		}
-		if (threadIdx.x == 0)
-			first_bad_lds = ~0u;
-		__syncthreads();
-		if (bad != ~0u)
-			atomicMin(&first_bad_lds, bad);
+		a.limit = u64_of(r[RB_LIMIT], r[RB_LIMIT + 1]);
+		a.first_bad = &first_bad_lds;
+		csum_loop<G, U, K, false, 2>(a);
+		/* a descriptor outside the request's bounds: its frame was not
+		 * read; report the workgroup's first (the host fails the call) */
 		__syncthreads();
 		const uint32_t first_bad = __builtin_amdgcn_readfirstlane(first_bad_lds);
-		if (first_bad == ~0u) {
-			csum_loop<G, U, K, false, 2>(a);
-		} else if (threadIdx.x == 0) {
+		if (first_bad != ~0u && threadIdx.x == 0) {
 			const u32x4 d = *((gu32x4 *)(a.desc + first_bad));
 			uint32_t *o = &done->done[RB_DONE_STRIDE * blockIdx.x + RB_BAD];
 			o[1] = first_bad;

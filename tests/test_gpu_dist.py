@@ -1,7 +1,7 @@
 """GPU: bench.py's N > 1 path on the HIP engine.  Two ranks (gloo, both on
 cuda:0 -- the box has one GPU; on an 8-GPU node the driver runs the same code
 with RCCL, one rank per GPU) launched by torch.distributed.run as a fresh
-child process.  Config 5 is one 8M-frame job sharded by bytes: the ranks'
+child process (and one rank over RCCL, `test_rccl_branch_one_rank`).  Config 5 is one 8M-frame job sharded by bytes: the ranks'
 outputs, gathered and concatenated, must equal the reference's digest of the
 whole job; config 2 is weak scaling: rank 0's batch is the digested one."""
 import json
@@ -22,11 +22,11 @@ def free_port():
         return s.getsockname()[1]
 
 
-def run_dist(config, steps=2, extra=()):
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
-           "--master-addr", "127.0.0.1", "--master-port", str(free_port()),
-           os.path.join(ROOT, "bench.py"), "--gpus", "2", "--same-device", "--dist-backend",
-           "gloo", "--config", str(config), "--steps", str(steps), "--warmup", "1",
+def run_dist(config, steps=2, extra=(), nproc=2, backend="gloo"):
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node",
+           str(nproc), "--master-addr", "127.0.0.1", "--master-port", str(free_port()),
+           os.path.join(ROOT, "bench.py"), "--gpus", str(nproc), "--same-device",
+           "--dist-backend", backend, "--config", str(config), "--steps", str(steps), "--warmup", "1",
            "--reps", "2", "--ramp-ms", "0", "--no-ceiling", "--no-cpu-baseline", *extra]
     env = dict(os.environ, MASTER_ADDR="127.0.0.1")
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, cwd=ROOT, env=env)
@@ -68,3 +68,18 @@ def check_per_rank(line, world):
 def test_two_ranks_config5_per_rank_fields():
     line = run_dist(5)
     check_per_rank(line, 2)
+
+
+@pytest.mark.parametrize("config", [2, 5])
+def test_rccl_branch_one_rank(config):
+    """The RCCL branch on the box's one GPU: a one-rank `nccl` process group
+    (--dist-init) runs the barrier, the MAX/SUM reductions, the per-rank
+    all_gather and, for config 5, the shard gather, all on device tensors,
+    as every rank of the driver's 8-GPU run does (two ranks cannot share one
+    GPU under RCCL)."""
+    line = run_dist(config, steps=2, extra=("--dist-init",), nproc=1, backend="nccl")
+    assert line["n_gpus"] == 1
+    assert line["parity_digest"]["ok"] is True, line["parity_digest"]
+    if config == 5:
+        assert "concatenated outputs of 1 ranks" in line["parity_digest"]["what"]
+    check_per_rank(line, 1)

@@ -1,7 +1,8 @@
 """GPU: host batches served by resident workgroups (xcsum_ctx_set_resident,
 csrc/xcsum_resident.hip) against the reference fixtures and the oracle.  The
 resident path must give the same bytes as the launched one in every mode,
-flag and transport (registered UMEM read in place, pageable frames staged),
+flag and transport (registered or pageable UMEM: the frames are gathered into
+the library's pinned stage),
 stay correct when the same UMEM changes between calls (no stale cache
 lines), and serve every frame exactly once when its workgroups leave and
 come back between calls (an in-place frame served twice would sum its own
@@ -84,8 +85,8 @@ def test_resident_verify(res_engine, golden):
 @pytest.mark.parametrize("fam", [4, 6])
 @pytest.mark.parametrize("register", [False, True])
 def test_resident_slots(res_engine, fam, register):
-    """xudp's TX layout (one frame per 4096-byte chunk): gathered from a
-    pageable UMEM, read in place from a registered one; in place + IP header."""
+    """xudp's TX layout (one frame per 4096-byte chunk), pageable and
+    registered UMEM (gathered either way); in place + IP header."""
     umem, desc = X.gen_frames_host(100, fam, 0, 1458, seed=77 + fam, stride=4096,
                                    offset=322 if fam == 6 else 342)
     mode = X.MODE_V6 if fam == 6 else X.MODE_V4_RFC
@@ -172,7 +173,7 @@ def test_resident_fresh_staged_bytes_every_call(res_engine):
 
 def test_resident_large_descriptor_batches(res_engine):
     """4096-frame batches (the doorbell's capacity), a different selection
-    and order every call, read in place from a registered UMEM: all 64 KiB
+    and order every call, from a registered UMEM: all 64 KiB
     of descriptors must be the ones just written."""
     umem, desc = X.gen_frames_host(6000, 4, 0, 200, seed=16, stride=512, offset=0)
     exp_all = oracle.batch(umem, desc, X.MODE_V4_RFC)
@@ -312,3 +313,35 @@ def test_resident_auto_mixed_families_verify_iphdr(res_engine, golden):
                                   X.F_VERIFY | X.F_IPHDR).any()
     finally:
         res_engine.unregister_umem(umem)
+
+
+def test_resident_descriptor_check(monkeypatch, capfd):
+    """The workgroups check every descriptor against the request's bounds
+    inside the checksum loop, before any load of its frame: with the limit cut
+    one byte short (test hook XCSUM_RESIDENT_LIMIT_CUT) the last staged frame
+    is refused, the call fails with XCSUM_ERR_INVAL and names it; the same
+    context then serves the frames that fit.  Under the bounds-checked build
+    the refused frame leaves no load outside its extent either."""
+    monkeypatch.setenv("XCSUM_RESIDENT_LIMIT_CUT", "1")
+    e = X.Engine(0)
+    try:
+        e.set_resident(8)
+        umem, desc = X.gen_frames_host(100, 4, 0, 1400, seed=13, align=8)
+        with pytest.raises(X.XcsumError) as ex:
+            host_batch(e, umem, desc, X.MODE_V4_RFC)
+        assert ex.value.rc == -X.ERR_INVAL
+        assert "descriptor 99 " in capfd.readouterr().err
+        exp = oracle.batch(umem, desc[:1], X.MODE_V4_RFC)
+        # one frame: its limit is its own length, one byte short again
+        with pytest.raises(X.XcsumError):
+            host_batch(e, umem, desc[:1], X.MODE_V4_RFC)
+        assert "descriptor 0 " in capfd.readouterr().err
+    finally:
+        e.close()
+    monkeypatch.delenv("XCSUM_RESIDENT_LIMIT_CUT")
+    e = X.Engine(0)
+    try:
+        e.set_resident(8)
+        assert np.array_equal(host_batch(e, umem, desc[:1], X.MODE_V4_RFC), exp)
+    finally:
+        e.close()
