@@ -372,6 +372,13 @@ static int resident_call(xcsum_ctx *c, const CsumArgs &a, uint64_t limit)
 	b->req[RB_MODE] = a.mode;
 	b->req[RB_FLAGS] = a.flags;
 	put64(RB_LIMIT, limit);
+	/* a small batch's descriptors also go into the lines the workgroups
+	 * poll (three a line, the line's echo after them) */
+	if (a.n <= RB_INLINE)
+		for (uint32_t l = 0; l * 3 < a.n; l++) {
+			memcpy(b->inl[l], &b->desc[3 * l], 3 * sizeof(struct xcsum_desc));
+			bell_store(&b->inl[l][RB_INL_ECHO], seq);
+		}
 	/* the echo last, after everything else of the request has left the
 	 * write-combining buffers: a workgroup that reads the echo equal to seq
 	 * has the whole request in the same 64-byte read */

@@ -64,10 +64,14 @@ static __device__ __forceinline__ bool desc_ok(const CsumArgs &, u32x4)
 }
 static __device__ __forceinline__ void desc_bad(const CsumArgs &, uint32_t) {}
 
-template <bool UNIFORM>
-static __device__ __forceinline__ u32x4 load_desc(const CsumArgs &a, uint32_t p)
+template <bool UNIFORM, class A>
+static __device__ __forceinline__ u32x4 load_desc(const A &a, uint32_t p)
 {
 	uint32_t q = p < a.n ? p : a.n - 1;
+	if constexpr (A::kChecked) {
+		if (a.inl)   /* descriptors that came with the request (LDS) */
+			return desc_inline(a, q);
+	}
 	if (UNIFORM)
 		return *((cu32x4 *)(a.desc + q));
 	return *((gu32x4 *)(a.desc + q));

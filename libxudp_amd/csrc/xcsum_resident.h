@@ -25,14 +25,23 @@ enum {
 	RB_REQ_WORDS = 16
 };
 
+/* A batch of at most RB_INLINE frames also carries its descriptors in the
+ * two 64-byte lines after the request, three per line, each line with the
+ * request's sequence number in word RB_INL_ECHO: the poll that reads the
+ * request reads them too, which saves the workgroups the round trip for the
+ * descriptors. */
+constexpr uint32_t RB_INLINE = 6;
+constexpr int RB_INL_ECHO = 12;
+
 /* The doorbell, in pinned coherent host memory the workgroups read over
- * PCIe.  The host writes desc[] and req[], then seq; `stop` asks the
- * workgroups to leave.  Sequence numbers skip 0. */
+ * PCIe.  The host writes desc[] (always), the inline lines and req[], then
+ * seq; `stop` asks the workgroups to leave.  Sequence numbers skip 0. */
 struct alignas(64) ResidentBell {
-	uint32_t seq;                  /* words 0-31 are read by one load per poll */
+	uint32_t seq;                  /* words 0-63 are read by one load per poll */
 	uint32_t stop;
 	uint32_t pad0[14];
 	uint32_t req[16];              /* word 16 on */
+	uint32_t inl[2][16];           /* word 32 on: descriptors 0-2, 3-5 */
 	struct xcsum_desc desc[RB_DESC_CAP];
 };
 
@@ -42,9 +51,10 @@ struct alignas(64) ResidentBell {
  * generation) as it leaves -- so the host learns that the workgroups are gone
  * without asking the HIP runtime on every call. */
 constexpr int RB_LEFT = 1;
-/* a workgroup that finds a descriptor of its frames outside the request's
- * limit serves none of them and reports it: [2] = seq, [3] = frame index,
- * [4..5] = desc.addr, [6] = desc.len (a bad request never faults the GPU) */
+/* a workgroup that finds descriptors of its frames outside the request's
+ * limit reads none of those frames and reports the first: [2] = seq,
+ * [3] = frame index, [4..5] = desc.addr, [6] = desc.len (a bad request never
+ * faults the GPU) */
 constexpr int RB_BAD = 2;
 struct alignas(64) ResidentDone {
 	uint32_t done[RB_MAX_WG * RB_DONE_STRIDE];

@@ -61,7 +61,14 @@ struct ResidentArgs : CsumArgs {
 	static constexpr bool kChecked = true;
 	uint64_t limit;
 	uint32_t *first_bad;   /* LDS */
+	const uint32_t *inl;   /* LDS: the request's inline descriptors, or null */
 };
+
+static __device__ __forceinline__ u32x4 desc_inline(const ResidentArgs &a, uint32_t q)
+{
+	const uint32_t *w = a.inl + 4u * q;
+	return u32x4{w[0], w[1], w[2], w[3]};
+}
 
 static __device__ __forceinline__ bool desc_ok(const ResidentArgs &a, u32x4 d)
 {
@@ -85,6 +92,8 @@ __global__ void __launch_bounds__(256) resident_kernel(const ResidentBell *bell,
 {
 	__shared__ uint32_t cmd[RB_REQ_WORDS + 1];
 	__shared__ uint32_t first_bad_lds;   /* ResidentArgs::first_bad */
+	__shared__ uint32_t inl_lds[4 * RB_INLINE];   /* ResidentArgs::inl */
+	__shared__ uint32_t inl_on;
 	const uint32_t lane = threadIdx.x & 63;
 	uint32_t served = served0;
 	if (blockIdx.x < 64 && ((skip_mask >> blockIdx.x) & 1ull))
@@ -92,21 +101,28 @@ __global__ void __launch_bounds__(256) resident_kernel(const ResidentBell *bell,
 	uint64_t last = wall_clock64();
 	for (;;) {
 		if (threadIdx.x < 64) {
-			/* one load of the doorbell's first 128 bytes per poll: lane i
-			 * reads word i -- seq (0), stop (1) and the request (16...),
-			 * whose own echo of its sequence number (written after the
-			 * other request words, xcsum_api.hip resident_call) says the
-			 * words read with it belong to that request.  Relaxed: no cache
+			/* one load of the doorbell's first 256 bytes per poll: lane i
+			 * reads word i -- seq (0), stop (1), the request (16...) and
+			 * the inline descriptors (32...), each 64-byte line with its
+			 * own echo of the sequence number (written after the line's
+			 * other words, xcsum_api.hip resident_call) saying the words
+			 * read with it belong to that request.  Relaxed: no cache
 			 * maintenance per poll (an acquire load per poll invalidated the
 			 * L2 every time: 12-55 us per request, tools/latency_probe). */
 			const uint32_t *words = (const uint32_t *)bell;
-			uint32_t s = served, go = 0, v = 0;
+			uint32_t s = served, go = 0, v = 0, inl = 0;
 			for (;;) {
-				v = lane < 32 ? ld_relaxed_sys(words + lane) : 0u;
+				v = ld_relaxed_sys(words + lane);
 				s = __builtin_amdgcn_readlane(v, 0);
 				if (__builtin_amdgcn_readlane(v, 1))
 					break;   /* stop */
 				if (s != served && __builtin_amdgcn_readlane(v, 16 + RB_SEQ) == s) {
+					/* inline descriptors only if their lines are this
+					 * request's; else the ones in desc[] (always written) */
+					const uint32_t n = __builtin_amdgcn_readlane(v, 16 + RB_N);
+					inl = n <= RB_INLINE &&
+					      __builtin_amdgcn_readlane(v, 32 + RB_INL_ECHO) == s &&
+					      (n <= 3 || __builtin_amdgcn_readlane(v, 48 + RB_INL_ECHO) == s);
 					go = 1;
 					break;
 				}
@@ -120,9 +136,12 @@ __global__ void __launch_bounds__(256) resident_kernel(const ResidentBell *bell,
 				__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
 			if (lane >= 16 && lane < 16 + RB_REQ_WORDS)
 				cmd[1 + lane - 16] = v;
+			if (lane >= 32 && (lane & 15) < RB_INL_ECHO)   /* 3 descriptors a line */
+				inl_lds[(lane >> 4 == 3 ? 12 : 0) + (lane & 15)] = v;
 			if (lane == 0) {
 				cmd[0] = go ? s : 0u;
 				first_bad_lds = ~0u;
+				inl_on = go && inl;
 			}
 		}
 		__syncthreads();
@@ -159,6 +178,7 @@ __global__ void __launch_bounds__(256) resident_kernel(const ResidentBell *bell,
 		a.dense = a.ord;
 		a.limit = u64_of(r[RB_LIMIT], r[RB_LIMIT + 1]);
 		a.first_bad = &first_bad_lds;
+		a.inl = __builtin_amdgcn_readfirstlane(inl_on) ? inl_lds : nullptr;
 		csum_loop<G, U, K, false, 2>(a);
 		/* a descriptor outside the request's bounds: its frame was not
 		 * read; report the workgroup's first (the host fails the call) */

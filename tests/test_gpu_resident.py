@@ -345,3 +345,21 @@ def test_resident_descriptor_check(monkeypatch, capfd):
         assert np.array_equal(host_batch(e, umem, desc[:1], X.MODE_V4_RFC), exp)
     finally:
         e.close()
+
+
+def test_resident_inline_descriptors(res_engine):
+    """Batches of 1-6 frames carry their descriptors in the polled doorbell
+    lines (RB_INLINE): a different selection, order and count every call,
+    alternating with larger batches that use the descriptor array, so a stale
+    inline line would show as a wrong result."""
+    umem, desc = X.gen_frames_host(500, 6, 0, 1400, seed=21, stride=2048, offset=64)
+    res_engine.register_umem(umem)
+    rng = np.random.default_rng(8)
+    try:
+        for it in range(400):
+            n = int(rng.integers(1, 7)) if it % 3 else int(rng.integers(7, 40))
+            d = desc[rng.choice(len(desc), n, replace=False)]
+            got = host_batch(res_engine, umem, d, X.MODE_V6)
+            assert np.array_equal(got, oracle.batch(umem, d, X.MODE_V6)), (it, n)
+    finally:
+        res_engine.unregister_umem(umem)
