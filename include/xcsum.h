@@ -261,8 +261,8 @@ int xcsum_unregister_umem(xcsum_ctx *ctx, void *base);
  * device and poll a doorbell in pinned host memory: a host batch of at most
  * 4096 frames and 256 KiB of frame bytes is gathered into the context's
  * pinned stage and then costs a doorbell store and a spin on the answer
- * instead of a kernel launch and its completion (TX loop: 1 frame ~11 us
- * instead of 17-24 us, 100 MTU frames 18-20 us instead of ~25 us).
+ * instead of a kernel launch and its completion (TX loop: 1 frame 9-11 us
+ * instead of 17-24 us, 100 MTU frames 18-21 us instead of ~25 us).
  * Results are the same bytes.  The workgroups leave after `idle_us` (0:
  * 20000) without a batch and come back with the next one.  0 workgroups: off
  * (the default; env XCSUM_RESIDENT="W[,idle_us[,max_frames]]" sets it at

@@ -130,6 +130,9 @@ static void env_resident(xcsum_ctx *c)
 	 * (tests/test_gpu_resident.py::test_resident_descriptor_check) */
 	const char *cut = getenv("XCSUM_RESIDENT_LIMIT_CUT");
 	c->res_limit_cut = cut ? strtoull(cut, nullptr, 10) : 0;
+	/* diagnostic: descriptors only in the array (A/B of the inline lines) */
+	const char *inl = getenv("XCSUM_RESIDENT_INLINE");
+	c->res_inline = !(inl && strcmp(inl, "0") == 0);
 	c->res_calls = 0;
 	c->res_spin_us = c->res_call_us = 0;
 	const char *e = getenv("XCSUM_RESIDENT");
@@ -374,7 +377,7 @@ static int resident_call(xcsum_ctx *c, const CsumArgs &a, uint64_t limit)
 	put64(RB_LIMIT, limit);
 	/* a small batch's descriptors also go into the lines the workgroups
 	 * poll (three a line, the line's echo after them) */
-	if (a.n <= RB_INLINE)
+	if (a.n <= RB_INLINE && c->res_inline)
 		for (uint32_t l = 0; l * 3 < a.n; l++) {
 			memcpy(b->inl[l], &b->desc[3 * l], 3 * sizeof(struct xcsum_desc));
 			bell_store(&b->inl[l][RB_INL_ECHO], seq);

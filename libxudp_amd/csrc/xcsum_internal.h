@@ -236,6 +236,7 @@ struct Ctx {
 	/* XCSUM_RESIDENT_TRACE=1: per-call timing, printed by xcsum_ctx_destroy */
 	bool res_trace;
 	uint64_t res_limit_cut;        /* test hook: XCSUM_RESIDENT_LIMIT_CUT */
+	bool res_inline;               /* XCSUM_RESIDENT_INLINE=0 turns it off */
 	uint64_t res_calls;
 	double res_spin_us, res_call_us;
 };
