@@ -468,6 +468,25 @@ def inplace_ceiling(torch, dev, bufs, desc, flags, family, sptr):
             torch.cuda.synchronize(dev)
             ts.append(e0.elapsed_time(e1) / per)
         by_unroll[unroll] = float(np.median(ts[1:]))
+    # the two-pass schedule's probe: the plain read, then the field stores in
+    # frame order (probe_stream_read_twopass), both launches between the events
+    two = getattr(L, "probe_stream_read_twopass", None)
+    if two is not None:
+        two.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64,
+                        ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p,
+                        ctypes.c_int, ctypes.c_void_p]
+        ts = []
+        for r in range(6):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(s)
+            for k in range(per):
+                if two(bufs[k % len(bufs)].data_ptr(), nbytes, fstride, int(a[0]), len(a), f1, f2,
+                       scratch.data_ptr(), blocks, sptr) != 0:
+                    return None
+            e1.record(s)
+            torch.cuda.synchronize(dev)
+            ts.append(e0.elapsed_time(e1) / per)
+        by_unroll["two_pass"] = float(np.median(ts[1:]))
     t = min(by_unroll.values())
     return {"ms": round(t, 4), "ms_by_unroll": {str(k): round(v, 4) for k, v in by_unroll.items()},
             "GBps_read": round(nbytes / (t * 1e-3) / 1e9, 1),
@@ -475,8 +494,59 @@ def inplace_ceiling(torch, dev, bufs, desc, flags, family, sptr):
                     f"{'s' if len(bufs) > 1 else ''} + a 2-byte store per frame at eth+{f1}"
                     f"{f' and eth+{f2}' if f2 != f1 else ''} from the thread that read it "
                     f"(tools/hbm_probe.hip probe_stream_read_inplace, 1 or 4 chunks in flight "
-                    f"per thread, the faster), {per} back-to-back launches between two events, "
-                    f"median of 5"}
+                    f"per thread), or the stream read followed by a launch storing the fields "
+                    f"in frame order (probe_stream_read_twopass); the fastest of the three, "
+                    f"{per} back-to-back launches between two events, median of 5"}
+
+
+# Visiting orders the same-run A/B times next to the automatic one
+# (xcsum_ctx_set_order "R,T": 2^R regions of 2^T-frame tiles; 0,0 = descriptor
+# order).  The automatic order of MTU frames is 3,4.
+ORDER_AB = [(0, 0), (3, 4), (4, 4), (2, 5)]
+
+
+def order_ab(torch, dev, eng, bufs, d_desc, count, out_arg, cfg, flags, len_hint, sptr,
+             real, ceiling_gbps, per=10, reps=6):
+    """Same-run A/B of dense visiting orders on the timed workload: for each
+    order in ORDER_AB and the automatic one, `per` back-to-back eager launches
+    between two events, median of `reps` - 1 (the first is a warm-up); the
+    per-launch time and its fraction of the same-run stream-read ceiling (real
+    bytes, as roofline.frac_vs_ceiling).  Leaves the automatic order set."""
+    s = torch.cuda.current_stream(dev)
+    best_ms = {}
+    # two rounds with the legs interleaved, the lower median of each leg:
+    # the first leg measured after the ceiling probe ran ~10 % slow once
+    for rnd in range(2):
+        for order in [None] + ORDER_AB:
+            if order is None:
+                eng.set_order(-1, 0)
+            else:
+                eng.set_order(*order)
+            ts = []
+            for r in range(reps):
+                e0 = torch.cuda.Event(enable_timing=True)
+                e1 = torch.cuda.Event(enable_timing=True)
+                e0.record(s)
+                for k in range(per):
+                    eng.batch_device(bufs[k % len(bufs)], d_desc, count, out_arg, cfg["mode"],
+                                     flags, len_hint, stream=sptr)
+                e1.record(s)
+                torch.cuda.synchronize(dev)
+                ts.append(e0.elapsed_time(e1) / per)
+            key = "auto" if order is None else f"{order[0]},{order[1]}"
+            best_ms[key] = min(best_ms.get(key, 1e9), float(np.median(ts[1:])))
+    res = {}
+    for key, ms in best_ms.items():
+        res[key] = {"ms": round(ms, 4)}
+        if ceiling_gbps:
+            res[key]["frac_vs_ceiling"] = round(real / (ms * 1e-3) / 1e9 / ceiling_gbps, 4)
+    eng.set_order(-1, 0)
+    best = min(res, key=lambda k: res[k]["ms"])
+    return {"orders": res, "fastest": best,
+            "auto_vs_fastest": round(res[best]["ms"] / res["auto"]["ms"], 4),
+            "what": f"{per} back-to-back eager launches per order between two events, median "
+                    f"of {reps - 1}, the lower of two interleaved rounds; R,T = 2^R regions of "
+                    f"2^T-frame tiles (0,0 = descriptor order), auto = the library's choice"}
 
 
 def digest_check(cfg, out, count, world, rank, dist, sdev):
@@ -543,6 +613,10 @@ def main():
                     help="untimed back-to-back K-step bodies before timing (clock ramp)")
     ap.add_argument("--no-ceiling", action="store_true",
                     help="skip the same-run streaming-read ceiling probe")
+    ap.add_argument("--no-order-ab", dest="order_ab", action="store_false",
+                    help="skip the same-run A/B of dense visiting orders (configs 2 and 4)")
+    ap.add_argument("--inplace-schedule", default="auto", choices=["auto", "fused", "two_pass"],
+                    help="how --flags inplace writes the check fields (xcsum_ctx_set_inplace)")
     ap.add_argument("--flags", default="",
                     help="comma list of inplace,iphdr,rfc,verify (XCSUM_F_*); with inplace the "
                          "checks go into the frames and no result array is written, as in "
@@ -575,6 +649,8 @@ def main():
     eng = X.Engine(dev.index)
     if args.geometry:
         eng.set_geometry(*[int(v) for v in args.geometry.split(",")])
+    eng.set_inplace({"auto": X.INPLACE_AUTO, "fused": X.INPLACE_FUSED,
+                     "two_pass": X.INPLACE_TWO_PASS}[args.inplace_schedule])
     stream = torch.cuda.current_stream(dev)
     sptr = stream.cuda_stream
     desc, d_desc, bufs, out, first, count = build_batch(cfg, rank, world, torch, dev, eng, sptr)
@@ -697,11 +773,17 @@ def main():
     elapsed_max = float(np.median(walls_max))
     alg_all, frames_all = float(tot[0]), float(tot[1])
 
-    ceiling = inplace = None
+    ceiling = inplace = orders = None
     if rank == 0 and not args.no_ceiling:
         ceiling = stream_ceiling(torch, dev, bufs, sptr)
         if flags & X.F_INPLACE and with_out is False:
             inplace = inplace_ceiling(torch, dev, bufs, desc, flags, cfg["family"], sptr)
+        if args.order_ab and cfg["id"] in (2, 4) and not flags and not args.geometry:
+            # after the in-place probe (none here: no flags), before the
+            # parity pass: the order never changes results
+            orders = order_ab(torch, dev, eng, bufs, d_desc, count, out_arg, cfg, flags,
+                              len_hint, sptr, real_bytes(desc),
+                              ceiling["GBps"] if ceiling else None)
 
     if not with_out and count:
         # the in-place passes rewrote the check fields of every buffer (and the
@@ -770,6 +852,20 @@ def main():
             roof["ceiling_measured"] = ceiling["GBps"]
             roof["frac_vs_ceiling"] = round(roof["real_achieved"] / ceiling["GBps"], 4)
             roof["ceiling_probe"] = ceiling["what"]
+            # The layout's own bound: a launch must move `real` bytes to
+            # deliver `alg` algorithmic ones (config 3: a 106-byte frame in
+            # 112 bytes + a 16-byte descriptor per 82 algorithmic bytes), so
+            # at the same-run ceiling the algorithmic rate tops out at
+            # ceiling x alg / real.  layout_bound_frac = that bound over the
+            # 8 TB/s peak; frac_of_layout_bound = achieved over that bound.
+            alg_launch = slow[1]
+            bound = ceiling["GBps"] * alg_launch / real
+            roof["layout_alg_over_real"] = round(alg_launch / real, 4)
+            roof["layout_bound_GBps"] = round(bound, 1)
+            roof["layout_bound_frac"] = round(bound / HBM_PEAK_GBS, 4)
+            roof["frac_of_layout_bound"] = round(achieved / bound, 4)
+        if orders:
+            roof["order_ab"] = orders
         if inplace:
             # same buffers, same reads, the same stores per frame, no arithmetic
             roof["inplace_probe_ms"] = inplace["ms"]
@@ -799,6 +895,8 @@ def main():
                        "family": cfg["family"], "mode": MODE_NAMES[cfg["mode"]],
                        "flags": fl or "none",
                        "result_array": with_out,
+                       "inplace_schedule": (args.inplace_schedule if flags & X.F_INPLACE
+                                            and not flags & X.F_VERIFY else None),
                        "layout": "packed, 8-byte aligned frames" if args.layout == "packed"
                        else "xudp TX UMEM: one frame per 4096-byte chunk",
                        "visiting_order": "automatic (32 regions of 16-frame tiles if the batch "

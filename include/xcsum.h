@@ -113,6 +113,25 @@ int xcsum_ctx_set_launch(xcsum_ctx *ctx, int blocks_per_cu);
  * XCSUM_ORDER="R,T" sets it at context creation. */
 int xcsum_ctx_set_order(xcsum_ctx *ctx, int region_log2, int tile_log2);
 
+/* How xcsum_batch_device writes the check fields with XCSUM_F_INPLACE
+ * (results and frame bytes are identical either way):
+ *   FUSED: each field is stored by the pass that sums its frame;
+ *   TWO_PASS: the checksum pass writes a result array (d_out, or a scratch
+ *     array of the context), then a second launch stores the fields in frame
+ *     order -- the stores no longer interleave with the read stream
+ *     (DESIGN.md 5.3).  Its scratch is allocated on the first such call, so
+ *     make one call before capturing a stream into a graph (a call under
+ *     capture that finds no scratch runs FUSED); calls of one context on
+ *     different streams are ordered through an event.
+ *   AUTO (default): FUSED.  Measured on config 2, the
+ *     second pass costs more than the interleaving it removes: the lines it
+ *     writes have left the caches by then and come back from HBM.
+ * Env XCSUM_INPLACE=fused|two_pass sets it at context creation. */
+#define XCSUM_INPLACE_AUTO     0
+#define XCSUM_INPLACE_FUSED    1
+#define XCSUM_INPLACE_TWO_PASS 2
+int xcsum_ctx_set_inplace(xcsum_ctx *ctx, int schedule);
+
 /* ---- device-resident batch ------------------------------------------------
  * Replaces the per-frame checksum work of the xudp_frame_send loop
  * (xudp/tx.c:696-726 -> __xudp_frame_send -> xudp_packet_udp, packet.c:156)

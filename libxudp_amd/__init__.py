@@ -65,7 +65,7 @@ SEG_GEOMETRIES = [(64, 64, 4), (64, 64, 8), (64, 16, 4)]
 # csrc/xcsum_internal.h, in order from 1)
 BOUNDS_SITES = ["csum_chunk", "csum_walk", "csum_hdr", "csum_out", "csum_inplace",
                 "stream_region", "stream_stage", "build_src", "build_data", "build_out",
-                "rx_chunk", "rx_rec", "rx_part", "rx_stream", "gen_store"]
+                "rx_chunk", "rx_rec", "rx_part", "rx_stream", "gen_store", "scatter"]
 
 
 def debug_build():
@@ -101,6 +101,9 @@ def variant_geometries():
     """The A/B geometries the loaded library runs ([] for libxcsum.so)."""
     return LDS_GEOMETRIES + SEG_GEOMETRIES if variants_built() else []
 
+
+# xcsum_ctx_set_inplace schedules
+INPLACE_AUTO, INPLACE_FUSED, INPLACE_TWO_PASS = 0, 1, 2
 
 F_BUILD_INPLACE = 0x20
 F_SRC_ALIGNED = 0x40
@@ -139,6 +142,7 @@ _SIGS = {
     "xcsum_ctx_set_launch": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     "xcsum_ctx_set_order": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int]),
     "xcsum_ctx_set_resident": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_uint32]),
+    "xcsum_ctx_set_inplace": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     "xcsum_batch_device": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                           ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint32,
                                           ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p]),
@@ -322,6 +326,10 @@ class Engine:
     def set_order(self, region_log2=-1, tile_log2=0):
         _check(lib().xcsum_ctx_set_order(self._ctx, region_log2, tile_log2),
                "xcsum_ctx_set_order")
+
+    def set_inplace(self, schedule=INPLACE_AUTO):
+        """how XCSUM_F_INPLACE writes the check fields (INPLACE_*)"""
+        _check(lib().xcsum_ctx_set_inplace(self._ctx, schedule), "xcsum_ctx_set_inplace")
 
     def set_resident(self, workgroups=0, idle_us=0):
         """Resident workgroups for small host batches (0: off), see xcsum.h."""

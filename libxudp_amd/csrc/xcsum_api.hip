@@ -13,6 +13,8 @@
 #include <mutex>
 #include <thread>
 
+#include <hsa/hsa_ext_amd.h>
+
 #include "xcsum_internal.h"
 #include "xcsum_gen.h"
 
@@ -42,6 +44,11 @@ extern "C" int xcsum_last_hip_error(int *line, const char **name)
 
 /* resident server defaults (xcsum_ctx_set_resident) */
 static constexpr uint32_t RES_IDLE_US = 20000;     /* workgroups leave after 20 ms idle */
+/* ... and after 2 ms alive even when busy: a live resident grid blocks the
+ * work of any stream that shares its hardware queue (GPU_MAX_HW_QUEUES is 4;
+ * streams beyond that share queues), so its life is bounded; the next batch
+ * relaunches (~10 us, once per 2 ms of service) */
+static constexpr uint32_t RES_LIFE_US = 2000;
 static constexpr uint32_t RES_MAX_FRAMES = 4096;   /* larger batches are launched */
 static constexpr int RES_TIMEOUT_S = 30;           /* no answer: the call fails */
 
@@ -125,6 +132,11 @@ static void env_resident(xcsum_ctx *c)
 	c->res_seq = 0;
 	c->res_gen = 0;
 	c->res_trace = getenv("XCSUM_RESIDENT_TRACE") != nullptr;
+	/* diagnostic: the workgroups' life bound (RES_LIFE_US), to measure what
+	 * a long-lived grid does to streams sharing its hardware queue
+	 * (tests/test_gpu_resident.py::test_resident_queue_sharing) */
+	const char *life = getenv("XCSUM_RESIDENT_LIFE_US");
+	c->res_life_us = life && atoi(life) > 0 ? (uint32_t)atoi(life) : RES_LIFE_US;
 	/* test hook: requests carry a limit this many bytes short, so the
 	 * workgroups' own descriptor check refuses the frames past it
 	 * (tests/test_gpu_resident.py::test_resident_descriptor_check) */
@@ -176,6 +188,46 @@ static int resident_stop(xcsum_ctx *c)
 		return -XCSUM_ERR_HIP;
 	}
 	return 0;
+}
+
+/* A caller stream a device entry point launched this context's work on. */
+static void note_stream(xcsum_ctx *c, void *s)
+{
+	for (void *x : c->streams_used)
+		if (x == s)
+			return;
+	c->streams_used.push_back(s);
+}
+
+static void drain_slots(xcsum_ctx *c);
+static void reg_trace(const char *what, const void *base, size_t size, const void *dev,
+		      int known_before);
+
+/* Wait for everything this context started: its resident workgroups (asked
+ * to leave), its host-path slots, and the caller streams its device entry
+ * points launched on.  Not hipDeviceSynchronize: another context's resident
+ * workgroups leave only after their idle time without a batch, so a
+ * device-wide wait lasts as long as that context stays busy.
+ * A caller stream destroyed since is skipped (the runtime refuses the
+ * handle); any other error is returned. */
+static int drain_ctx(xcsum_ctx *c)
+{
+	int rc = resident_stop(c);
+	drain_slots(c);
+	for (void *s : c->streams_used) {
+		const hipError_t e = hipStreamSynchronize((hipStream_t)s);
+		if (e == hipErrorContextIsDestroyed || e == hipErrorInvalidHandle ||
+		    e == hipErrorInvalidResourceHandle) {
+			(void)hipGetLastError();
+			continue;
+		}
+		if (e != hipSuccess && !rc) {
+			t_hip_err = (int)e;
+			t_hip_line = __LINE__;
+			rc = -XCSUM_ERR_HIP;
+		}
+	}
+	return rc;
 }
 
 /* Doorbell memory: the doorbell (request + descriptors) and the done words in
@@ -328,6 +380,7 @@ static hipError_t resident_launch(xcsum_ctx *c, uint32_t served0, uint32_t skip_
 	c->res_gen = c->res_gen + 1u ? c->res_gen + 1u : 1u;
 	const hipError_t e = launch_resident(c->res_vbell, c->res_vdone, c->d_err, c->res_wg,
 					     c->res_gen, served0, skip_seq, skip_mask, c->res_idle_us,
+					     c->res_life_us,
 					     c->res_stream);
 	c->res_live = e == hipSuccess;
 	return e;
@@ -392,8 +445,11 @@ static int resident_call(xcsum_ctx *c, const CsumArgs &a, uint64_t limit)
 	if (c->res_live)
 		for (int w = 0; w < W; w++)
 			if (done_word(c, w, RB_LEFT) == c->res_gen) {
-				HIPCHK(hipStreamSynchronize(c->res_stream));
-				c->res_live = false;
+				/* the rest are told to leave at once (seq is not
+				 * out yet), or they would poll to their deadline */
+				const int rc = resident_stop(c);
+				if (rc)
+					return rc;
 				break;
 			}
 	if (!c->res_live)
@@ -430,8 +486,14 @@ static int resident_call(xcsum_ctx *c, const CsumArgs &a, uint64_t limit)
 		if (gone == pending) {
 			/* every workgroup still owing an answer left before it saw
 			 * the request: once all are gone (and done[] is final),
-			 * relaunch; those that answered skip it */
-			HIPCHK(hipStreamSynchronize(c->res_stream));
+			 * relaunch; those that answered skip it.  The ones that
+			 * answered are told to leave first, or they would poll
+			 * until their idle deadline */
+			{
+				const int rc = resident_stop(c);
+				if (rc)
+					return rc;
+			}
 			for (int w = 0; w < W; w++)
 				if (((pending >> w) & 1ull) && done_word(c, w, 0) == seq)
 					pending &= ~(1ull << w);
@@ -515,6 +577,20 @@ extern "C" int xcsum_ctx_create(int device, xcsum_ctx **out)
 	}
 	c->frame_cap = 0;
 	c->desc_cap = 0;
+	c->inplace_sched = XCSUM_INPLACE_AUTO;
+	if (const char *e = getenv("XCSUM_INPLACE"))
+		c->inplace_sched = strcmp(e, "fused") == 0      ? XCSUM_INPLACE_FUSED
+				   : strcmp(e, "two_pass") == 0 ? XCSUM_INPLACE_TWO_PASS
+								: XCSUM_INPLACE_AUTO;
+	/* XCSUM_INPLACE_BLOCK=0|32|64: the second pass's store width (A/B) */
+	c->inplace_block = 32;
+	if (const char *e = getenv("XCSUM_INPLACE_BLOCK"))
+		c->inplace_block = (uint32_t)atoi(e) == 64 ? 64u : (uint32_t)atoi(e) == 32 ? 32u : 0u;
+	c->d_inplace = nullptr;
+	c->inplace_cap = 0;
+	c->inplace_done = nullptr;
+	c->inplace_stream = nullptr;
+	c->inplace_recorded = false;
 	c->geom = env_geometry();
 	c->blocks_per_cu = 0;
 	env_order(c);
@@ -560,21 +636,26 @@ extern "C" void xcsum_ctx_destroy(xcsum_ctx *c)
 	if (!c)
 		return;
 	(void)hipSetDevice(c->device);
-	(void)resident_stop(c);
 	if (c->res_trace && c->res_calls)
 		fprintf(stderr, "xcsum resident: %llu calls, %.2f us per call, %.2f us of it "
 			"from the doorbell store to the last answer\n",
 			(unsigned long long)c->res_calls, c->res_call_us / c->res_calls,
 			c->res_spin_us / c->res_calls);
-	(void)hipDeviceSynchronize();
+	(void)drain_ctx(c);
 	resident_free(c);
 	free_staging(c);
-	for (auto &r : c->regions)
-		(void)hipHostUnregister(r.host);
+	for (auto &r : c->regions) {
+		(void)hipHostUnregister(r.reg);
+		reg_trace("unregister", r.host, r.size, r.dev, 0);
+	}
 	if (c->d_err)
 		(void)hipFree(c->d_err);
 	if (c->d_rx_part)
 		(void)hipFree(c->d_rx_part);
+	if (c->d_inplace)
+		(void)hipFree(c->d_inplace);
+	if (c->inplace_done)
+		(void)hipEventDestroy(c->inplace_done);
 	delete c;
 }
 
@@ -590,11 +671,10 @@ extern "C" int xcsum_ctx_take_errors(xcsum_ctx *c, uint64_t *count)
 		return -XCSUM_ERR_INVAL;
 	HIPCHK(hipSetDevice(c->device));
 	{
-		const int rc = resident_stop(c);   /* or the device sync waits for it */
+		const int rc = drain_ctx(c);
 		if (rc)
 			return rc;
 	}
-	HIPCHK(hipDeviceSynchronize());
 	HIPCHK(hipMemcpy(&v, c->d_err, sizeof(v), hipMemcpyDeviceToHost));
 	HIPCHK(hipMemset(c->d_err, 0, sizeof(v)));
 	*count = v;
@@ -687,6 +767,68 @@ extern "C" int xcsum_ctx_set_launch(xcsum_ctx *c, int blocks_per_cu)
 	return 0;
 }
 
+/* XCSUM_F_INPLACE in two passes (xcsum_scatter.hip): the checksum pass
+ * without INPLACE into d_out (or the context's scratch) and, with IPHDR, the
+ * scratch's iph->check half; then the scatter launch stores the fields.
+ * *done = false: the caller runs the fused pass instead (the scratch would
+ * have to be allocated while the stream is being captured). */
+static int inplace_two_pass(xcsum_ctx *c, const CsumArgs &a, const Geometry &g, hipStream_t s,
+			    bool *done)
+{
+	const bool iph = (a.flags & XCSUM_F_IPHDR) != 0;
+	const bool scratch = !a.out || iph;
+	hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+	HIPCHK(hipStreamIsCapturing(s, &cs));
+	const bool capturing = cs != hipStreamCaptureStatusNone;
+	if (scratch && c->inplace_cap < a.n) {
+		if (capturing)
+			return 0;   /* no allocation under capture: fused */
+		uint32_t cap = 1u << 16;
+		while (cap < a.n)
+			cap = cap >= (1u << 31) ? a.n : cap * 2;
+		uint16_t *p = nullptr;
+		/* hipFree waits for the device: the previous array is idle */
+		if (c->d_inplace)
+			HIPCHK(hipFree(c->d_inplace));
+		c->d_inplace = nullptr;
+		c->inplace_cap = 0;
+		if (hipMalloc(&p, (size_t)cap * 2 * sizeof(uint16_t)) != hipSuccess)
+			return -XCSUM_ERR_NOMEM;
+		c->d_inplace = p;
+		c->inplace_cap = cap;
+	}
+	if (scratch && !capturing) {
+		if (!c->inplace_done)
+			HIPCHK(hipEventCreateWithFlags(&c->inplace_done, hipEventDisableTiming));
+		/* the scratch is the context's: a call on another stream waits for
+		 * the last one's second pass */
+		if (c->inplace_recorded && c->inplace_stream != (void *)s)
+			HIPCHK(hipStreamWaitEvent(s, c->inplace_done, 0));
+	}
+	CsumArgs b = a;
+	b.flags &= ~XCSUM_F_INPLACE;
+	b.out = a.out ? a.out : c->d_inplace;
+	b.out_ip = iph ? c->d_inplace + c->inplace_cap : nullptr;
+	HIPCHK(launch_csum(b, g, c->cus, s));
+	ScatterArgs t;
+	t.umem = a.umem;
+	t.desc = a.desc;
+	t.n = a.n;
+	t.mode = a.mode;
+	t.res = b.out;
+	t.res_ip = b.out_ip;
+	t.bias = a.bias;
+	t.block = c->inplace_block;
+	HIPCHK(launch_scatter(t, c->cus, s));
+	if (scratch && !capturing) {
+		HIPCHK(hipEventRecord(c->inplace_done, s));
+		c->inplace_stream = (void *)s;
+		c->inplace_recorded = true;
+	}
+	*done = true;
+	return 0;
+}
+
 extern "C" int xcsum_batch_device(xcsum_ctx *c, uint8_t *d_umem, const struct xcsum_desc *d_desc,
 				  uint32_t n, uint16_t *d_out, uint32_t mode, uint32_t flags,
 				  uint32_t len_hint, void *stream)
@@ -698,6 +840,7 @@ extern "C" int xcsum_batch_device(xcsum_ctx *c, uint8_t *d_umem, const struct xc
 	if (!d_umem || !d_desc || (!d_out && !(flags & XCSUM_F_INPLACE)))
 		return -XCSUM_ERR_INVAL;
 	HIPCHK(hipSetDevice(c->device));
+	note_stream(c, stream);
 	CsumArgs a;
 	a.umem = d_umem;
 	a.desc = d_desc;
@@ -712,7 +855,22 @@ extern "C" int xcsum_batch_device(xcsum_ctx *c, uint8_t *d_umem, const struct xc
 	a.err = c->d_err;
 	const Geometry g = geometry_for(c, len_hint, a.flags);
 	set_order(c, a, g);
+	/* AUTO is FUSED: the two-pass schedule measured slower */
+	if ((a.flags & XCSUM_F_INPLACE) && c->inplace_sched == XCSUM_INPLACE_TWO_PASS) {
+		bool done = false;
+		const int rc = inplace_two_pass(c, a, g, (hipStream_t)stream, &done);
+		if (rc || done)
+			return rc;
+	}
 	HIPCHK(launch_csum(a, g, c->cus, (hipStream_t)stream));
+	return 0;
+}
+
+extern "C" int xcsum_ctx_set_inplace(xcsum_ctx *c, int schedule)
+{
+	if (!c || schedule < XCSUM_INPLACE_AUTO || schedule > XCSUM_INPLACE_TWO_PASS)
+		return -XCSUM_ERR_INVAL;
+	c->inplace_sched = schedule;
 	return 0;
 }
 
@@ -740,6 +898,7 @@ extern "C" int xcsum_rx_device(xcsum_ctx *c, const uint8_t *d_umem, const struct
 	a.msgs = d_msgs;
 	a.count = d_count;
 	a.part = c->d_rx_part;
+	note_stream(c, stream);
 	HIPCHK(launch_rx(a, len_hint, c->cus, (hipStream_t)stream));
 	return 0;
 }
@@ -819,6 +978,7 @@ extern "C" int xcsum_build_device(xcsum_ctx *c, const struct xcsum_route *route,
 		const uint32_t typ = hdr + (len_hint ? len_hint : 1472u);
 		a.ord = frame_size >= 2u * typ ? order_regions(n, 5, 4) : order_identity(n);
 	}
+	note_stream(c, stream);
 	HIPCHK(launch_build(a, len_hint, c->cus, (hipStream_t)stream));
 	return 0;
 }
@@ -834,19 +994,117 @@ extern "C" int xcsum_sync(xcsum_ctx *c, void *stream)
 
 /* ---- UMEM registration --------------------------------------------------- */
 
+/* XCSUM_REG_TRACE=<file>: one line per registration and unregistration
+ * (diagnostic of the registered-memory faults): the host range,
+ * its page range, the device alias the runtime returned, whether the runtime
+ * already knew the address before the call, the VMA flags of the pages
+ * (locked "lo", THP "hg"/"nh", from /proc/self/smaps), and whether the device
+ * alias overlaps one handed out by an earlier, since unregistered,
+ * registration of this process (a recycled GPU virtual range). */
+static std::mutex g_reg_mu;
+struct DevRange {
+	uintptr_t lo, hi;
+};
+static std::vector<DevRange> g_reg_freed;   /* device ranges of past registrations */
+
+static void vma_flags(uintptr_t lo, uintptr_t hi, char *out, size_t cap)
+{
+	out[0] = 0;
+	FILE *f = fopen("/proc/self/smaps", "r");
+	if (!f)
+		return;
+	char line[512];
+	uintptr_t s = 0, e = 0;
+	unsigned long thp_kb = 0;
+	size_t used = 0;
+	while (fgets(line, sizeof line, f)) {
+		unsigned long a, b;
+		if (sscanf(line, "%lx-%lx ", &a, &b) == 2 && strchr(line, '-') < strchr(line, ' ')) {
+			s = a;
+			e = b;
+			thp_kb = 0;
+			continue;
+		}
+		(void)sscanf(line, "AnonHugePages: %lu kB", &thp_kb);
+		if (strncmp(line, "VmFlags:", 8) == 0 && s < hi && e > lo) {
+			line[strcspn(line, "\n")] = 0;
+			const int k = snprintf(out + used, cap - used, "[%lx-%lx:%s thp_kb=%lu]",
+					       (unsigned long)s, (unsigned long)e, line + 8, thp_kb);
+			if (k > 0 && used + (size_t)k < cap)
+				used += (size_t)k;
+		}
+	}
+	fclose(f);
+}
+
+/* What ROCr knows about the allocation holding p: its type, host base and
+ * size ("%d:%p+%zu"), for the trace; *lo / *sz get the locked extent. */
+static int rocr_extent(const void *p, uintptr_t *lo, size_t *sz)
+{
+	hsa_amd_pointer_info_t info;
+	memset(&info, 0, sizeof info);
+	info.size = sizeof info;
+	if (hsa_amd_pointer_info(p, &info, nullptr, nullptr, nullptr) != HSA_STATUS_SUCCESS)
+		return -1;
+	*lo = (uintptr_t)info.hostBaseAddress;
+	*sz = info.sizeInBytes;
+	return (int)info.type;
+}
+
+static void reg_trace(const char *what, const void *base, size_t size, const void *dev,
+		      int known_before)
+{
+	const char *path = getenv("XCSUM_REG_TRACE");
+	std::lock_guard<std::mutex> g(g_reg_mu);
+	const uintptr_t plo = (uintptr_t)base & ~(uintptr_t)4095;
+	const uintptr_t phi = ((uintptr_t)base + size + 4095) & ~(uintptr_t)4095;
+	const uintptr_t dlo = (uintptr_t)dev & ~(uintptr_t)4095;
+	const uintptr_t dhi = dlo + (phi - plo);
+	bool recycled = false;
+	if (what[0] == 'r')
+		for (const DevRange &r : g_reg_freed)
+			recycled |= r.lo < dhi && r.hi > dlo;
+	else if (dev) {
+		g_reg_freed.push_back(DevRange{dlo, dhi});
+		if (g_reg_freed.size() > 4096)
+			g_reg_freed.erase(g_reg_freed.begin());
+	}
+	if (!path)
+		return;
+	char flags[1024];
+	vma_flags(plo, phi, flags, sizeof flags);
+	uintptr_t xl = 0;
+	size_t xs = 0;
+	const int xt = rocr_extent(base, &xl, &xs);
+	if (FILE *f = fopen(path, "a")) {
+		fprintf(f, "%s host=%p size=%zu pages=[%#lx,%#lx) dev=%p known_before=%d "
+			   "recycled_dev=%d rocr_now=%d:%#lx+%zu vma=%s\n",
+			what, base, size, (unsigned long)plo, (unsigned long)phi, dev, known_before,
+			(int)recycled, xt, (unsigned long)xl, xs, flags);
+		fclose(f);
+	}
+}
+
 extern "C" int xcsum_register_umem(xcsum_ctx *c, void *base, size_t size)
 {
 	void *dev = nullptr;
 	if (!c || !base || !size)
 		return -XCSUM_ERR_INVAL;
 	HIPCHK(hipSetDevice(c->device));
+	/* did the runtime know this address already (a registration or pinning
+	 * that was never released)?  Trace only. */
+	hipPointerAttribute_t pa;
+	const bool known = hipPointerGetAttributes(&pa, base) == hipSuccess &&
+			   pa.type != hipMemoryTypeUnregistered;
+	(void)hipGetLastError();
 	if (hipHostRegister(base, size, hipHostRegisterMapped) != hipSuccess)
 		return -XCSUM_ERR_HIP;
 	if (hipHostGetDevicePointer(&dev, base, 0) != hipSuccess) {
 		(void)hipHostUnregister(base);
 		return -XCSUM_ERR_HIP;
 	}
-	c->regions.push_back(Region{(uint8_t *)base, size, (uint8_t *)dev});
+	reg_trace("register", base, size, dev, known);
+	c->regions.push_back(Region{(uint8_t *)base, size, (uint8_t *)dev, (uint8_t *)base});
 	return 0;
 }
 
@@ -857,13 +1115,14 @@ extern "C" int xcsum_unregister_umem(xcsum_ctx *c, void *base)
 	for (size_t i = 0; i < c->regions.size(); i++) {
 		if (c->regions[i].host == (uint8_t *)base) {
 			HIPCHK(hipSetDevice(c->device));
-			/* no kernel or copy may still read or write the region once
-			 * it is unmapped: this context's resident workgroups, its
-			 * host-path streams and any stream a caller launched on its
-			 * device alias */
-			(void)resident_stop(c);
-			(void)hipDeviceSynchronize();
-			(void)hipHostUnregister(base);
+			/* no kernel or copy of this context may still read or write
+			 * the region once it is unmapped: its resident workgroups,
+			 * its host-path streams and the streams its device entry
+			 * points ran on (the region's device alias may have been
+			 * handed to them) */
+			(void)drain_ctx(c);
+			(void)hipHostUnregister(c->regions[i].reg);
+			reg_trace("unregister", base, c->regions[i].size, c->regions[i].dev, 0);
 			c->regions.erase(c->regions.begin() + i);
 			return 0;
 		}
@@ -1273,6 +1532,10 @@ static int batch_host_run(xcsum_ctx *c, uint8_t *h_umem, const struct xcsum_desc
 		rc = batch_host_resident(c, h_umem, h_desc, n, h_out, h_out_ip, mode, flags, zc,
 					 gather);
 		if (rc != RES_DECLINE)
+			return rc;
+		/* the launched path's slot streams may share a hardware queue
+		 * with the live grid, and would wait behind it: stop it first */
+		if (c->res_live && (rc = resident_stop(c)))
 			return rc;
 	}
 

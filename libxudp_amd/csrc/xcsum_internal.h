@@ -72,6 +72,7 @@ enum BoundsSite : uint32_t {
 	XB_RX_PART,             /* receive: per-block count slot */
 	XB_RX_STREAM,           /* receive stream kernel: region load */
 	XB_GEN_STORE,           /* synthetic fill: store vs the frame */
+	XB_SCATTER,             /* two-pass in-place: h_proto load / field store */
 	XB_SITE_COUNT
 };
 
@@ -113,6 +114,23 @@ struct CsumArgs {
 	 * each one before any load of its frame (desc_ok / desc_bad) */
 	static constexpr bool kChecked = false;
 };
+
+/* Second pass of the two-pass in-place schedule (xcsum_scatter.hip): store
+ * res[p] (and res_ip[p]) into the check fields of every well-formed frame. */
+struct ScatterArgs {
+	uint8_t *umem;
+	const struct xcsum_desc *desc;
+	uint32_t n;
+	uint32_t mode;
+	const uint16_t *res;
+	const uint16_t *res_ip;        /* IPHDR: iph->check values, else null */
+	uint64_t bias;
+	uint32_t block;                /* 0: 2-byte stores; 32 / 64: the whole
+					  sector / line holding a field, read and
+					  patched, when it lies inside the frame */
+};
+
+hipError_t launch_scatter(const ScatterArgs &a, int cus, hipStream_t s);
 
 /* Frame-build kernel arguments (xcsum_build.hip). */
 struct BuildArgs {
@@ -183,6 +201,7 @@ struct Region {
 	uint8_t *host;
 	size_t size;
 	uint8_t *dev;  /* device alias of the page-locked mapping */
+	uint8_t *reg;  /* the address handed to hipHostRegister (host, or its page) */
 };
 
 /* Per-thread context.  Owns only scratch: the error counter and the staging
@@ -196,7 +215,20 @@ struct Ctx {
 	int order_rlog, order_tlog;    /* visiting order, rlog < 0: automatic */
 	unsigned long long *d_err;
 	uint32_t *d_rx_part;           /* RX_PART_MAX per-block receive counts */
+	/* two-pass in-place schedule (xcsum_ctx_set_inplace): the result arrays
+	 * the first pass writes, 2 x u16 per frame, grown on demand */
+	int inplace_sched;
+	uint32_t inplace_block;        /* second-pass store width (ScatterArgs) */
+	uint16_t *d_inplace;
+	uint32_t inplace_cap;          /* frames */
+	hipEvent_t inplace_done;       /* after the last two-pass call's scatter */
+	void *inplace_stream;          /* the stream of that call */
+	bool inplace_recorded;         /* inplace_done was recorded */
 	std::vector<Region> regions;
+	/* caller streams the device entry points launched on: take_errors,
+	 * unregister_umem and destroy wait for these, the host-path slots and
+	 * the resident workgroups -- never for the whole device */
+	std::vector<void *> streams_used;
 
 	/* host path staging: NSLOT slots of frames + descriptors + results */
 	static const int NSLOT = 2;
@@ -224,6 +256,7 @@ struct Ctx {
 	 * xcsum_resident.hip): res_wg workgroups, 0 = off */
 	int res_wg;
 	uint32_t res_idle_us;
+	uint32_t res_life_us;          /* workgroups leave after this long alive */
 	uint32_t res_max_frames;       /* larger batches take the launched path */
 	ResidentBell *res_bell;        /* the doorbell, pinned host memory (lazy) */
 	ResidentBell *res_vbell;       /* its device alias */

@@ -62,7 +62,7 @@ struct alignas(64) ResidentDone {
 
 hipError_t launch_resident(ResidentBell *v_bell, ResidentDone *v_done, unsigned long long *err,
 			   int wg, uint32_t gen, uint32_t served0, uint32_t skip_seq,
-			   uint64_t skip_mask, uint32_t idle_us, hipStream_t s);
+			   uint64_t skip_mask, uint32_t idle_us, uint32_t life_us, hipStream_t s);
 
 } /* namespace xcsum */
 

@@ -29,9 +29,10 @@
  *     lane), never through the scalar cache, which the acquire does not
  *     invalidate.
  *
- * Lifetime: a workgroup leaves when the host sets `stop`, or after idle_ticks
- * of the 100 MHz wall clock without a request, so the grid always drains on
- * its own.  The host relaunches on the next batch (see resident_call in
+ * Lifetime: a workgroup leaves when the host sets `stop`, after idle_ticks
+ * of the 100 MHz wall clock without a request, or once it has lived
+ * life_ticks (checked between requests), so the grid always drains on its
+ * own and a busy server gives its hardware queue back every few ms.  The host relaunches on the next batch (see resident_call in
  * xcsum_api.hip, which also covers a workgroup that left at the idle deadline
  * while a request was on its way: it is relaunched with a mask of the
  * workgroups that already served that request, so no frame is done twice --
@@ -88,7 +89,8 @@ template <int G, int U, int K>
 __global__ void __launch_bounds__(256) resident_kernel(const ResidentBell *bell, ResidentDone *done,
 						       unsigned long long *err, uint32_t gen,
 						       uint32_t served0, uint32_t skip_seq,
-						       uint64_t skip_mask, uint64_t idle_ticks)
+						       uint64_t skip_mask, uint64_t idle_ticks,
+						       uint64_t life_ticks)
 {
 	__shared__ uint32_t cmd[RB_REQ_WORDS + 1];
 	__shared__ uint32_t first_bad_lds;   /* ResidentArgs::first_bad */
@@ -99,6 +101,7 @@ __global__ void __launch_bounds__(256) resident_kernel(const ResidentBell *bell,
 	if (blockIdx.x < 64 && ((skip_mask >> blockIdx.x) & 1ull))
 		served = skip_seq;
 	uint64_t last = wall_clock64();
+	const uint64_t born = last;
 	for (;;) {
 		if (threadIdx.x < 64) {
 			/* one load of the doorbell's first 256 bytes per poll: lane i
@@ -126,7 +129,13 @@ __global__ void __launch_bounds__(256) resident_kernel(const ResidentBell *bell,
 					go = 1;
 					break;
 				}
-				if (wall_clock64() - last > idle_ticks)
+				/* idle, or alive for life_ticks: leave (the next batch
+				 * relaunches).  The life bound caps how long a busy
+				 * server holds its hardware queue, which other streams
+				 * of the process may share (GPU_MAX_HW_QUEUES): their
+				 * work waits behind this grid */
+				const uint64_t now = wall_clock64();
+				if (now - last > idle_ticks || now - born > life_ticks)
 					break;
 				__builtin_amdgcn_s_sleep(1);
 			}
@@ -207,13 +216,14 @@ __global__ void __launch_bounds__(256) resident_kernel(const ResidentBell *bell,
 
 hipError_t launch_resident(ResidentBell *v_bell, ResidentDone *v_done, unsigned long long *err,
 			   int wg, uint32_t gen, uint32_t served0, uint32_t skip_seq,
-			   uint64_t skip_mask, uint32_t idle_us, hipStream_t s)
+			   uint64_t skip_mask, uint32_t idle_us, uint32_t life_us, hipStream_t s)
 {
 	if (wg <= 0 || wg > RB_MAX_WG)
 		return hipErrorInvalidValue;
 	(void)hipGetLastError();
 	hipLaunchKernelGGL((resident_kernel<16, 2, 6>), dim3((unsigned)wg), dim3(256), 0, s, v_bell, v_done,
-			   err, gen, served0, skip_seq, skip_mask, (uint64_t)idle_us * 100ull);
+			   err, gen, served0, skip_seq, skip_mask, (uint64_t)idle_us * 100ull,
+			   (uint64_t)life_us * 100ull);
 	return hipGetLastError();
 }
 

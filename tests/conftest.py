@@ -2,6 +2,12 @@ import json
 import os
 import sys
 
+if os.environ.get("XCSUM_TEST_NO_THP"):
+    # diagnostic: no transparent huge pages in this process
+    # (PR_SET_THP_DISABLE = 41), set before the heap grows
+    import ctypes
+    assert ctypes.CDLL(None, use_errno=True).prctl(41, 1, 0, 0, 0) == 0
+
 import numpy as np
 import pytest
 
@@ -64,6 +70,18 @@ def engine():
     e = X.Engine(0)
     yield e
     e.close()
+
+
+@pytest.fixture(autouse=True)
+def reg_trace_marker(request):
+    """With XCSUM_REG_TRACE=<file> (the library's registration trace,
+    DESIGN.md 6), each test's node id goes into the same file before the
+    test, so a registration line names the test that made it."""
+    path = os.environ.get("XCSUM_REG_TRACE")
+    if path:
+        with open(path, "a") as f:
+            f.write(f"test {request.node.nodeid}\n")
+    yield
 
 
 @pytest.fixture(autouse=True)

@@ -14,7 +14,7 @@ import pytest
 
 import libxudp_amd as X
 import oracle
-from conftest import golden_desc
+from conftest import golden_desc, h2d, d2h
 from test_gpu_host_path import check_inplace, host_batch
 
 pytestmark = pytest.mark.gpu
@@ -363,3 +363,105 @@ def test_resident_inline_descriptors(res_engine):
             assert np.array_equal(got, oracle.batch(umem, d, X.MODE_V6)), (it, n)
     finally:
         res_engine.unregister_umem(umem)
+
+
+def _busy_resident_loop(eng, stop, errors, calls):
+    """Context `eng` keeps sending 100-frame batches (libxudp's tx_batch_num)
+    through its resident workgroups until `stop` is set."""
+    umem, desc = X.gen_frames_host(100, 4, 0, 1400, seed=61, align=8)
+    exp = oracle.batch(umem, desc, X.MODE_V4_RFC)
+    try:
+        while not stop.is_set():
+            if not np.array_equal(host_batch(eng, umem, desc, X.MODE_V4_RFC), exp):
+                errors.append("mismatch")
+                return
+            calls[0] += 1
+    except Exception as ex:   # surfaces in the main thread's assert
+        errors.append(repr(ex))
+
+
+def test_resident_peer_busy_teardown_bounded():
+    """one context's take_errors, unregister_umem and destroy wait
+    for that context's own work only -- never for a peer context whose
+    resident workgroups stay busy (a device-wide wait would last as long as
+    the peer keeps sending)."""
+    import threading
+    a = X.Engine(0)
+    a.set_resident(8)
+    stop, errors, calls = threading.Event(), [], [0]
+    t = threading.Thread(target=_busy_resident_loop, args=(a, stop, errors, calls))
+    t.start()
+    try:
+        time.sleep(0.05)
+        b = X.Engine(0)
+        b.set_resident(8)
+        umem, desc = X.gen_frames_host(50, 6, 0, 600, seed=62, align=8)
+        t0 = time.perf_counter()
+        b.register_umem(umem)
+        assert np.array_equal(host_batch(b, umem, desc, X.MODE_V6),
+                              oracle.batch(umem, desc, X.MODE_V6))
+        b.take_errors()
+        b.unregister_umem(umem)
+        b.close()
+        dt = time.perf_counter() - t0
+        n_during = calls[0]
+    finally:
+        stop.set()
+        t.join(60)
+        a.close()
+    assert not errors, errors
+    assert n_during > 0
+    assert dt < 2.0, f"teardown beside a busy peer took {dt:.3f} s"
+
+
+@pytest.mark.parametrize("life_us", [None, 200000])
+def test_resident_queue_sharing(torch_cuda, monkeypatch, capsys, life_us):
+    """streams beyond GPU_MAX_HW_QUEUES share hardware queues, and
+    work behind a live resident grid on a shared queue waits until the grid
+    leaves.  Measured: a busy resident context in one thread, small device
+    batches on eight fresh streams in this one; the slowest batch's latency
+    is printed for both life bounds (the default 2 ms, and 200 ms as the
+    diagnostic XCSUM_RESIDENT_LIFE_US sets it).  With the default the wait
+    is bounded by the life bound; results are always right."""
+    import threading
+    torch = torch_cuda
+    dev = torch.device("cuda:0")
+    if life_us:
+        monkeypatch.setenv("XCSUM_RESIDENT_LIFE_US", str(life_us))
+    a = X.Engine(0)
+    a.set_resident(8)
+    monkeypatch.delenv("XCSUM_RESIDENT_LIFE_US", raising=False)
+    b = X.Engine(0)
+    umem, desc = X.gen_frames_host(2000, 4, 0, 1472, seed=63, align=8)
+    exp = oracle.batch(umem, desc, X.MODE_V4_LEGACY)
+    d_umem = h2d(torch, umem, dev)
+    d_desc = h2d(torch, desc.view(np.uint8), dev)
+    streams = [torch.cuda.Stream(dev) for _ in range(8)]
+    outs = [torch.zeros(len(desc), dtype=torch.int16, device=dev) for _ in streams]
+    stop, errors, calls = threading.Event(), [], [0]
+    t = threading.Thread(target=_busy_resident_loop, args=(a, stop, errors, calls))
+    t.start()
+    worst = 0.0
+    try:
+        time.sleep(0.05)
+        for _ in range(5):
+            for s, o in zip(streams, outs):
+                t0 = time.perf_counter()
+                b.batch_device(d_umem, d_desc, len(desc), o, X.MODE_V4_LEGACY, 0, 1500,
+                               stream=s.cuda_stream)
+                s.synchronize()
+                worst = max(worst, time.perf_counter() - t0)
+    finally:
+        stop.set()
+        t.join(60)
+        a.close()
+        b.close()
+    assert not errors, errors
+    for o in outs:
+        assert np.array_equal(d2h(o).view(np.uint16), exp)
+    with capsys.disabled():
+        print(f"\n[queue sharing] resident life {life_us or 'default 2000'} us: slowest of 40 "
+              f"device batches on 8 streams beside a busy resident context: "
+              f"{worst * 1e3:.2f} ms ({calls[0]} resident calls meanwhile)")
+    if life_us is None:
+        assert worst < 0.1, f"a device batch waited {worst * 1e3:.1f} ms"

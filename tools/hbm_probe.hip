@@ -212,3 +212,164 @@ extern "C" int probe_stream_read_inplace(void *p, uint64_t nbytes, uint64_t fstr
 #undef L
 	return hipGetLastError() == hipSuccess ? 0 : -1;
 }
+
+/* Two-pass schedule of the in-place probe: the plain stream read (no
+ * stores), then a second launch that stores the 2-byte field(s) of every
+ * frame, one thread per frame, in frame order -- the write pattern of the
+ * library's two-pass in-place schedule (xcsum_scatter.hip) with none of its
+ * arithmetic.  Both launches go on `stream`; time them together. */
+__global__ void __launch_bounds__(256) scatter_fields(uint8_t *p, uint64_t fstride, uint64_t off,
+						      uint64_t nframes, uint32_t f1, uint32_t f2)
+{
+	const uint64_t stride = (uint64_t)gridDim.x * 256;
+	for (uint64_t j = (uint64_t)blockIdx.x * 256 + threadIdx.x; j < nframes; j += stride) {
+		uint8_t *e = p + j * fstride + off;
+		*reinterpret_cast<uint16_t *>(e + f1) = (uint16_t)j;
+		if (f2 != f1)
+			*reinterpret_cast<uint16_t *>(e + f2) = (uint16_t)(j >> 16);
+	}
+}
+
+extern "C" int probe_stream_read_twopass(void *p, uint64_t nbytes, uint64_t fstride, uint64_t off,
+					 uint64_t nframes, uint32_t f1, uint32_t f2, uint32_t *out,
+					 int blocks, void *stream)
+{
+	if (fstride < 16 || !nframes || (f1 & 1) || (f2 & 1) || (off & 1))
+		return -1;
+	if ((nframes - 1) * fstride + off + (f1 > f2 ? f1 : f2) + 2 > nbytes)
+		return -1;
+	hipLaunchKernelGGL((stream_read<true, 4>), dim3(blocks), dim3(256), 0, (hipStream_t)stream,
+			   (const u32x4 *)p, nbytes / 16, out);
+	uint64_t sb = (nframes + 255) / 256;
+	if (sb > (uint64_t)blocks)
+		sb = (uint64_t)blocks;
+	hipLaunchKernelGGL(scatter_fields, dim3((unsigned)sb), dim3(256), 0, (hipStream_t)stream,
+			   (uint8_t *)p, fstride, off, nframes, f1, f2);
+	return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+/* The second pass with whole-block writes: for each field, the W-byte block
+ * (W = 32: a sector, 64: a line) holding it is read, patched and written
+ * back in full (W/16 dwordx4 loads, then as many stores), so the memory
+ * side sees complete blocks rather than 2-byte partial writes.  Blocks that
+ * hold both fields are written once. */
+template <int W>
+__global__ void __launch_bounds__(256) scatter_blocks(uint8_t *p, uint64_t fstride, uint64_t off,
+						      uint64_t nframes, uint32_t f1, uint32_t f2)
+{
+	const uint64_t stride = (uint64_t)gridDim.x * 256;
+	for (uint64_t j = (uint64_t)blockIdx.x * 256 + threadIdx.x; j < nframes; j += stride) {
+		uint8_t *e = p + j * fstride + off;
+		uint8_t *b1 = (uint8_t *)((uintptr_t)(e + f1) & ~(uintptr_t)(W - 1));
+		uint8_t *b2 = (uint8_t *)((uintptr_t)(e + f2) & ~(uintptr_t)(W - 1));
+		const int nb = b1 == b2 ? 1 : 2;
+		for (int k = 0; k < nb; k++) {
+			uint8_t *b = k ? b2 : b1;
+			u32x4 v[W / 16];
+#pragma unroll
+			for (int q = 0; q < W / 16; q++)
+				v[q] = *((gu32x4 *)(b + 16 * q));
+			v[0].x ^= (uint32_t)j;   /* "patch" */
+#pragma unroll
+			for (int q = 0; q < W / 16; q++)
+				*((u32x4 *)(b + 16 * q)) = v[q];
+		}
+	}
+}
+
+/* stream read, then the block-write second pass (W = 32 or 64) */
+extern "C" int probe_stream_read_twopass_blocks(void *p, uint64_t nbytes, uint64_t fstride,
+						uint64_t off, uint64_t nframes, uint32_t f1,
+						uint32_t f2, uint32_t *out, int blocks, int W,
+						int read_first, void *stream)
+{
+	if (fstride < 64 || !nframes || ((uintptr_t)p & 63))
+		return -1;
+	if ((nframes - 1) * fstride + off + (f1 > f2 ? f1 : f2) + 64 > nbytes)
+		return -1;
+	if (read_first)
+		hipLaunchKernelGGL((stream_read<true, 4>), dim3(blocks), dim3(256), 0,
+				   (hipStream_t)stream, (const u32x4 *)p, nbytes / 16, out);
+	uint64_t sb = (nframes + 255) / 256;
+	if (sb > (uint64_t)blocks)
+		sb = (uint64_t)blocks;
+	if (W == 64)
+		hipLaunchKernelGGL((scatter_blocks<64>), dim3((unsigned)sb), dim3(256), 0,
+				   (hipStream_t)stream, (uint8_t *)p, fstride, off, nframes, f1, f2);
+	else
+		hipLaunchKernelGGL((scatter_blocks<32>), dim3((unsigned)sb), dim3(256), 0,
+				   (hipStream_t)stream, (uint8_t *)p, fstride, off, nframes, f1, f2);
+	return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+/* the 2-byte second pass alone (no read pass), to time the stores by themselves */
+extern "C" int probe_scatter_fields(void *p, uint64_t nbytes, uint64_t fstride, uint64_t off,
+				    uint64_t nframes, uint32_t f1, uint32_t f2, int blocks,
+				    void *stream)
+{
+	if (fstride < 16 || !nframes || (f1 & 1) || (f2 & 1) || (off & 1))
+		return -1;
+	if ((nframes - 1) * fstride + off + (f1 > f2 ? f1 : f2) + 2 > nbytes)
+		return -1;
+	uint64_t sb = (nframes + 255) / 256;
+	if (sb > (uint64_t)blocks)
+		sb = (uint64_t)blocks;
+	hipLaunchKernelGGL(scatter_fields, dim3((unsigned)sb), dim3(256), 0, (hipStream_t)stream,
+			   (uint8_t *)p, fstride, off, nframes, f1, f2);
+	return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+/* frame j whose field at eth + f lies in chunk i, or -1 (as probe_field_store) */
+__device__ __forceinline__ int64_t probe_field_frame(uint64_t i, uint64_t fstride, uint64_t off,
+						     uint64_t nframes, uint32_t f, double inv)
+{
+	const int64_t x = (int64_t)(16 * i) - (int64_t)(off + f);
+	if (x + 16 <= 0)
+		return -1;
+	int64_t j = x <= 0 ? 0 : (int64_t)((double)x * inv);
+	if ((int64_t)(j * fstride) < x)
+		j++;
+	return j >= 0 && (uint64_t)j < nframes && (int64_t)(j * fstride) < x + 16 ? j : -1;
+}
+
+/* The in-place probe with the chunks that hold a field loaded temporally
+ * (allocated in L2 / the Infinity Cache, so the store that follows finds the
+ * line cached) and every other chunk nontemporal. */
+__global__ void __launch_bounds__(256) stream_read_inplace_tl(uint8_t *p, uint64_t n16,
+							    uint64_t fstride, uint64_t off,
+							    uint64_t nframes, uint32_t f1,
+							    uint32_t f2, double inv, uint32_t *out)
+{
+	uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+	const uint64_t stride = (uint64_t)gridDim.x * 256;
+	uint32_t acc = 0;
+	for (; i < n16; i += stride) {
+		const int64_t j1 = probe_field_frame(i, fstride, off, nframes, f1, inv);
+		const int64_t j2 = f2 != f1 ? probe_field_frame(i, fstride, off, nframes, f2, inv) : -1;
+		u32x4 v;
+		if (j1 >= 0 || j2 >= 0)
+			v = *((gu32x4 *)(p + 16 * i));
+		else
+			v = __builtin_nontemporal_load((gu32x4 *)(p + 16 * i));
+		acc += v.x ^ v.y ^ v.z ^ v.w;
+		if (j1 >= 0)
+			*reinterpret_cast<uint16_t *>(p + j1 * fstride + off + f1) = (uint16_t)(v.x ^ v.w);
+		if (j2 >= 0)
+			*reinterpret_cast<uint16_t *>(p + j2 * fstride + off + f2) = (uint16_t)(v.y ^ v.w);
+	}
+	out[(uint64_t)blockIdx.x * 256 + threadIdx.x] = acc;
+}
+
+extern "C" int probe_stream_read_inplace_tl(void *p, uint64_t nbytes, uint64_t fstride,
+					    uint64_t off, uint64_t nframes, uint32_t f1,
+					    uint32_t f2, uint32_t *out, int blocks, void *stream)
+{
+	if (fstride < 16 || !nframes || (f1 & 1) || (f2 & 1) || (off & 1))
+		return -1;
+	if ((nframes - 1) * fstride + off + (f1 > f2 ? f1 : f2) + 2 > nbytes)
+		return -1;
+	hipLaunchKernelGGL(stream_read_inplace_tl, dim3(blocks), dim3(256), 0, (hipStream_t)stream,
+			   (uint8_t *)p, nbytes / 16, fstride, off, nframes, f1, f2,
+			   1.0 / (double)fstride, out);
+	return hipGetLastError() == hipSuccess ? 0 : -1;
+}
