@@ -269,10 +269,22 @@ int xcsum_batch_host(xcsum_ctx *ctx, uint8_t *h_umem, const struct xcsum_desc *h
 
 /* Page-lock and map a host region (xudp's UMEM, xudp/xsk.c:222-341) for DMA
  * and zero-copy access.  Ownership stays with the caller.  Unregistering
- * waits for all work on the context's device first, so the caller may unmap
- * the region as soon as it returns. */
+ * waits for this context's work first (its host-path streams, its resident
+ * workgroups, the streams its device entry points ran on), so the caller may
+ * unmap the region as soon as it returns.
+ *
+ * Only memory whose pages stay put is mapped for the GPU: a region that is
+ * eligible for transparent huge pages (a VMA flagged MADV_HUGEPAGE -- numpy
+ * does that to arrays of 4 MiB and up -- or THP "always" without
+ * MADV_NOHUGEPAGE) is registered for bookkeeping only and its batches are
+ * staged through the context's pinned buffers (same results; DESIGN.md 6:
+ * every registered-memory GPU fault of rounds 2-4 was on such memory).
+ * libxudp's UMEM (anon_map: MAP_SHARED | MAP_ANONYMOUS | MAP_POPULATE |
+ * MAP_LOCKED, include/common.h:37-41) is mapped.  xcsum_umem_mapped() says
+ * which: 1 mapped, 0 staged, -XCSUM_ERR_NOT_REGISTERED if base is unknown. */
 int xcsum_register_umem(xcsum_ctx *ctx, void *base, size_t size);
 int xcsum_unregister_umem(xcsum_ctx *ctx, void *base);
+int xcsum_umem_mapped(xcsum_ctx *ctx, const void *base);
 
 /* Resident workgroups for small host batches (libxudp sends in batches of
  * tx_batch_num = 100 frames, xudp/xudp.c:74; tx.c:673-734 is one batch).

@@ -65,7 +65,7 @@ SEG_GEOMETRIES = [(64, 64, 4), (64, 64, 8), (64, 16, 4)]
 # csrc/xcsum_internal.h, in order from 1)
 BOUNDS_SITES = ["csum_chunk", "csum_walk", "csum_hdr", "csum_out", "csum_inplace",
                 "stream_region", "stream_stage", "build_src", "build_data", "build_out",
-                "rx_chunk", "rx_rec", "rx_part", "rx_stream", "gen_store", "scatter"]
+                "rx_chunk", "rx_rec", "rx_part", "rx_stream", "gen_store", "scatter", "csum_region", "res_req"]
 
 
 def debug_build():
@@ -162,6 +162,7 @@ _SIGS = {
                                      ctypes.POINTER(ctypes.c_uint32), ctypes.c_uint32]),
     "xcsum_register_umem": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t]),
     "xcsum_unregister_umem": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
+    "xcsum_umem_mapped": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
     "xcsum_sync": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
     "xcsum_ctx_pending": (ctypes.c_int, [ctypes.c_void_p]),
     "xcsum_last_hip_error": (ctypes.c_int, [ctypes.POINTER(ctypes.c_int),
@@ -257,6 +258,35 @@ def gen_layout(n, family, pmin, pmax=None, seed=0, first_index=0, align=8, strid
     _check(lib().xcsum_gen_layout(n, family, pmin, pmax, seed, first_index, align, stride,
                                   offset, _ptr(desc), ctypes.byref(nbytes)), "xcsum_gen_layout")
     return desc, int(nbytes.value)
+
+
+def umem_buffer(nbytes):
+    """A host UMEM mapped the way libxudp maps one (anon_map: MAP_SHARED |
+    MAP_ANONYMOUS, populated and locked, include/common.h:37-41), never backed
+    by transparent huge pages (MADV_NOHUGEPAGE before the pages exist), as a
+    zeroed uint8 ndarray.  xcsum_register_umem GPU-maps such memory (numpy's
+    own heap arrays may be THP-eligible and are then staged).
+    The mapping lives as long as the array; locking is best effort."""
+    import mmap
+    size = max(4096, (int(nbytes) + 4095) & ~4095)
+    m = mmap.mmap(-1, size, flags=mmap.MAP_SHARED | mmap.MAP_ANONYMOUS)
+    if hasattr(mmap, "MADV_NOHUGEPAGE"):
+        m.madvise(mmap.MADV_NOHUGEPAGE)
+    arr = np.frombuffer(m, dtype=np.uint8, count=int(nbytes))
+    arr[:] = 0                                  # populate
+    try:
+        libc = ctypes.CDLL(None, use_errno=True)
+        libc.mlock(ctypes.c_void_p(arr.ctypes.data), ctypes.c_size_t(size))
+    except (OSError, AttributeError):
+        pass
+    return arr
+
+
+def as_umem(arr):
+    """A copy of `arr` (uint8) in a umem_buffer()."""
+    u = umem_buffer(len(arr))
+    u[:] = arr
+    return u
 
 
 def gen_fill_host(umem, desc, family, seed=0, first_index=0):
@@ -380,6 +410,11 @@ class Engine:
 
     def unregister_umem(self, buf):
         _check(lib().xcsum_unregister_umem(self._ctx, _ptr(buf)), "xcsum_unregister_umem")
+
+    def umem_mapped(self, buf):
+        """1: the registered buffer is GPU-mapped; 0: staged (xcsum_umem_mapped)"""
+        return _check_nonneg(lib().xcsum_umem_mapped(self._ctx, _ptr(buf)),
+                             "xcsum_umem_mapped")
 
     def pending(self):
         """Host-path slots with work still in flight (0 after every host call)."""

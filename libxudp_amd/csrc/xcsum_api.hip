@@ -5,6 +5,7 @@
  * codes, never abort, errno untouched except by the packet.c mirrors.
  */
 #include <errno.h>
+#include <sys/prctl.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -428,6 +429,13 @@ static int resident_call(xcsum_ctx *c, const CsumArgs &a, uint64_t limit)
 	b->req[RB_MODE] = a.mode;
 	b->req[RB_FLAGS] = a.flags;
 	put64(RB_LIMIT, limit);
+	/* the buffers the request may point into (checked by the debug build) */
+	b->allow[RB_ALLOW_STAGE] = (uint64_t)(uintptr_t)c->v_stage[0];
+	b->allow[RB_ALLOW_STAGE + 1] = (uint64_t)(uintptr_t)c->v_stage[0] + c->frame_cap + 64;
+	b->allow[RB_ALLOW_DESC] = (uint64_t)(uintptr_t)c->res_vbell->desc;
+	b->allow[RB_ALLOW_DESC + 1] = (uint64_t)(uintptr_t)(c->res_vbell->desc + RB_DESC_CAP);
+	b->allow[RB_ALLOW_OUT] = (uint64_t)(uintptr_t)c->v_out[0];
+	b->allow[RB_ALLOW_OUT + 1] = (uint64_t)(uintptr_t)c->v_out[0] + 2 * c->desc_cap * sizeof(uint16_t);
 	/* a small batch's descriptors also go into the lines the workgroups
 	 * poll (three a line, the line's echo after them) */
 	if (a.n <= RB_INLINE && c->res_inline)
@@ -508,6 +516,16 @@ static int resident_call(xcsum_ctx *c, const CsumArgs &a, uint64_t limit)
 			 * RES_TIMEOUT_S rather than spin forever */
 			const hipError_t q = hipStreamQuery(c->res_stream);
 			if (q != hipErrorNotReady && q != hipSuccess) {
+#ifdef XCSUM_DEBUG_BOUNDS
+				/* what each workgroup was serving when the grid died */
+				for (int w = 0; w < W; w++) {
+					const uint32_t *cr = &c->res_done->done[RB_DONE_STRIDE * w + RB_CRUMB];
+					fprintf(stderr, "xcsum resident: fault: workgroup %d last request %u "
+						"umem %#llx n %u desc %#llx (this request %u)\n", w, cr[0],
+						(unsigned long long)(((uint64_t)cr[2] << 32) | cr[1]), cr[3],
+						(unsigned long long)(((uint64_t)cr[5] << 32) | cr[4]), seq);
+				}
+#endif
 				c->res_live = false;
 				t_hip_err = (int)q;
 				t_hip_line = __LINE__;
@@ -586,6 +604,9 @@ extern "C" int xcsum_ctx_create(int device, xcsum_ctx **out)
 	c->inplace_block = 32;
 	if (const char *e = getenv("XCSUM_INPLACE_BLOCK"))
 		c->inplace_block = (uint32_t)atoi(e) == 64 ? 64u : (uint32_t)atoi(e) == 32 ? 32u : 0u;
+	c->inplace_tl = 0;
+	if (const char *e = getenv("XCSUM_INPLACE_TL"))
+		c->inplace_tl = atoi(e) == 2 || atoi(e) == 4 ? atoi(e) : 0;
 	c->d_inplace = nullptr;
 	c->inplace_cap = 0;
 	c->inplace_done = nullptr;
@@ -645,7 +666,8 @@ extern "C" void xcsum_ctx_destroy(xcsum_ctx *c)
 	resident_free(c);
 	free_staging(c);
 	for (auto &r : c->regions) {
-		(void)hipHostUnregister(r.reg);
+		if (r.mapped)
+			(void)hipHostUnregister(r.reg);
 		reg_trace("unregister", r.host, r.size, r.dev, 0);
 	}
 	if (c->d_err)
@@ -861,6 +883,10 @@ extern "C" int xcsum_batch_device(xcsum_ctx *c, uint8_t *d_umem, const struct xc
 		const int rc = inplace_two_pass(c, a, g, (hipStream_t)stream, &done);
 		if (rc || done)
 			return rc;
+	}
+	if ((a.flags & XCSUM_F_INPLACE) && c->inplace_tl && g.G == 16 && g.U == 2 && g.K == 6) {
+		HIPCHK(launch_csum_tl(a, g, c->inplace_tl, c->cus, (hipStream_t)stream));
+		return 0;
 	}
 	HIPCHK(launch_csum(a, g, c->cus, (hipStream_t)stream));
 	return 0;
@@ -1085,6 +1111,50 @@ static void reg_trace(const char *what, const void *base, size_t size, const voi
 	}
 }
 
+/* Can the kernel move the pages of [lo, hi) under a GPU mapping?  The
+ * registered-memory faults of rounds 2-4 all hit memory
+ * eligible for transparent huge pages (numpy's heap, madvise(MADV_HUGEPAGE)
+ * by numpy for arrays of 4 MiB and up: VmFlags "hg"); none hit libxudp's
+ * UMEM mapping (anon_map, MAP_LOCKED | MAP_POPULATE, not THP-eligible under
+ * THP "madvise"), and the same suite ran clean with THP disabled for the
+ * process.  Eligible: a VMA of the range flagged "hg", or THP "always" and
+ * not "nh", unless THP is disabled for the process (PR_GET_THP_DISABLE). */
+static bool thp_eligible(uintptr_t lo, uintptr_t hi)
+{
+	if (prctl(PR_GET_THP_DISABLE, 0, 0, 0, 0) == 1)
+		return false;
+	bool always = false;
+	if (FILE *f = fopen("/sys/kernel/mm/transparent_hugepage/enabled", "r")) {
+		char buf[128] = {0};
+		const bool got = fgets(buf, sizeof buf, f) != nullptr;
+		fclose(f);
+		if (got && strstr(buf, "[never]"))
+			return false;
+		always = got && strstr(buf, "[always]") != nullptr;
+	}
+	FILE *f = fopen("/proc/self/smaps", "r");
+	if (!f)
+		return true;   /* cannot tell: assume the worst */
+	char line[512];
+	uintptr_t s = 0, e = 0;
+	bool eligible = false;
+	while (fgets(line, sizeof line, f)) {
+		unsigned long a, b;
+		if (sscanf(line, "%lx-%lx ", &a, &b) == 2 && strchr(line, '-') < strchr(line, ' ')) {
+			s = a;
+			e = b;
+			continue;
+		}
+		if (strncmp(line, "VmFlags:", 8) == 0 && s < hi && e > lo) {
+			const bool hg = strstr(line, " hg") != nullptr;
+			const bool nh = strstr(line, " nh") != nullptr;
+			eligible |= hg || (always && !nh);
+		}
+	}
+	fclose(f);
+	return eligible;
+}
+
 extern "C" int xcsum_register_umem(xcsum_ctx *c, void *base, size_t size)
 {
 	void *dev = nullptr;
@@ -1097,6 +1167,15 @@ extern "C" int xcsum_register_umem(xcsum_ctx *c, void *base, size_t size)
 	const bool known = hipPointerGetAttributes(&pa, base) == hipSuccess &&
 			   pa.type != hipMemoryTypeUnregistered;
 	(void)hipGetLastError();
+	const uintptr_t plo = (uintptr_t)base & ~(uintptr_t)4095;
+	const uintptr_t phi = ((uintptr_t)base + size + 4095) & ~(uintptr_t)4095;
+	const char *force = getenv("XCSUM_REG_ALLOW_THP");   /* diagnostic */
+	if (!(force && strcmp(force, "1") == 0) && thp_eligible(plo, phi)) {
+		/* kept for bookkeeping, never mapped: batches in it are staged */
+		reg_trace("register_staged", base, size, nullptr, known);
+		c->regions.push_back(Region{(uint8_t *)base, size, nullptr, nullptr, false});
+		return 0;
+	}
 	if (hipHostRegister(base, size, hipHostRegisterMapped) != hipSuccess)
 		return -XCSUM_ERR_HIP;
 	if (hipHostGetDevicePointer(&dev, base, 0) != hipSuccess) {
@@ -1104,8 +1183,18 @@ extern "C" int xcsum_register_umem(xcsum_ctx *c, void *base, size_t size)
 		return -XCSUM_ERR_HIP;
 	}
 	reg_trace("register", base, size, dev, known);
-	c->regions.push_back(Region{(uint8_t *)base, size, (uint8_t *)dev, (uint8_t *)base});
+	c->regions.push_back(Region{(uint8_t *)base, size, (uint8_t *)dev, (uint8_t *)base, true});
 	return 0;
+}
+
+extern "C" int xcsum_umem_mapped(xcsum_ctx *c, const void *base)
+{
+	if (!c || !base)
+		return -XCSUM_ERR_INVAL;
+	for (auto &r : c->regions)
+		if (r.host == (const uint8_t *)base)
+			return r.mapped ? 1 : 0;
+	return -XCSUM_ERR_NOT_REGISTERED;
 }
 
 extern "C" int xcsum_unregister_umem(xcsum_ctx *c, void *base)
@@ -1121,7 +1210,8 @@ extern "C" int xcsum_unregister_umem(xcsum_ctx *c, void *base)
 			 * points ran on (the region's device alias may have been
 			 * handed to them) */
 			(void)drain_ctx(c);
-			(void)hipHostUnregister(c->regions[i].reg);
+			if (c->regions[i].mapped)
+				(void)hipHostUnregister(c->regions[i].reg);
 			reg_trace("unregister", base, c->regions[i].size, c->regions[i].dev, 0);
 			c->regions.erase(c->regions.begin() + i);
 			return 0;
@@ -1130,12 +1220,22 @@ extern "C" int xcsum_unregister_umem(xcsum_ctx *c, void *base)
 	return -XCSUM_ERR_NOT_REGISTERED;
 }
 
+/* the GPU-mapped registered region holding [lo, hi), or null */
 static const Region *find_region(const xcsum_ctx *c, const uint8_t *lo, const uint8_t *hi)
 {
 	for (auto &r : c->regions)
-		if (lo >= r.host && hi <= r.host + r.size)
+		if (r.mapped && lo >= r.host && hi <= r.host + r.size)
 			return &r;
 	return nullptr;
+}
+
+/* any registered region holding [lo, hi), mapped or staged */
+static bool in_any_region(const xcsum_ctx *c, const uint8_t *lo, const uint8_t *hi)
+{
+	for (auto &r : c->regions)
+		if (lo >= r.host && hi <= r.host + r.size)
+			return true;
+	return false;
 }
 
 /* ---- host-resident batches ----------------------------------------------- */
@@ -1514,7 +1614,8 @@ static int batch_host_run(xcsum_ctx *c, uint8_t *h_umem, const struct xcsum_desc
 			if (h_desc[i].addr + h_desc[i].len > hi) hi = h_desc[i].addr + h_desc[i].len;
 		}
 		zc = find_region(c, h_umem + lo, h_umem + hi);
-		if (!zc)
+		/* a registered region the GPU does not map is staged instead */
+		if (!zc && !in_any_region(c, h_umem + lo, h_umem + hi))
 			return -XCSUM_ERR_NOT_REGISTERED;
 	} else {
 		zc = zerocopy_pays(c, h_umem, h_desc, n);
@@ -1594,6 +1695,10 @@ static int batch_host_run(xcsum_ctx *c, uint8_t *h_umem, const struct xcsum_desc
 			a.bias = 0;
 			a.flags = flags & (XCSUM_F_INPLACE | XCSUM_F_IPHDR | XCSUM_F_V4_RFC |
 					   XCSUM_F_VERIFY);
+#ifdef XCSUM_DEBUG_BOUNDS
+			a.reg_lo = (uint64_t)(uintptr_t)zc->dev;
+			a.reg_hi = a.reg_lo + zc->size;
+#endif
 		} else if (gather) {
 			/* each frame copied on its own into the pinned stage, then
 			 * one DMA of the packed bytes and one of their descriptors */
@@ -1759,7 +1864,9 @@ static int rx_host_run(xcsum_ctx *c, const uint8_t *h_umem, const struct xcsum_d
 	const Region *zc = nullptr;
 	if (flags & XCSUM_F_ZEROCOPY) {
 		zc = find_region(c, h_umem + blo, h_umem + bhi);
-		if (!zc || ((uintptr_t)zc->dev & 3u) != ((uintptr_t)zc->host & 3u))
+		if (!zc && !in_any_region(c, h_umem + blo, h_umem + bhi))
+			return -XCSUM_ERR_NOT_REGISTERED;
+		if (zc && ((uintptr_t)zc->dev & 3u) != ((uintptr_t)zc->host & 3u))
 			return -XCSUM_ERR_NOT_REGISTERED;
 	} else {
 		zc = zerocopy_pays(c, h_umem, h_desc, n);

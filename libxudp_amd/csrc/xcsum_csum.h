@@ -100,6 +100,14 @@ static __device__ __forceinline__ Frame resolve(const A &a, u32x4 d, bool presen
 #ifdef XCSUM_DEBUG_BOUNDS
 	f.lim = (const uint8_t *)(((uintptr_t)f.eth + len + 15u) & ~(uintptr_t)15);
 	f.dlen = len;
+	/* a zero-copy frame must lie in its registered region, 16-byte blocks
+	 * included: else it is not read at all */
+	if constexpr (!A::kChecked) {
+		if (present && a.reg_hi &&
+		    !XB_IN((uintptr_t)f.eth & ~(uintptr_t)15, (uintptr_t)f.lim - ((uintptr_t)f.eth & ~(uintptr_t)15),
+			   a.reg_lo, a.reg_hi, XB_CSUM_REGION, addr))
+			present = false;
+	}
 #endif
 	if (present && mode == XCSUM_MODE_AUTO) {
 		/* h_proto only inside the frame: a descriptor shorter than the
@@ -156,7 +164,11 @@ static __device__ __forceinline__ Frame resolve(const A &a, u32x4 d, bool presen
 			w = (const uint32_t *)g_zero_chunk;
 #pragma unroll
 		for (int j = 0; j < 6; j++)
+#ifdef XCSUM_IH_NT   /* A/B (make variant): the header dwords nontemporal */
+			f.ih[j] = __builtin_nontemporal_load(w + j);
+#else
 			f.ih[j] = w[j];
+#endif
 	}
 	return f;
 }
@@ -371,7 +383,7 @@ static __device__ __forceinline__ void consume_any(const A &a, const Frame (&fc)
  * at the loop latch, that copy needs the next step's loads to have landed,
  * and the ISA showed a vmcnt(0) there -- one step in flight, not two.
  */
-template <int G, int U, int K, bool ORD, int FEAT, class A>
+template <int G, int U, int K, bool ORD, int FEAT, class A, int TL = 0>
 static __device__ __forceinline__ void csum_loop(const A &a)
 {
 	const uint32_t lane = threadIdx.x & (G - 1);
@@ -401,7 +413,7 @@ static __device__ __forceinline__ void csum_loop(const A &a)
 	 * vmcnt queue with: the next wait for the descriptors then leaves all
 	 * chunk loads in flight */
 	__builtin_amdgcn_sched_barrier(0);
-	issue<G, U, K>(fa, lane, va);
+	issue<G, U, K, TL>(fa, lane, va);
 
 	Frame fb[U];
 	u32x4 vb[U][K];
@@ -413,7 +425,7 @@ static __device__ __forceinline__ void csum_loop(const A &a)
 		for (int u = 0; u < U; u++)
 			d[u] = load_desc<G == 64>(a, fidx<ORD>(a, p0 + 2 * step + u * nseg));
 		__builtin_amdgcn_sched_barrier(0);
-		issue<G, U, K>(fb, lane, vb);
+		issue<G, U, K, TL>(fb, lane, vb);
 		consume_any<G, U, K, ORD, FEAT, A>(a, fa, va, lane, p0, nseg);
 
 #pragma unroll
@@ -424,7 +436,7 @@ static __device__ __forceinline__ void csum_loop(const A &a)
 		for (int u = 0; u < U; u++)
 			d[u] = load_desc<G == 64>(a, fidx<ORD>(a, p0 + 3 * step + u * nseg));
 		__builtin_amdgcn_sched_barrier(0);
-		issue<G, U, K>(fa, lane, va);
+		issue<G, U, K, TL>(fa, lane, va);
 		consume_any<G, U, K, ORD, FEAT, A>(a, fb, vb, lane, p0 + step, nseg);
 	}
 }
@@ -432,14 +444,14 @@ static __device__ __forceinline__ void csum_loop(const A &a)
 /* The identity order gets its own copy of the loop, so descriptor-order
  * batches pay nothing for the region order; which copy runs is decided once
  * per launch (uniform branch, after resolve_order). */
-template <int G, int U, int K, int FEAT>
+template <int G, int U, int K, int FEAT, int TL = 0>
 static __device__ __forceinline__ void csum_body(CsumArgs &a)
 {
 	resolve_order(a);
 	if (a.ord.rshift == 0)
-		csum_loop<G, U, K, false, FEAT>(a);
+		csum_loop<G, U, K, false, FEAT, CsumArgs, TL>(a);
 	else
-		csum_loop<G, U, K, true, FEAT>(a);
+		csum_loop<G, U, K, true, FEAT, CsumArgs, TL>(a);
 }
 
 template <int G, int U, int K, int FEAT>

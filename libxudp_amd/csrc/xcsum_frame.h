@@ -262,7 +262,11 @@ static __device__ __forceinline__ void store_u16(uint8_t *p, uint16_t v)
 	}
 }
 
-template <int G, int U, int K>
+/* TL > 0 (in-place A/B, xcsum_csum_tl.hip): a frame's first TL chunks -- the
+ * ones holding udp->check -- are loaded temporally (allocated in the caches),
+ * the rest nontemporally, so the in-place store that follows may find its
+ * line still cached */
+template <int G, int U, int K, int TL = 0>
 static __device__ __forceinline__ void issue(const Frame (&f)[U], uint32_t lane,
 					     u32x4 (&v)[U][K])
 {
@@ -272,9 +276,13 @@ static __device__ __forceinline__ void issue(const Frame (&f)[U], uint32_t lane,
 #pragma unroll
 		for (int k = 0; k < K; k++) {
 			uint32_t c = lane + k * G;
-			v[u][k] = load_chunk(c < f[u].nchunks ? XB_LOAD(f[u].base + 16u * c, 16, f[u].eth,
-									f[u].lim, XB_CSUM_CHUNK, c, zero)
-							      : zero);
+			const uint8_t *q = c < f[u].nchunks ? XB_LOAD(f[u].base + 16u * c, 16, f[u].eth,
+								      f[u].lim, XB_CSUM_CHUNK, c, zero)
+							    : zero;
+			if (TL > 0 && k == 0 && c < (uint32_t)TL)
+				v[u][k] = *((gu32x4 *)q);
+			else
+				v[u][k] = load_chunk(q);
 		}
 }
 

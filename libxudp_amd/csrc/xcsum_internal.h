@@ -73,6 +73,9 @@ enum BoundsSite : uint32_t {
 	XB_RX_STREAM,           /* receive stream kernel: region load */
 	XB_GEN_STORE,           /* synthetic fill: store vs the frame */
 	XB_SCATTER,             /* two-pass in-place: h_proto load / field store */
+	XB_CSUM_REGION,         /* zero-copy: frame vs the registered region's extent */
+	XB_RES_REQ,             /* resident request: umem / desc / out pointers vs
+				   the context's stage, doorbell and result slot */
 	XB_SITE_COUNT
 };
 
@@ -113,6 +116,11 @@ struct CsumArgs {
 	 * batch); an argument type with kChecked (xcsum_resident.hip) checks
 	 * each one before any load of its frame (desc_ok / desc_bad) */
 	static constexpr bool kChecked = false;
+#ifdef XCSUM_DEBUG_BOUNDS
+	/* zero-copy launches: the registered region's device extent, every
+	 * frame checked against it before any load (0, 0: unchecked) */
+	uint64_t reg_lo = 0, reg_hi = 0;
+#endif
 };
 
 /* Second pass of the two-pass in-place schedule (xcsum_scatter.hip): store
@@ -193,6 +201,9 @@ hipError_t launch_csum(const CsumArgs &a, Geometry g, int cus, hipStream_t s);
 hipError_t launch_csum_f0(const CsumArgs &a, Geometry g, int cus, hipStream_t s);
 hipError_t launch_csum_f1(const CsumArgs &a, Geometry g, int cus, hipStream_t s);
 hipError_t launch_csum_f2(const CsumArgs &a, Geometry g, int cus, hipStream_t s);
+/* in-place A/B: the (16,2,6) kernel with temporal loads of each frame's
+ * first tl (2 or 4) chunks (xcsum_csum_tl.hip) */
+hipError_t launch_csum_tl(const CsumArgs &a, Geometry g, int tl, int cus, hipStream_t s);
 hipError_t launch_gen(uint8_t *d_umem, const struct xcsum_desc *d_desc, uint32_t n,
 		      uint32_t family, uint64_t seed, uint64_t first_index, int max_blocks,
 		      hipStream_t s);
@@ -200,8 +211,11 @@ hipError_t launch_gen(uint8_t *d_umem, const struct xcsum_desc *d_desc, uint32_t
 struct Region {
 	uint8_t *host;
 	size_t size;
-	uint8_t *dev;  /* device alias of the page-locked mapping */
-	uint8_t *reg;  /* the address handed to hipHostRegister (host, or its page) */
+	uint8_t *dev;  /* device alias of the page-locked mapping (null: staged) */
+	uint8_t *reg;  /* the address handed to hipHostRegister */
+	bool mapped;   /* false: registered for bookkeeping only -- its pages may
+			  be moved by transparent huge pages, so
+			  the GPU never touches it; batches in it are staged */
 };
 
 /* Per-thread context.  Owns only scratch: the error counter and the staging
@@ -219,6 +233,8 @@ struct Ctx {
 	 * the first pass writes, 2 x u16 per frame, grown on demand */
 	int inplace_sched;
 	uint32_t inplace_block;        /* second-pass store width (ScatterArgs) */
+	int inplace_tl;                /* XCSUM_INPLACE_TL: fused in-place with the
+					  first chunks loaded temporally (A/B) */
 	uint16_t *d_inplace;
 	uint32_t inplace_cap;          /* frames */
 	hipEvent_t inplace_done;       /* after the last two-pass call's scatter */

@@ -36,10 +36,18 @@ constexpr int RB_INL_ECHO = 12;
 /* The doorbell, in pinned coherent host memory the workgroups read over
  * PCIe.  The host writes desc[] (always), the inline lines and req[], then
  * seq; `stop` asks the workgroups to leave.  Sequence numbers skip 0. */
+/* words 2..13 of the doorbell: the context's stage, doorbell descriptor
+ * array and result slot as (lo, hi) device-address pairs, which the
+ * bounds-checked build checks every request's pointers against (RB_ALLOW_*
+ * are u64 indices into allow[]) */
+enum { RB_ALLOW_STAGE = 0, RB_ALLOW_DESC = 2, RB_ALLOW_OUT = 4, RB_ALLOW_N = 6 };
+
 struct alignas(64) ResidentBell {
 	uint32_t seq;                  /* words 0-63 are read by one load per poll */
 	uint32_t stop;
-	uint32_t pad0[14];
+	uint64_t allow[RB_ALLOW_N];    /* words 2-13 (written by the host, read with
+					  every poll; only the debug build uses them) */
+	uint32_t pad0[2];
 	uint32_t req[16];              /* word 16 on */
 	uint32_t inl[2][16];           /* word 32 on: descriptors 0-2, 3-5 */
 	struct xcsum_desc desc[RB_DESC_CAP];
@@ -56,6 +64,11 @@ constexpr int RB_LEFT = 1;
  * [3] = frame index, [4..5] = desc.addr, [6] = desc.len (a bad request never
  * faults the GPU) */
 constexpr int RB_BAD = 2;
+/* the bounds-checked build's breadcrumb: before serving request seq a
+ * workgroup stores [8] = seq, [9..10] = umem, [11] = n, [12..13] = desc, so
+ * a fault names what the workgroups were reading (pinned host memory
+ * survives the fault) */
+constexpr int RB_CRUMB = 8;
 struct alignas(64) ResidentDone {
 	uint32_t done[RB_MAX_WG * RB_DONE_STRIDE];
 };

@@ -96,6 +96,9 @@ __global__ void __launch_bounds__(256) resident_kernel(const ResidentBell *bell,
 	__shared__ uint32_t first_bad_lds;   /* ResidentArgs::first_bad */
 	__shared__ uint32_t inl_lds[4 * RB_INLINE];   /* ResidentArgs::inl */
 	__shared__ uint32_t inl_on;
+#ifdef XCSUM_DEBUG_BOUNDS
+	__shared__ uint32_t allow_lds[2 * RB_ALLOW_N];
+#endif
 	const uint32_t lane = threadIdx.x & 63;
 	uint32_t served = served0;
 	if (blockIdx.x < 64 && ((skip_mask >> blockIdx.x) & 1ull))
@@ -145,6 +148,10 @@ __global__ void __launch_bounds__(256) resident_kernel(const ResidentBell *bell,
 				__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
 			if (lane >= 16 && lane < 16 + RB_REQ_WORDS)
 				cmd[1 + lane - 16] = v;
+#ifdef XCSUM_DEBUG_BOUNDS
+			if (lane >= 2 && lane < 2 + 2 * RB_ALLOW_N)
+				allow_lds[lane - 2] = v;
+#endif
 			if (lane >= 32 && (lane & 15) < RB_INL_ECHO)   /* 3 descriptors a line */
 				inl_lds[(lane >> 4 == 3 ? 12 : 0) + (lane & 15)] = v;
 			if (lane == 0) {
@@ -188,6 +195,39 @@ __global__ void __launch_bounds__(256) resident_kernel(const ResidentBell *bell,
 		a.limit = u64_of(r[RB_LIMIT], r[RB_LIMIT + 1]);
 		a.first_bad = &first_bad_lds;
 		a.inl = __builtin_amdgcn_readfirstlane(inl_on) ? inl_lds : nullptr;
+#ifdef XCSUM_DEBUG_BOUNDS
+		{
+			/* the request's pointers against the context's own buffers:
+			 * frames [umem, umem + limit) in the stage, n descriptors in
+			 * the doorbell (unless inline), n (2n with IPHDR) results in
+			 * the result slot; a request outside them is not served */
+			auto al = [&](int k) {
+				return u64_of(allow_lds[2 * k], allow_lds[2 * k + 1]);
+			};
+			const uint64_t um = (uint64_t)(uintptr_t)a.umem;
+			const uint64_t ds = (uint64_t)(uintptr_t)a.desc;
+			const uint64_t ot = (uint64_t)(uintptr_t)a.out;
+			const uint64_t oi = (uint64_t)(uintptr_t)a.out_ip;
+			bool ok = xb_in(um, a.limit, al(RB_ALLOW_STAGE), al(RB_ALLOW_STAGE + 1), XB_RES_REQ,
+					s);
+			ok = ok && (a.inl || xb_in(ds, 16ull * a.n, al(RB_ALLOW_DESC), al(RB_ALLOW_DESC + 1),
+						   XB_RES_REQ, s));
+			ok = ok && xb_in(ot, 2ull * a.n, al(RB_ALLOW_OUT), al(RB_ALLOW_OUT + 1), XB_RES_REQ, s);
+			ok = ok && (!oi || xb_in(oi, 2ull * a.n, al(RB_ALLOW_OUT), al(RB_ALLOW_OUT + 1),
+						 XB_RES_REQ, s));
+			if (!ok)
+				a.n = 0;
+			if (threadIdx.x == 0) {
+				uint32_t *cr = &done->done[RB_DONE_STRIDE * blockIdx.x + RB_CRUMB];
+				cr[1] = (uint32_t)um;
+				cr[2] = (uint32_t)(um >> 32);
+				cr[3] = a.n;
+				cr[4] = (uint32_t)ds;
+				cr[5] = (uint32_t)(ds >> 32);
+				__hip_atomic_store(&cr[0], s, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+			}
+		}
+#endif
 		csum_loop<G, U, K, false, 2>(a);
 		/* a descriptor outside the request's bounds: its frame was not
 		 * read; report the workgroup's first (the host fails the call) */

@@ -113,7 +113,7 @@ extern "C" int xudp_packet_udp_batch(xcsum_ctx *ctx, struct packet_info *infos, 
 	 * one (pinned DMA / zero-copy), else relative to address 0 */
 	uint8_t *base = nullptr;
 	for (auto &r : ctx->regions)
-		if (lo >= r.host && hi <= r.host + r.size)
+		if (r.mapped && lo >= r.host && hi <= r.host + r.size)
 			base = r.host;
 	/* IPv4 without XCSUM_F_V4_RFC: udp->check stays 0 (packet.c:125) and
 	 * only iph->check is computed, from the 20-byte header (its tot_len

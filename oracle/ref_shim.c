@@ -209,3 +209,59 @@ int ref_packet_parse(const uint8_t *pkt, uint32_t len, int *family, uint32_t *l3
 	}
 	return r;
 }
+
+/* The reference's own per-frame TX work, timed: xudp_packet_udp()
+ * (packet.c:156-194: headers, then xudp_checksum_half for IPv4 or udp_csum6
+ * for IPv6) on n frames whose payload already sits at its data offset in
+ * xudp's 4096-byte slots (data at F + 384, tx.c:31-53) -- what
+ * xudp_frame_send does per frame (tx.c:696-726) -- repeated reps times on
+ * one thread.  Returns seconds.  For the crossover of DESIGN.md 5.10. */
+double ref_packet_udp_timed(uint8_t *umem, uint32_t n, int family, int payload_size, int reps)
+{
+	struct packet_info info;
+	struct sockaddr_in from4, to4;
+	struct sockaddr_in6 from6, to6;
+	unsigned char smac[6] = {2, 0, 0, 0, 0, 1}, dmac[6] = {2, 0, 0, 0, 0, 2};
+	struct timespec t0, t1;
+	uint32_t i;
+	int r;
+
+	memset(&from4, 0, sizeof(from4));
+	memset(&to4, 0, sizeof(to4));
+	memset(&from6, 0, sizeof(from6));
+	memset(&to6, 0, sizeof(to6));
+	from4.sin_family = to4.sin_family = AF_INET;
+	from4.sin_addr.s_addr = htonl(0x0a002302);
+	to4.sin_addr.s_addr = htonl(0x0a002301);
+	from4.sin_port = htons(3486);
+	to4.sin_port = htons(40000);
+	from6.sin6_family = to6.sin6_family = AF_INET6;
+	from6.sin6_addr.s6_addr[0] = 0x10;
+	from6.sin6_addr.s6_addr[15] = 2;
+	to6.sin6_addr.s6_addr[0] = 0x10;
+	to6.sin6_addr.s6_addr[15] = 1;
+	from6.sin6_port = htons(3487);
+	to6.sin6_port = htons(40000);
+	clock_gettime(CLOCK_MONOTONIC, &t0);
+	for (r = 0; r < reps; r++)
+		for (i = 0; i < n; i++) {
+			memset(&info, 0, sizeof(info));
+			info.family = family == 6 ? AF_INET6 : AF_INET;
+			info.smac = smac;
+			info.dmac = dmac;
+			if (family == 6) {
+				info.from6 = &from6;
+				info.to6 = &to6;
+			} else {
+				info.from = &from4;
+				info.to = &to4;
+			}
+			info.head = (char *)umem + (uint64_t)i * 4096 + 320;
+			info.data = info.head + 64;
+			info.payload = info.data;
+			info.payload_size = payload_size;
+			xudp_packet_udp(&info);
+		}
+	clock_gettime(CLOCK_MONOTONIC, &t1);
+	return (t1.tv_sec - t0.tv_sec) + 1e-9 * (t1.tv_nsec - t0.tv_nsec);
+}

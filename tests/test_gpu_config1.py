@@ -31,6 +31,7 @@ def test_config1_batch_host_digest(engine, config1, how):
     umem = umem.copy()
     flags = X.F_ZEROCOPY if how == "zerocopy" else 0
     if how != "staged":
+        umem = X.as_umem(umem)   # libxudp's UMEM mapping
         engine.register_umem(umem)
     try:
         for mode, key in ((X.MODE_V4_LEGACY, "sha256_out"), (X.MODE_V4_RFC, "sha256_out_v4_rfc")):
@@ -65,6 +66,7 @@ def test_config1_packet_udp_batch_digest(engine, config1, where):
     d, umem, desc = config1
     slots = np.zeros(4096 * len(desc), dtype=np.uint8) if where != "own_buffers" else None
     if where == "umem_registered":
+        slots = X.as_umem(slots)   # libxudp's UMEM mapping
         engine.register_umem(slots)
     try:
         # packet.c semantics: udp->check = 0 (packet.c:125), iph->check computed

@@ -137,6 +137,7 @@ def host_fuzz_case(torch_cuda, engine, seed):
     host = umem.copy()
     out = np.full(len(desc), 0x5a5a, dtype=np.uint16)
     if zerocopy:
+        host = X.as_umem(host)   # libxudp's UMEM mapping
         engine.register_umem(host)
     try:
         engine.batch_host(host, desc, out, mode, flags | (X.F_ZEROCOPY if zerocopy else 0))

@@ -1,6 +1,7 @@
 """GPU: host-resident batches (frames in a UMEM-like host buffer) and the
 packet.c-level mirror, through the C ABI, against the reference fixtures and
 the oracle."""
+import os
 import socket
 
 import numpy as np
@@ -48,6 +49,7 @@ def test_host_batch_inplace(engine, golden, how):
     desc = golden_desc(golden)
     flags = X.F_INPLACE | X.F_IPHDR
     if how != "pageable":
+        umem = X.as_umem(umem)   # libxudp's UMEM mapping
         engine.register_umem(umem)
     if how == "zerocopy":
         flags |= X.F_ZEROCOPY
@@ -75,6 +77,7 @@ def test_host_batch_many_chunks(engine, shuffle):
         desc = desc[np.random.default_rng(0).permutation(len(desc))]
     exp = oracle.batch(umem, desc, X.MODE_V4_LEGACY)
     assert np.array_equal(host_batch(engine, umem, desc, X.MODE_V4_LEGACY), exp)
+    umem = X.as_umem(umem)   # libxudp's UMEM mapping
     engine.register_umem(umem)
     try:
         assert np.array_equal(host_batch(engine, umem, desc, X.MODE_V4_LEGACY), exp)
@@ -106,6 +109,7 @@ def test_host_batch_small_frames_in_slots(engine, n, fam, register):
     flags = X.F_INPLACE | (X.F_IPHDR if fam == 4 else 0)
     before = umem.copy()
     if register:
+        umem = X.as_umem(umem)   # libxudp's UMEM mapping
         engine.register_umem(umem)
     try:
         assert np.array_equal(host_batch(engine, umem, desc, mode), exp)
@@ -182,6 +186,7 @@ def test_packet_udp_batch_random(engine, register):
         umem[4096 * i + 320 + 64:4096 * i + 320 + 64 + L] = pa.payload[:L]
         pas.append(pa)
     if register:
+        umem = X.as_umem(umem)   # libxudp's UMEM mapping
         engine.register_umem(umem)
     try:
         X.packet_udp_batch(engine, pas)
@@ -279,10 +284,11 @@ def test_inplace_skips_truncated_frame(torch_cuda, engine, how):
     if how == "device":
         got, after = run_device(torch_cuda, engine, big, d, X.MODE_V4_RFC, X.F_INPLACE)
     else:
-        after = big
         flags = X.F_INPLACE
         if how != "pageable":
+            big = X.as_umem(big)   # libxudp's UMEM mapping
             engine.register_umem(big)
+        after = big
         if how == "zerocopy":
             flags |= X.F_ZEROCOPY
         try:
@@ -295,3 +301,52 @@ def test_inplace_skips_truncated_frame(torch_cuda, engine, how):
     changed = set(np.nonzero(after != before)[0].tolist())
     own = {int(a) + k for a in d["addr"][1:] for k in (40, 41)}
     assert changed <= own            # only the valid frames' own udp->check fields
+
+
+def _thp_staging_expected():
+    """xcsum_register_umem stages THP-eligible memory unless THP is off for
+    the system ([never]) or for this process (XCSUM_TEST_NO_THP)."""
+    if os.environ.get("XCSUM_TEST_NO_THP"):
+        return False
+    try:
+        return "[never]" not in open("/sys/kernel/mm/transparent_hugepage/enabled").read()
+    except OSError:
+        return True
+
+
+def test_thp_eligible_memory_is_staged(engine):
+    """every registered-memory GPU fault was on memory eligible
+    for transparent huge pages.  A numpy array of >= 4 MiB (numpy marks it
+    MADV_HUGEPAGE) is registered for bookkeeping only (xcsum_umem_mapped
+    0) and staged -- with XCSUM_F_ZEROCOPY too -- while the same frames in a
+    libxudp-style mapping (umem_buffer) are GPU-mapped; every transport gives
+    the oracle's results and in-place bytes."""
+    umem, desc = X.gen_frames_host(4000, 4, 1472, seed=81, align=8)
+    assert umem.nbytes >= 4 << 20
+    exp = oracle.batch(umem, desc, X.MODE_V4_RFC)
+    for buf, mapped in ((umem.copy(), 0 if _thp_staging_expected() else 1),
+                        (X.as_umem(umem), 1)):
+        engine.register_umem(buf)
+        try:
+            assert engine.umem_mapped(buf) == mapped
+            a = desc["addr"].astype(np.int64)
+            for flags in (0, X.F_ZEROCOPY, X.F_INPLACE | X.F_IPHDR,
+                          X.F_ZEROCOPY | X.F_INPLACE | X.F_IPHDR):
+                buf[a[:, None] + np.array([24, 25, 40, 41])] = 0   # as packet.c leaves them
+                got = host_batch(engine, buf, desc, X.MODE_V4_RFC, flags)
+                assert np.array_equal(got, exp), (mapped, flags)
+            check_inplace_frames(buf, desc, exp)
+        finally:
+            engine.unregister_umem(buf)
+    with pytest.raises(X.XcsumError):
+        engine.umem_mapped(umem)
+
+
+def check_inplace_frames(buf, desc, exp):
+    a = desc["addr"].astype(np.int64)
+    assert np.array_equal(buf[a[:, None] + np.array([40, 41])].copy().view("<u2").ravel(), exp)
+    for i in range(0, len(desc), 397):
+        f = buf[int(a[i]):int(a[i]) + int(desc["len"][i])].copy()
+        ip = int(f[24:26].view("<u2")[0])
+        f[24:26] = 0
+        assert ip == oracle.ip_header_rfc(f)

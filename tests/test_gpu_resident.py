@@ -36,6 +36,7 @@ def test_resident_golden(res_engine, golden, mode, col, fam, register):
     sel = np.nonzero(golden["family"] == fam)[0]
     umem = golden["umem"].copy()
     if register:
+        umem = X.as_umem(umem)   # libxudp's UMEM mapping
         res_engine.register_umem(umem)
     try:
         for lo in range(0, len(sel), 300):       # batches the resident path takes
@@ -53,6 +54,7 @@ def test_resident_inplace(res_engine, golden, how):
     desc = golden_desc(golden)
     flags = X.F_INPLACE | X.F_IPHDR
     if how != "pageable":
+        umem = X.as_umem(umem)   # libxudp's UMEM mapping
         res_engine.register_umem(umem)
     if how == "zerocopy":
         flags |= X.F_ZEROCOPY
@@ -92,6 +94,7 @@ def test_resident_slots(res_engine, fam, register):
     mode = X.MODE_V6 if fam == 6 else X.MODE_V4_RFC
     exp = oracle.batch(umem, desc, mode)
     if register:
+        umem = X.as_umem(umem)   # libxudp's UMEM mapping
         res_engine.register_umem(umem)
     try:
         assert np.array_equal(host_batch(res_engine, umem, desc, mode), exp)
@@ -114,6 +117,7 @@ def test_resident_sizes(res_engine, n):
     umem, desc = X.gen_frames_host(n, 4, 0, 1472, seed=n, align=8)
     exp = oracle.batch(umem, desc, X.MODE_V4_LEGACY)
     assert np.array_equal(host_batch(res_engine, umem, desc, X.MODE_V4_LEGACY), exp)
+    umem = X.as_umem(umem)   # libxudp's UMEM mapping
     res_engine.register_umem(umem)
     try:
         assert np.array_equal(host_batch(res_engine, umem, desc, X.MODE_V4_LEGACY), exp)
@@ -126,6 +130,7 @@ def test_resident_fresh_bytes_every_call(res_engine):
     """The same registered UMEM rewritten between calls: every call must read
     the new bytes (the workgroups' acquire drops cached lines)."""
     umem, desc = X.gen_frames_host(100, 6, 0, 1400, seed=5, stride=4096, offset=322)
+    umem = X.as_umem(umem)   # libxudp's UMEM mapping
     res_engine.register_umem(umem)
     rng = np.random.default_rng(1)
     a = desc["addr"].astype(np.int64)
@@ -144,6 +149,7 @@ def test_resident_fresh_descriptors_every_call(res_engine):
     """A different batch every call (size, frames, order) from one registered
     UMEM: the descriptors the host wrote into the doorbell are the ones read."""
     umem, desc = X.gen_frames_host(2000, 4, 0, 1472, seed=12, stride=2048, offset=64)
+    umem = X.as_umem(umem)   # libxudp's UMEM mapping
     res_engine.register_umem(umem)
     rng = np.random.default_rng(3)
     try:
@@ -177,6 +183,7 @@ def test_resident_large_descriptor_batches(res_engine):
     of descriptors must be the ones just written."""
     umem, desc = X.gen_frames_host(6000, 4, 0, 200, seed=16, stride=512, offset=0)
     exp_all = oracle.batch(umem, desc, X.MODE_V4_RFC)
+    umem = X.as_umem(umem)   # libxudp's UMEM mapping
     res_engine.register_umem(umem)
     rng = np.random.default_rng(6)
     try:
@@ -201,6 +208,7 @@ def test_resident_leave_and_return(idle_us):
     a = desc["addr"].astype(np.int64)
     chk = a[:, None] + np.array([60, 61])
     exp = oracle.batch(umem, desc, X.MODE_V6)
+    umem = X.as_umem(umem)   # libxudp's UMEM mapping
     e.register_umem(umem)
     try:
         for it in range(300):
@@ -282,6 +290,7 @@ def test_resident_inplace_skips_truncated_frame(res_engine, how):
     before = big.copy()
     res_engine.take_errors()
     if how == "registered":
+        big = X.as_umem(big)   # libxudp's UMEM mapping
         res_engine.register_umem(big)
     try:
         got = host_batch(res_engine, big, d, X.MODE_V4_RFC, X.F_INPLACE)
@@ -300,6 +309,7 @@ def test_resident_auto_mixed_families_verify_iphdr(res_engine, golden):
     umem = golden["umem"].copy()
     desc = golden_desc(golden)
     fam = golden["family"]
+    umem = X.as_umem(umem)   # libxudp's UMEM mapping
     res_engine.register_umem(umem)
     try:
         for lo in range(0, len(desc), 400):
@@ -353,6 +363,7 @@ def test_resident_inline_descriptors(res_engine):
     alternating with larger batches that use the descriptor array, so a stale
     inline line would show as a wrong result."""
     umem, desc = X.gen_frames_host(500, 6, 0, 1400, seed=21, stride=2048, offset=64)
+    umem = X.as_umem(umem)   # libxudp's UMEM mapping
     res_engine.register_umem(umem)
     rng = np.random.default_rng(8)
     try:
@@ -397,6 +408,7 @@ def test_resident_peer_busy_teardown_bounded():
         b.set_resident(8)
         umem, desc = X.gen_frames_host(50, 6, 0, 600, seed=62, align=8)
         t0 = time.perf_counter()
+        umem = X.as_umem(umem)   # libxudp's UMEM mapping
         b.register_umem(umem)
         assert np.array_equal(host_batch(b, umem, desc, X.MODE_V6),
                               oracle.batch(umem, desc, X.MODE_V6))

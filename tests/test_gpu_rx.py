@@ -228,6 +228,7 @@ def test_rx_host_vs_oracle(torch_cuda, engine, zerocopy):
     desc["addr"], desc["len"] = offs, lens
     flags_zc = X.F_ZEROCOPY if zerocopy else 0
     if zerocopy:
+        umem = X.as_umem(umem)   # libxudp's UMEM mapping
         engine.register_umem(umem)
     try:
         for flags in FLAGS.values():
@@ -253,6 +254,7 @@ def test_rx_host_sparse_umem_vs_oracle(engine, n, register):
     rng = np.random.default_rng(14)
     umem, desc = umem_chunks(frames, rng, n)
     if register:
+        umem = X.as_umem(umem)   # libxudp's UMEM mapping
         engine.register_umem(umem)
     try:
         for flags in FLAGS.values():

@@ -13,6 +13,8 @@ frames, packed (1520-B stride) or in xudp's 4096-B slots, 1M frames in a
   lib_two_pass    the library's in-place pass, TWO_PASS schedule
   fused_nt        the read with each field stored by the thread that read it
   fused_tl        the same, the chunks holding a field loaded temporally
+  lib_fused_tl2/4 the library's fused pass with each frame's first 2 / 4
+                  chunks loaded temporally (XCSUM_INPLACE_TL)
 Prints one JSON line per layout and family."""
 import argparse
 import ctypes
@@ -98,6 +100,20 @@ def main():
             eng.batch_device(b, d_desc, len(desc), o, mode, flags, 1500, stream=sp)
             return 0
         return f
+    engs_tl = {}
+    for tl in (2, 4):
+        os.environ["XCSUM_INPLACE_TL"] = str(tl)
+        engs_tl[tl] = X.Engine(0)
+    del os.environ["XCSUM_INPLACE_TL"]
+
+    def lib_tl(tl):
+        def f(b):
+            engs_tl[tl].batch_device(b, d_desc, len(desc), None, mode, X.F_INPLACE | iph, 1500,
+                                     stream=sp)
+            return 0
+        return f
+    legs["lib_fused_tl2"] = lib_tl(2)
+    legs["lib_fused_tl4"] = lib_tl(4)
     legs["lib_plain"] = lib(X.INPLACE_AUTO, iph, out)
     legs["lib_fused"] = lib(X.INPLACE_FUSED, X.F_INPLACE | iph, None)
     legs["lib_two_pass"] = lib(X.INPLACE_TWO_PASS, X.F_INPLACE | iph, None)
