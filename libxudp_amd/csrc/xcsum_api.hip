@@ -604,9 +604,9 @@ extern "C" int xcsum_ctx_create(int device, xcsum_ctx **out)
 	c->inplace_block = 32;
 	if (const char *e = getenv("XCSUM_INPLACE_BLOCK"))
 		c->inplace_block = (uint32_t)atoi(e) == 64 ? 64u : (uint32_t)atoi(e) == 32 ? 32u : 0u;
-	c->inplace_tl = 0;
+	c->inplace_tl = 1;
 	if (const char *e = getenv("XCSUM_INPLACE_TL"))
-		c->inplace_tl = atoi(e) == 2 || atoi(e) == 4 ? atoi(e) : 0;
+		c->inplace_tl = atoi(e) != 0;
 	c->d_inplace = nullptr;
 	c->inplace_cap = 0;
 	c->inplace_done = nullptr;
@@ -884,8 +884,11 @@ extern "C" int xcsum_batch_device(xcsum_ctx *c, uint8_t *d_umem, const struct xc
 		if (rc || done)
 			return rc;
 	}
-	if ((a.flags & XCSUM_F_INPLACE) && c->inplace_tl && g.G == 16 && g.U == 2 && g.K == 6) {
-		HIPCHK(launch_csum_tl(a, g, c->inplace_tl, c->cus, (hipStream_t)stream));
+	/* in place without the IPv4 header at MTU: temporal loads of the chunks
+	 * that hold udp->check (xcsum_csum_tl.hip: config 4 -1.5 %) */
+	if ((a.flags & XCSUM_F_INPLACE) && !(a.flags & XCSUM_F_IPHDR) && c->inplace_tl &&
+	    g.G == 16 && g.U == 2 && g.K == 6) {
+		HIPCHK(launch_csum_inplace_tl(a, g, c->cus, (hipStream_t)stream));
 		return 0;
 	}
 	HIPCHK(launch_csum(a, g, c->cus, (hipStream_t)stream));
@@ -1119,19 +1122,32 @@ static void reg_trace(const char *what, const void *base, size_t size, const voi
  * THP "madvise"), and the same suite ran clean with THP disabled for the
  * process.  Eligible: a VMA of the range flagged "hg", or THP "always" and
  * not "nh", unless THP is disabled for the process (PR_GET_THP_DISABLE). */
+/* the bracketed word of a THP sysfs setting ("always", "never", ...) */
+static bool thp_mode_is(const char *path, const char *word)
+{
+	char buf[160] = {0}, want[32];
+	snprintf(want, sizeof want, "[%s]", word);
+	FILE *f = fopen(path, "r");
+	if (!f)
+		return false;
+	const bool got = fgets(buf, sizeof buf, f) != nullptr;
+	fclose(f);
+	return got && strstr(buf, want) != nullptr;
+}
+
 static bool thp_eligible(uintptr_t lo, uintptr_t hi)
 {
 	if (prctl(PR_GET_THP_DISABLE, 0, 0, 0, 0) == 1)
 		return false;
-	bool always = false;
-	if (FILE *f = fopen("/sys/kernel/mm/transparent_hugepage/enabled", "r")) {
-		char buf[128] = {0};
-		const bool got = fgets(buf, sizeof buf, f) != nullptr;
-		fclose(f);
-		if (got && strstr(buf, "[never]"))
-			return false;
-		always = got && strstr(buf, "[always]") != nullptr;
-	}
+	/* private anonymous memory: "enabled"; shared (shmem, anon_map's
+	 * MAP_SHARED | MAP_ANONYMOUS): "shmem_enabled" */
+	const char *en = "/sys/kernel/mm/transparent_hugepage/enabled";
+	const char *sh = "/sys/kernel/mm/transparent_hugepage/shmem_enabled";
+	const bool never = thp_mode_is(en, "never");
+	const bool always = thp_mode_is(en, "always");
+	const bool sh_always = thp_mode_is(sh, "always") || thp_mode_is(sh, "force") ||
+			       thp_mode_is(sh, "within_size");
+	const bool sh_advise = thp_mode_is(sh, "advise");
 	FILE *f = fopen("/proc/self/smaps", "r");
 	if (!f)
 		return true;   /* cannot tell: assume the worst */
@@ -1148,7 +1164,10 @@ static bool thp_eligible(uintptr_t lo, uintptr_t hi)
 		if (strncmp(line, "VmFlags:", 8) == 0 && s < hi && e > lo) {
 			const bool hg = strstr(line, " hg") != nullptr;
 			const bool nh = strstr(line, " nh") != nullptr;
-			eligible |= hg || (always && !nh);
+			if (strstr(line, " sh") != nullptr)
+				eligible |= !nh && (sh_always || (sh_advise && hg));
+			else
+				eligible |= !never && (hg || (always && !nh));
 		}
 	}
 	fclose(f);

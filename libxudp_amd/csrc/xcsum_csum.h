@@ -162,13 +162,13 @@ static __device__ __forceinline__ Frame resolve(const A &a, u32x4 d, bool presen
 		if (ih != (const uint8_t *)g_zero_chunk &&
 		    !XB_IN(w, 24, (uintptr_t)f.eth & ~(uintptr_t)3, f.lim, XB_CSUM_HDR, 14))
 			w = (const uint32_t *)g_zero_chunk;
+		/* plain (temporal) loads: with XCSUM_F_INPLACE the line they bring
+		 * into L2 takes the iph->check store; nontemporal, the in-place
+		 * pass ran 0.391 ms instead of 0.341 (config 2, same box, round 4
+		 * A/B, profiles/r04/inplace/r04g_c2_ihnt_*.log) */
 #pragma unroll
 		for (int j = 0; j < 6; j++)
-#ifdef XCSUM_IH_NT   /* A/B (make variant): the header dwords nontemporal */
-			f.ih[j] = __builtin_nontemporal_load(w + j);
-#else
 			f.ih[j] = w[j];
-#endif
 	}
 	return f;
 }

@@ -1,8 +1,12 @@
-/* xcsum_csum_tl.hip -- in-place A/B (XCSUM_INPLACE_TL=<chunks>):
- * csum_kernel_tl<16, 2, 6, FEAT, TL>, the MTU frame-group kernel with each
- * frame's first TL chunks (those holding udp->check: chunk 0-1 for IPv4,
- * 2-3 for IPv6) loaded temporally, so the in-place store finds its line in
- * the caches.  FEAT 0 (IPv6, no IP header) and 2 (IPv4 + IPHDR). */
+/* xcsum_csum_tl.hip -- csum_kernel_tl<16, 2, 6, 0, 4>: the MTU frame-group
+ * kernel for XCSUM_F_INPLACE without XCSUM_F_IPHDR (IPv6, or IPv4 with only
+ * udp->check), each frame's first 4 chunks -- the one holding udp->check
+ * among them (eth+40: chunk 0-1, eth+60: chunk 2-3) -- loaded temporally, so
+ * the in-place store finds its line in L2.  Config 4 in place 0.331 / 0.333
+ * -> 0.327 / 0.327 ms (same box, two alternating runs,
+ * profiles/r04/inplace/r04g_c4_*.log).  With IPHDR the IPv4 header load is
+ * temporal already and the extra temporal chunks cost: 0.341 -> 0.362 ms
+ * (r04g_c2_tl2_*.log), so that instantiation is not built. */
 #include "xcsum_csum.h"
 
 namespace xcsum {
@@ -37,18 +41,12 @@ static hipError_t launch_tl_t(const CsumArgs &a, int cus, int bpc, hipStream_t s
 	return hipGetLastError();
 }
 
-hipError_t launch_csum_tl(const CsumArgs &a, Geometry g, int tl, int cus, hipStream_t s)
+/* the in-place MTU launch without IPHDR (the caller checks the geometry) */
+hipError_t launch_csum_inplace_tl(const CsumArgs &a, Geometry g, int cus, hipStream_t s)
 {
-	if (!(g.G == 16 && g.U == 2 && g.K == 6) || (a.flags & XCSUM_F_VERIFY))
+	if (!(g.G == 16 && g.U == 2 && g.K == 6) || (a.flags & (XCSUM_F_VERIFY | XCSUM_F_IPHDR)))
 		return hipErrorInvalidValue;
-	const bool iph = (a.flags & XCSUM_F_IPHDR) != 0;
-	if (tl == 2)
-		return iph ? launch_tl_t<16, 2, 6, 2, 2>(a, cus, g.B, s)
-			   : launch_tl_t<16, 2, 6, 0, 2>(a, cus, g.B, s);
-	if (tl == 4)
-		return iph ? launch_tl_t<16, 2, 6, 2, 4>(a, cus, g.B, s)
-			   : launch_tl_t<16, 2, 6, 0, 4>(a, cus, g.B, s);
-	return hipErrorInvalidValue;
+	return launch_tl_t<16, 2, 6, 0, 4>(a, cus, g.B, s);
 }
 
 } /* namespace xcsum */

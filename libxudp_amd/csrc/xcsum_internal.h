@@ -201,9 +201,9 @@ hipError_t launch_csum(const CsumArgs &a, Geometry g, int cus, hipStream_t s);
 hipError_t launch_csum_f0(const CsumArgs &a, Geometry g, int cus, hipStream_t s);
 hipError_t launch_csum_f1(const CsumArgs &a, Geometry g, int cus, hipStream_t s);
 hipError_t launch_csum_f2(const CsumArgs &a, Geometry g, int cus, hipStream_t s);
-/* in-place A/B: the (16,2,6) kernel with temporal loads of each frame's
- * first tl (2 or 4) chunks (xcsum_csum_tl.hip) */
-hipError_t launch_csum_tl(const CsumArgs &a, Geometry g, int tl, int cus, hipStream_t s);
+/* XCSUM_F_INPLACE without IPHDR at (16,2,6): the kernel with each frame's
+ * first 4 chunks loaded temporally (xcsum_csum_tl.hip) */
+hipError_t launch_csum_inplace_tl(const CsumArgs &a, Geometry g, int cus, hipStream_t s);
 hipError_t launch_gen(uint8_t *d_umem, const struct xcsum_desc *d_desc, uint32_t n,
 		      uint32_t family, uint64_t seed, uint64_t first_index, int max_blocks,
 		      hipStream_t s);
@@ -233,8 +233,9 @@ struct Ctx {
 	 * the first pass writes, 2 x u16 per frame, grown on demand */
 	int inplace_sched;
 	uint32_t inplace_block;        /* second-pass store width (ScatterArgs) */
-	int inplace_tl;                /* XCSUM_INPLACE_TL: fused in-place with the
-					  first chunks loaded temporally (A/B) */
+	int inplace_tl;                /* in place without IPHDR at MTU: the
+					  temporal-first-chunks kernel (1, default)
+					  or the plain one (XCSUM_INPLACE_TL=0, A/B) */
 	uint16_t *d_inplace;
 	uint32_t inplace_cap;          /* frames */
 	hipEvent_t inplace_done;       /* after the last two-pass call's scatter */

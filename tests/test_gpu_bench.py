@@ -31,6 +31,21 @@ def test_default_line():
     roof = line["roofline"]
     assert roof["bound"] == "hbm" and 0 < roof["frac"] < 1
     assert "ceiling_measured" in roof and len(line["lib_sha16"]) == 16
+    # same-run visiting-order A/B and the layout's own bound
+    ab = roof["order_ab"]
+    assert set(ab["orders"]) == {"auto", "0,0", "3,4", "4,4", "2,5"}
+    assert all(0 < v["frac_vs_ceiling"] < 1.2 for v in ab["orders"].values())
+    assert 0 < roof["layout_bound_frac"] <= 1 and 0 < roof["frac_of_layout_bound"] < 1.2
+
+
+def test_config3_layout_bound():
+    """Config 3 (64-B payloads): the line states the layout's bound -- a
+    106-B frame in 112 B + a 16-B descriptor per 82 algorithmic bytes -- so
+    its fraction of 8 TB/s reads against what the layout allows."""
+    line = run_bench("--config", "3")
+    roof = line["roofline"]
+    assert 0.5 < roof["layout_alg_over_real"] < 0.75
+    assert roof["layout_bound_frac"] < 0.6 and roof["frac_of_layout_bound"] > 0.5
 
 
 @pytest.mark.parametrize("cid", [2, 4])

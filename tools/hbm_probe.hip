@@ -373,3 +373,57 @@ extern "C" int probe_stream_read_inplace_tl(void *p, uint64_t nbytes, uint64_t f
 			   1.0 / (double)fstride, out);
 	return hipGetLastError() == hipSuccess ? 0 : -1;
 }
+
+/* The in-place probe with whole-block stores from the reading wave: every
+ * thread reads its 16-B chunk (grid-stride, consecutive threads hold
+ * consecutive chunks); when the W-byte block holding the chunk contains a
+ * field of some frame, every thread of that block stores its chunk back (the
+ * field's bytes patched), so the block reaches L2 as one complete W-byte
+ * write from one wave instruction (W = 16: only the field's chunk).  Frame
+ * ownership is ignored (garbage in the fields, as in the other probes). */
+template <int W>
+__global__ void __launch_bounds__(256) stream_read_inplace_blk(uint8_t *p, uint64_t n16,
+							     uint64_t fstride, uint64_t off,
+							     uint64_t nframes, uint32_t f1,
+							     uint32_t f2, double inv, uint32_t *out)
+{
+	uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+	const uint64_t stride = (uint64_t)gridDim.x * 256;
+	uint32_t acc = 0;
+	for (; i < n16; i += stride) {
+		u32x4 v = __builtin_nontemporal_load((gu32x4 *)(p + 16 * i));
+		acc += v.x ^ v.y ^ v.z ^ v.w;
+		/* does this chunk's W-block hold a field? look at each chunk of it */
+		const uint64_t b0 = (16 * i) / W * (W / 16);
+		bool hit = false;
+#pragma unroll
+		for (int q = 0; q < W / 16; q++) {
+			hit |= probe_field_frame(b0 + q, fstride, off, nframes, f1, inv) >= 0;
+			if (f2 != f1)
+				hit |= probe_field_frame(b0 + q, fstride, off, nframes, f2, inv) >= 0;
+		}
+		if (hit) {
+			v.x ^= 1u;
+			*((u32x4 *)(p + 16 * i)) = v;
+		}
+	}
+	out[(uint64_t)blockIdx.x * 256 + threadIdx.x] = acc;
+}
+
+extern "C" int probe_stream_read_inplace_blk(void *p, uint64_t nbytes, uint64_t fstride,
+					     uint64_t off, uint64_t nframes, uint32_t f1,
+					     uint32_t f2, uint32_t *out, int blocks, int W,
+					     void *stream)
+{
+	if (fstride < 16 || !nframes || ((uintptr_t)p & 127))
+		return -1;
+#define L(W_) hipLaunchKernelGGL((stream_read_inplace_blk<W_>), dim3(blocks), dim3(256), 0,        \
+				 (hipStream_t)stream, (uint8_t *)p, nbytes / 16, fstride, off, nframes, \
+				 f1, f2, 1.0 / (double)fstride, out)
+	if (W == 16) L(16);
+	else if (W == 32) L(32);
+	else if (W == 64) L(64);
+	else L(128);
+#undef L
+	return hipGetLastError() == hipSuccess ? 0 : -1;
+}

@@ -13,6 +13,8 @@ frames, packed (1520-B stride) or in xudp's 4096-B slots, 1M frames in a
   lib_two_pass    the library's in-place pass, TWO_PASS schedule
   fused_nt        the read with each field stored by the thread that read it
   fused_tl        the same, the chunks holding a field loaded temporally
+  fused_blkW      the read, each W-byte block holding a field stored back
+                  whole by the wave that read it (W = 16/32/64/128)
   lib_fused_tl2/4 the library's fused pass with each frame's first 2 / 4
                   chunks loaded temporally (XCSUM_INPLACE_TL)
 Prints one JSON line per layout and family."""
@@ -35,6 +37,8 @@ def main():
     ap.add_argument("--family", type=int, default=4)
     ap.add_argument("--layout", default="packed", choices=["packed", "umem"])
     ap.add_argument("--n", type=int, default=1 << 20)
+    ap.add_argument("--legs", default="", help="comma list of legs to run (default: all)")
+    ap.add_argument("--rounds", type=int, default=2)
     args = ap.parse_args()
     import torch
     dev = torch.device("cuda:0")
@@ -94,6 +98,11 @@ def main():
     legs["fused_tl"] = lambda b: L.probe_stream_read_inplace_tl(b, nb, fstride, a0, len(a), f1,
                                                                f2, scratch.data_ptr(), blocks, sp)
 
+    L.probe_stream_read_inplace_blk.argtypes = [V, U64, U64, U64, U64, U32, U32, V, I, I, V]
+    for W in (16, 32, 64, 128):
+        legs[f"fused_blk{W}"] = (lambda W_: lambda b: L.probe_stream_read_inplace_blk(
+            b, nb, fstride, a0, len(a), f1, f2, scratch.data_ptr(), blocks, W_, sp))(W)
+
     def lib(sched, flags, o):
         def f(b):
             eng.set_inplace(sched)
@@ -117,8 +126,10 @@ def main():
     legs["lib_plain"] = lib(X.INPLACE_AUTO, iph, out)
     legs["lib_fused"] = lib(X.INPLACE_FUSED, X.F_INPLACE | iph, None)
     legs["lib_two_pass"] = lib(X.INPLACE_TWO_PASS, X.F_INPLACE | iph, None)
+    if args.legs:
+        legs = {k: legs[k] for k in args.legs.split(",")}
     res = {}
-    for rnd in range(2):          # two rounds, interleaved legs; the min of the medians
+    for rnd in range(args.rounds):   # rounds of interleaved legs; the min of the medians
         for name, fn in legs.items():
             ts = []
             for r in range(6):
