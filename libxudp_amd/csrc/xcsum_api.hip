@@ -873,6 +873,8 @@ extern "C" int xcsum_batch_device(xcsum_ctx *c, uint8_t *d_umem, const struct xc
 	a.flags = flags & (XCSUM_F_INPLACE | XCSUM_F_IPHDR | XCSUM_F_V4_RFC | XCSUM_F_VERIFY);
 	if (a.flags & XCSUM_F_VERIFY)
 		a.flags &= ~XCSUM_F_INPLACE; /* verifying never writes frames */
+	if (mode == XCSUM_MODE_V6)
+		a.flags &= ~XCSUM_F_IPHDR;   /* IPv4 only; the lighter kernel */
 	a.bias = 0;
 	a.err = c->d_err;
 	const Geometry g = geometry_for(c, len_hint, a.flags);

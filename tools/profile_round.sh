@@ -17,11 +17,10 @@ for c in 2 3 4 5; do
   tools/gpu_run.sh $out/bench_config$c 300 $B --config $c --steps 100
 done
 tools/gpu_run.sh $out/bench_config2_umem 300 $B --config 2 --layout umem --steps 100
-for c in 2 4; do
-  tools/gpu_run.sh $out/bench_config${c}_inplace 300 $B --config $c --steps 100 --flags inplace,iphdr
-done
+tools/gpu_run.sh $out/bench_config2_inplace 300 $B --config 2 --steps 100 --flags inplace,iphdr
+tools/gpu_run.sh $out/bench_config4_inplace 300 $B --config 4 --steps 100 --flags inplace
 # name:bench args
-WL="c2:--config 2|c3:--config 3|c4:--config 4|c5:--config 5|c2_inplace:--config 2 --flags inplace,iphdr"
+WL="c2:--config 2|c3:--config 3|c4:--config 4|c5:--config 5|c2_inplace:--config 2 --flags inplace,iphdr|c4_inplace:--config 4 --flags inplace"
 IFS='|' read -ra wls <<< "$WL"
 for w in "${wls[@]}"; do
   n=${w%%:*}; a=${w#*:}
@@ -36,7 +35,7 @@ for w in "${wls[@]}"; do
   tools/gpu_run.sh $out/write_$n 120 rocprofv3 --pmc WRITE_SIZE --output-format csv \
       -d gpurun_out/$out/write_$n -o run -- $P
   cid=$(echo "$a" | sed -n 's/.*--config \([0-9]\).*/\1/p')
-  fl=$(echo "$a" | grep -q inplace && echo 0x3 || echo 0)
+  fl=$(echo "$a" | grep -q "inplace,iphdr" && echo 0x3 || (echo "$a" | grep -q inplace && echo 0x1 || echo 0))
   alg=$(python3 -c "
 import bench, libxudp_amd as X
 cfg = dict(bench.CONFIGS[$cid], id=$cid)
