@@ -83,12 +83,17 @@ def test_bench_helpers_present_and_real_bytes():
     import bench
     for name in ("digest_check", "stream_ceiling", "gpu_clocks", "cpu_baseline", "pmc_traffic",
                  "host_cpu_facts", "real_bytes", "rank_slice", "build_batch", "inplace_ceiling",
-                 "lib_sha16", "parse_flags", "alg_bytes_flags"):
+                 "lib_sha16", "parse_flags", "alg_bytes_flags", "order_ab"):
         assert callable(getattr(bench, name)), name
     d = np.zeros(3, dtype=X.DESC_DTYPE)
     d["addr"] = [0, 100, 4096]
     d["len"] = [100, 28, 64]
     assert bench.real_bytes(d) == (2 + 1) * 64 + 3 * 18
+    # the visiting-order A/B: descriptor order and forced region orders
+    assert (0, 0) in bench.ORDER_AB and (3, 4) in bench.ORDER_AB
+    # the in-place kernel without IPHDR (csrc/xcsum_csum_tl.hip) is found
+    # by name in the library's code objects, so PMC counters can key on it
+    assert bench.kernel_sha16("void xcsum::csum_kernel_tl<16, 2, 6, 0, 4>(xcsum::CsumArgs)")
 
 
 def test_bench_flags_and_algorithmic_bytes():
