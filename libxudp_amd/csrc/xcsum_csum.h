@@ -223,7 +223,7 @@ static __device__ uint16_t ip_header_csum(const Frame &f, bool verify)
 
 template <int FEAT>
 static __device__ __forceinline__ void finalize(const CsumArgs &a, const Frame &f, uint32_t p,
-						uint32_t s, uint32_t skip = 0)
+						uint32_t s)
 {
 	uint16_t wire = 0;
 	if (f.mode >= 0) {
@@ -293,15 +293,20 @@ static __device__ __forceinline__ void finalize(const CsumArgs &a, const Frame &
 				r = 0xffffu; /* CSUM_MANGLED_0, packet.c:23, :115-116 */
 		}
 		wire = bswap16(r);
-		/* frame end: eth + hdr + udp_len (udp_len is not re-cut without VERIFY) */
+		/* In place: 2-byte stores from lane 0.  Round 4 A/B (same box,
+		 * alternating, profiles/r04/inplace/r04i_*.log): the lane holding
+		 * the field's 16-byte chunk storing the whole chunk, patched, ran
+		 * config 2 0.365 ms vs 0.342, config 4 0.397 vs 0.325, xudp's slots
+		 * 0.369 vs 0.358 -- deleted.
+		 * frame end: eth + hdr + udp_len (udp_len is not re-cut without VERIFY) */
 		const uint8_t *fend = f.eth + (f.mode == 2 ? 54u : 34u) + f.udp_len;
 		(void)fend;
-		if ((a.flags & XCSUM_F_INPLACE) && !(skip & 1u) &&
+		if ((a.flags & XCSUM_F_INPLACE) &&
 		    XB_STORE(f.eth + (f.mode == 2 ? 60 : 40), 2, f.eth, fend, XB_CSUM_INPLACE, p))
 			store_u16(f.eth + (f.mode == 2 ? 60 : 40), wire);
 		if ((a.flags & XCSUM_F_IPHDR) && f.mode != 2) {
 			uint16_t ipc = ip_header_csum<FEAT == 2>(f, false);
-			if ((a.flags & XCSUM_F_INPLACE) && !(skip & 2u) &&
+			if ((a.flags & XCSUM_F_INPLACE) &&
 			    XB_STORE(f.eth + 24, 2, f.eth, fend, XB_CSUM_INPLACE, p))
 				store_u16(f.eth + 24, ipc);
 			if (a.out_ip && XB_IDX(p, a.n, XB_CSUM_OUT))
@@ -327,67 +332,6 @@ static __device__ __forceinline__ uint32_t fidx(const CsumArgs &a, uint32_t p)
 	return ORD ? frame_of(a.ord, p) : p;
 }
 
-#ifdef XCSUM_INPLACE_CHUNK16
-/* In-place A/B (make variant NAME=cs16 DEFS=-DXCSUM_INPLACE_CHUNK16): the
- * lane that holds the 16-byte chunk with a check field stores that whole
- * chunk, the field patched, instead of lane 0 storing 2 bytes -- when the
- * chunk was preloaded, lies inside the frame and holds both field bytes.
- * Returns the fields it stored (bit 0 udp->check, bit 1 iph->check); every
- * lane of the segment computes the same values from the same sum. */
-template <int G, int K, int FEAT>
-static __device__ __forceinline__ uint32_t inplace_chunks(const CsumArgs &a, const Frame &f,
-							  const u32x4 (&vc)[K], uint32_t lane,
-							  uint32_t s)
-{
-	if (!(a.flags & XCSUM_F_INPLACE) || f.mode < 0 || (FEAT >= 1 && (a.flags & XCSUM_F_VERIFY)))
-		return 0;
-	const uint32_t udp_len = f.udp_len;
-	const uint32_t S = s + 17u + (udp_len >> 16) + (udp_len & 0xffffu);
-	uint32_t r;
-	if (f.mode == 0) {
-		r = ~((S & 0xffffu) + (S >> 16)) & 0xffffu;
-	} else {
-		uint32_t t = (S & 0xffffu) + (S >> 16);
-		t = (t & 0xffffu) + (t >> 16);
-		r = ~t & 0xffffu;
-		if (r == 0)
-			r = 0xffffu;
-	}
-	const uint32_t wire = bswap16(r);
-	const uint8_t *fend = f.eth + (f.mode == 2 ? 54u : 34u) + f.udp_len;
-	uint32_t done = 0;
-	auto put = [&](const uint8_t *fld, uint32_t val, uint32_t bit) {
-		const uint64_t off = (uint64_t)(fld - f.base);
-		const uint32_t c = (uint32_t)(off >> 4), o = (uint32_t)(off & 15);
-		const uint8_t *cp = f.base + 16u * c;
-		if (fld < f.base || c >= f.nchunks || c >= (uint32_t)(K * G) || o > 14 ||
-		    cp < f.eth || cp + 16 > fend)
-			return;
-		done |= bit;
-#pragma unroll
-		for (int k = 0; k < K; k++) {
-			if (lane + (uint32_t)k * G != c)
-				continue;
-			uint32_t w[4] = {vc[k].x, vc[k].y, vc[k].z, vc[k].w};
-#pragma unroll
-			for (int d = 0; d < 4; d++)
-#pragma unroll
-				for (int b = 0; b < 2; b++) {
-					const uint32_t pos = o + (uint32_t)b, sh = (pos & 3u) * 8u;
-					const uint32_t nw = (w[d] & ~(0xffu << sh)) | (((val >> (8 * b)) & 0xffu) << sh);
-					w[d] = (pos >> 2) == (uint32_t)d ? nw : w[d];
-				}
-			if (XB_STORE(cp, 16, f.eth, fend, XB_CSUM_INPLACE, c))
-				*((u32x4 *)cp) = u32x4{w[0], w[1], w[2], w[3]};
-		}
-	};
-	put(f.eth + (f.mode == 2 ? 60 : 40), wire, 1u);
-	if (FEAT == 2 && (a.flags & XCSUM_F_IPHDR) && f.mode != 2)
-		put(f.eth + 24, ip_header_csum<true>(f, false), 2u);
-	return done;
-}
-#endif
-
 template <int G, int U, int K, bool TAIL, bool ORD, int FEAT, class A>
 static __device__ __forceinline__ void consume(const A &a, const Frame (&fc)[U],
 					       const u32x4 (&vc)[U][K], uint32_t lane,
@@ -403,11 +347,6 @@ static __device__ __forceinline__ void consume(const A &a, const Frame (&fc)[U],
 			sum_walk<G, Grid<G, K>::DW>(f, lane, E, O);   /* jumbo frame */
 		uint32_t s = f.odd ? (O << 8) + E : (E << 8) + O;
 		s = seg_sum<G>(s);
-		uint32_t skip = 0;
-#ifdef XCSUM_INPLACE_CHUNK16
-		if constexpr (!A::kChecked)
-			skip = inplace_chunks<G, K, FEAT>(a, f, vc[u], lane, s);
-#endif
 		if (lane == 0 && f.mode != -2) {
 			if constexpr (A::kChecked) {
 				if (f.mode == -4)
@@ -415,7 +354,7 @@ static __device__ __forceinline__ void consume(const A &a, const Frame (&fc)[U],
 				else
 					finalize<FEAT>(a, f, fidx<ORD>(a, p0 + u * nseg), s);
 			} else {
-				finalize<FEAT>(a, f, fidx<ORD>(a, p0 + u * nseg), s, skip);
+				finalize<FEAT>(a, f, fidx<ORD>(a, p0 + u * nseg), s);
 			}
 		}
 	}
