@@ -205,6 +205,23 @@ def rank_slice(cfg, rank, world):
     return rank * n, n
 
 
+def h2d(torch, arr, dev):
+    """Host array -> device tensor through torch's pinned host memory: the HIP
+    runtime pins pageable buffers of >= 1 MiB in place for a copy, and numpy's
+    large arrays are backed by transparent huge pages -- the combination
+    DESIGN.md 6 traces the registered-memory faults to."""
+    return torch.from_numpy(np.ascontiguousarray(arr)).pin_memory().to(dev)
+
+
+def d2h(torch, t):
+    """Device tensor -> numpy array in pinned host memory (see h2d)."""
+    if t.device.type == "cpu":
+        return t.numpy().copy()
+    h = torch.empty(t.shape, dtype=t.dtype, pin_memory=True)
+    h.copy_(t)
+    return h.numpy()
+
+
 def build_batch(cfg, rank, world, torch, dev, eng, stream):
     """Descriptors + frames for this rank, generated on the device."""
     seed = SEED_BASE ^ cfg["id"]
@@ -218,7 +235,7 @@ def build_batch(cfg, rank, world, torch, dev, eng, stream):
     else:
         desc, nbytes = X.gen_layout(count, cfg["family"], cfg["pmin"], cfg["pmax"], seed=seed,
                                     first_index=first)
-    d_desc = torch.from_numpy(desc.view(np.uint8)).to(dev)
+    d_desc = h2d(torch, desc.view(np.uint8), dev)
     # rotate buffers so each pass streams >= 1 GiB: nothing is served from the
     # 256 MiB Infinity Cache (SURVEY.md 7 hard part iv)
     nrot = max(1, math.ceil((1 << 30) / max(nbytes, 1)))
@@ -577,12 +594,12 @@ def digest_check(cfg, out, count, world, rank, dist, sdev):
         dist.all_gather(parts, pad)
         if rank != 0:
             return None
-        blob = b"".join(p[:2 * int(c)].cpu().numpy().tobytes() for p, c in zip(parts, cnts))
+        blob = b"".join(d2h(torch, p[:2 * int(c)]).tobytes() for p, c in zip(parts, cnts))
         what = f"{key} sha256_out over the concatenated outputs of {world} ranks"
     else:
         if rank != 0:
             return None
-        blob = mine.cpu().numpy().tobytes()
+        blob = d2h(torch, mine).tobytes()
         what = f"{key} sha256_out over rank 0's timed output"
     return {"ok": hashlib.sha256(blob).hexdigest() == want, "what": what}
 
@@ -803,9 +820,9 @@ def main():
     if rank == 0 and count:
         import oracle  # checker only
         m = min(count, 4096)
-        got = out[:m].cpu().numpy().view(np.uint16)
+        got = d2h(torch, out[:m]).view(np.uint16)
         ubytes = int(desc["addr"][m - 1]) + int(desc["len"][m - 1])
-        hu = bufs[0][:ubytes].cpu().numpy()
+        hu = d2h(torch, bufs[0][:ubytes])
         if flags & X.F_INPLACE and not flags & X.F_VERIFY:
             fresh = hu.copy()
             off = 60 if cfg["family"] == 6 else 40

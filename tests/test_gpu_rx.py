@@ -204,7 +204,7 @@ def test_rx_round_trip_full_size(torch_cuda, engine, cid):
     assert np.array_equal(recs["body"], desc["addr"] + hdr)
     assert np.array_equal(recs["size"], desc["len"] - hdr)
     # flip one bit of the last payload byte of every frame
-    last = torch_cuda.from_numpy((desc["addr"] + desc["len"] - 1).astype(np.int64)).to(dev)
+    last = h2d(torch_cuda, (desc["addr"] + desc["len"] - 1).astype(np.int64), dev)
     d_umem[last] ^= 0x10
     engine.rx_device(d_umem, d_desc, n, d_msgs, d_count, X.F_VERIFY, int(desc["len"][0]))
     torch_cuda.cuda.synchronize()

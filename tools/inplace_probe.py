@@ -50,7 +50,7 @@ def main():
     fstride, a0 = int(a[1] - a[0]), int(a[0])
     nrot = max(1, math.ceil((1 << 30) / nbytes))
     bufs = [torch.empty(nbytes + 128, dtype=torch.uint8, device=dev) for _ in range(nrot)]
-    d_desc = torch.from_numpy(desc.view(np.uint8)).to(dev)
+    d_desc = torch.from_numpy(desc.view(np.uint8)).pin_memory().to(dev)
     eng = X.Engine(0)
     s = torch.cuda.current_stream(dev)
     sp = s.cuda_stream
