@@ -25,7 +25,7 @@ IFS='|' read -ra wls <<< "$WL"
 for w in "${wls[@]}"; do
   n=${w%%:*}; a=${w#*:}
   tools/gpu_run.sh $out/stats_$n 300 rocprofv3 --kernel-trace --stats --output-format csv \
-      -d gpurun_out/$out/stats_$n -o run -- $B $a --steps 20 --warmup 5
+      -d gpurun_out/$out/stats_$n -o run -- $B $a --steps 20 --warmup 5 --no-order-ab
 done
 for w in "${wls[@]}"; do
   n=${w%%:*}; a=${w#*:}
