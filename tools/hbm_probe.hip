@@ -427,3 +427,51 @@ extern "C" int probe_stream_read_inplace_blk(void *p, uint64_t nbytes, uint64_t 
 #undef L
 	return hipGetLastError() == hipSuccess ? 0 : -1;
 }
+
+/* The second pass as blind whole-block writes: for each field, the W-byte
+ * block holding it is written in full with junk, no load of it first -- what
+ * full-block stores cost when the data comes from elsewhere (registers, a
+ * side buffer) rather than from a read of the line. */
+template <int W>
+__global__ void __launch_bounds__(256) scatter_blind(uint8_t *p, uint64_t fstride, uint64_t off,
+						     uint64_t nframes, uint32_t f1, uint32_t f2)
+{
+	const uint64_t stride = (uint64_t)gridDim.x * 256;
+	for (uint64_t j = (uint64_t)blockIdx.x * 256 + threadIdx.x; j < nframes; j += stride) {
+		uint8_t *e = p + j * fstride + off;
+		uint8_t *b1 = (uint8_t *)((uintptr_t)(e + f1) & ~(uintptr_t)(W - 1));
+		uint8_t *b2 = (uint8_t *)((uintptr_t)(e + f2) & ~(uintptr_t)(W - 1));
+		const u32x4 v = {(uint32_t)j, (uint32_t)j * 3u, (uint32_t)j * 5u, (uint32_t)j * 7u};
+#pragma unroll
+		for (int q = 0; q < W / 16; q++)
+			*((u32x4 *)(b1 + 16 * q)) = v;
+		if (b2 != b1)
+#pragma unroll
+			for (int q = 0; q < W / 16; q++)
+				*((u32x4 *)(b2 + 16 * q)) = v;
+	}
+}
+
+extern "C" int probe_stream_read_blind(void *p, uint64_t nbytes, uint64_t fstride, uint64_t off,
+				       uint64_t nframes, uint32_t f1, uint32_t f2, uint32_t *out,
+				       int blocks, int W, int read_first, void *stream)
+{
+	if (fstride < 64 || !nframes || ((uintptr_t)p & 127))
+		return -1;
+	if ((nframes - 1) * fstride + off + (f1 > f2 ? f1 : f2) + 128 > nbytes)
+		return -1;
+	if (read_first)
+		hipLaunchKernelGGL((stream_read<true, 4>), dim3(blocks), dim3(256), 0,
+				   (hipStream_t)stream, (const u32x4 *)p, nbytes / 16, out);
+	uint64_t sb = (nframes + 255) / 256;
+	if (sb > (uint64_t)blocks)
+		sb = (uint64_t)blocks;
+#define L(W_) hipLaunchKernelGGL((scatter_blind<W_>), dim3((unsigned)sb), dim3(256), 0,             \
+				 (hipStream_t)stream, (uint8_t *)p, fstride, off, nframes, f1, f2)
+	if (W == 16) L(16);
+	else if (W == 32) L(32);
+	else if (W == 64) L(64);
+	else L(128);
+#undef L
+	return hipGetLastError() == hipSuccess ? 0 : -1;
+}

@@ -13,6 +13,8 @@ frames, packed (1520-B stride) or in xudp's 4096-B slots, 1M frames in a
   lib_two_pass    the library's in-place pass, TWO_PASS schedule
   fused_nt        the read with each field stored by the thread that read it
   fused_tl        the same, the chunks holding a field loaded temporally
+  [read+]blindW   whole W-byte blocks holding the fields written with junk,
+                  no load first (after the read pass, or alone)
   fused_blkW      the read, each W-byte block holding a field stored back
                   whole by the wave that read it (W = 16/32/64/128)
   lib_fused_tl2/4 the library's fused pass with each frame's first 2 / 4
@@ -102,6 +104,13 @@ def main():
     for W in (16, 32, 64, 128):
         legs[f"fused_blk{W}"] = (lambda W_: lambda b: L.probe_stream_read_inplace_blk(
             b, nb, fstride, a0, len(a), f1, f2, scratch.data_ptr(), blocks, W_, sp))(W)
+
+    L.probe_stream_read_blind.argtypes = [V, U64, U64, U64, U64, U32, U32, V, I, I, I, V]
+    for W in (16, 32, 64, 128):
+        for rf in (0, 1):
+            legs[f"{'read+' if rf else ''}blind{W}"] = (lambda W_, rf_: lambda b:
+                L.probe_stream_read_blind(b, nb, fstride, a0, len(a), f1, f2, scratch.data_ptr(),
+                                          blocks, W_, rf_, sp))(W, rf)
 
     def lib(sched, flags, o):
         def f(b):
