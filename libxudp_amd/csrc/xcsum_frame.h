@@ -286,6 +286,26 @@ static __device__ __forceinline__ void issue(const Frame (&f)[U], uint32_t lane,
 		}
 }
 
+/* In-place block stores (xcsum_csum_tl.hip): the 16-byte chunk just below
+ * the chunk grid, [base - 16, base), when it lies inside the frame -- the
+ * part of the 64-byte block holding a check field that the span does not
+ * cover (eth + 0..15 when the span starts at eth + 16).  Loaded by lane G-1,
+ * which holds no chunk of a header block (those are chunks 0..6). */
+template <int G, int U>
+static __device__ __forceinline__ void issue_pre(const Frame (&f)[U], uint32_t lane,
+						 u32x4 (&v)[U])
+{
+	const uint8_t *zero = (const uint8_t *)g_zero_chunk;
+#pragma unroll
+	for (int u = 0; u < U; u++) {
+		const uint8_t *pc = f[u].base - 16;
+		const bool need = lane == G - 1 && f[u].nchunks && pc >= f[u].eth;
+		v[u] = load_chunk(need ? XB_LOAD(pc, 16, f[u].eth, f[u].lim, XB_CSUM_CHUNK, 0xffffffffu,
+						 zero)
+				       : zero);
+	}
+}
+
 } /* namespace xcsum */
 
 #endif

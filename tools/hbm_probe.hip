@@ -475,3 +475,44 @@ extern "C" int probe_stream_read_blind(void *p, uint64_t nbytes, uint64_t fstrid
 #undef L
 	return hipGetLastError() == hipSuccess ? 0 : -1;
 }
+
+/* The second pass as a copy of saved blocks: the 64-byte block holding each
+ * field was saved by the first pass into a compact side array (64 B per
+ * block, in frame order); this pass streams that array and writes every
+ * block back whole -- four lanes per block, one 16-byte store each, so the
+ * memory side sees complete 64-byte writes and reads only the side array. */
+__global__ void __launch_bounds__(256) copy_blocks(uint8_t *p, const uint8_t *side,
+						   uint64_t fstride, uint64_t off, uint64_t nframes,
+						   uint32_t f1, uint32_t f2)
+{
+	const uint32_t nb = ((off + f1) & ~63ull) == ((off + f2) & ~63ull) ? 1u : 2u;
+	const uint64_t total = nframes * nb * 4;
+	const uint64_t stride = (uint64_t)gridDim.x * 256;
+	for (uint64_t g = (uint64_t)blockIdx.x * 256 + threadIdx.x; g < total; g += stride) {
+		const uint64_t j = g / (4 * nb);
+		const uint32_t k = (uint32_t)(g / 4 % nb), q = (uint32_t)(g & 3);
+		uint8_t *e = p + j * fstride + off;
+		uint8_t *b = (uint8_t *)((uintptr_t)(e + (k ? f2 : f1)) & ~(uintptr_t)63);
+		const u32x4 v = __builtin_nontemporal_load((gu32x4 *)(side + 16 * g));
+		*((u32x4 *)(b + 16 * q)) = v;
+	}
+}
+
+extern "C" int probe_stream_read_copy(void *p, uint64_t nbytes, uint64_t fstride, uint64_t off,
+				      uint64_t nframes, uint32_t f1, uint32_t f2, void *side,
+				      uint64_t side_bytes, uint32_t *out, int blocks, int read_first,
+				      void *stream)
+{
+	if (fstride < 64 || !nframes || ((uintptr_t)p & 127))
+		return -1;
+	if ((nframes - 1) * fstride + off + (f1 > f2 ? f1 : f2) + 128 > nbytes)
+		return -1;
+	if (side_bytes < nframes * 128)
+		return -1;
+	if (read_first)
+		hipLaunchKernelGGL((stream_read<true, 4>), dim3(blocks), dim3(256), 0,
+				   (hipStream_t)stream, (const u32x4 *)p, nbytes / 16, out);
+	hipLaunchKernelGGL(copy_blocks, dim3(blocks), dim3(256), 0, (hipStream_t)stream, (uint8_t *)p,
+			   (const uint8_t *)side, fstride, off, nframes, f1, f2);
+	return hipGetLastError() == hipSuccess ? 0 : -1;
+}
