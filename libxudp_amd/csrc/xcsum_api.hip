@@ -604,9 +604,6 @@ extern "C" int xcsum_ctx_create(int device, xcsum_ctx **out)
 	c->inplace_block = 32;
 	if (const char *e = getenv("XCSUM_INPLACE_BLOCK"))
 		c->inplace_block = (uint32_t)atoi(e) == 64 ? 64u : (uint32_t)atoi(e) == 32 ? 32u : 0u;
-	c->inplace_b64 = 0;
-	if (const char *e = getenv("XCSUM_INPLACE_B64"))
-		c->inplace_b64 = atoi(e) == 2 ? 2 : atoi(e) != 0;
 	c->inplace_tl = 1;
 	if (const char *e = getenv("XCSUM_INPLACE_TL"))
 		c->inplace_tl = atoi(e) != 0;
@@ -888,12 +885,6 @@ extern "C" int xcsum_batch_device(xcsum_ctx *c, uint8_t *d_umem, const struct xc
 		const int rc = inplace_two_pass(c, a, g, (hipStream_t)stream, &done);
 		if (rc || done)
 			return rc;
-	}
-	if ((a.flags & XCSUM_F_INPLACE) && !(a.flags & XCSUM_F_VERIFY) && c->inplace_b64 &&
-	    g.G == 16 && g.U == 2 && g.K == 6) {
-		HIPCHK(launch_csum_inplace_b64(a, g, c->cus, c->inplace_tl, c->inplace_b64 == 2,
-					       (hipStream_t)stream));
-		return 0;
 	}
 	/* in place without the IPv4 header at MTU: temporal loads of the chunks
 	 * that hold udp->check (xcsum_csum_tl.hip: config 4 -1.5 %) */

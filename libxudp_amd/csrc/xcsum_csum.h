@@ -114,7 +114,7 @@ static __device__ __forceinline__ Frame resolve(const A &a, u32x4 d, bool presen
 		 * Ethernet header is malformed whatever its next bytes hold */
 		uint32_t proto = 0;
 		if (len >= 14 && XB_IN(f.eth + 12, 2, f.eth, f.eth + len, XB_CSUM_HDR, 12))
-			proto = ((uint32_t)f.eth[12] << 8) | f.eth[13];
+			proto = ((uint32_t)ld_g<uint8_t>(f.eth + 12) << 8) | ld_g<uint8_t>(f.eth + 13);
 		mode = proto == 0x0800u ? ((a.flags & XCSUM_F_V4_RFC) ? 1 : 0)
 		     : proto == 0x86DDu ? 2 : -1;
 	}
@@ -146,12 +146,12 @@ static __device__ __forceinline__ Frame resolve(const A &a, u32x4 d, bool presen
 		 * them apart cost every mode 20 %: it coarsened the waitcnts. */
 		const uint8_t *z = (const uint8_t *)g_zero_chunk;
 		const uint32_t lo = mode == 2 ? 58u : 38u;
-		f.ul = *(const uint16_t *)(f.nchunks ? XB_LOAD(f.eth + lo, 2, f.eth, f.eth + len,
-								XB_CSUM_HDR, lo, z)
-						     : z);
-		f.ck = *(const uint16_t *)(f.nchunks ? XB_LOAD(f.eth + lo + 2, 2, f.eth, f.eth + len,
-								XB_CSUM_HDR, lo + 2, z + 8)
-						     : z + 8);
+		f.ul = ld_g<uint16_t>(f.nchunks ? XB_LOAD(f.eth + lo, 2, f.eth, f.eth + len,
+							   XB_CSUM_HDR, lo, z)
+						: z);
+		f.ck = ld_g<uint16_t>(f.nchunks ? XB_LOAD(f.eth + lo + 2, 2, f.eth, f.eth + len,
+							   XB_CSUM_HDR, lo + 2, z + 8)
+						: z + 8);
 	}
 	/* IPHDR: the IPv4 header too (six dwords, same reasoning) */
 	if (FEAT == 2 && (a.flags & XCSUM_F_IPHDR)) {
@@ -159,8 +159,9 @@ static __device__ __forceinline__ Frame resolve(const A &a, u32x4 d, bool presen
 							   : (const uint8_t *)g_zero_chunk;
 		f.ihs = (uint32_t)(uintptr_t)ih & 3u;
 		/* global loads: the integer round trip loses the address space,
-		 * and flat loads (counted on lgkmcnt too) turned every wait of
-		 * the software pipeline into a full vmcnt(0) drain */
+		 * and as flat loads (counted on lgkmcnt too) they ran config 2 in
+		 * place 0.3419 ms instead of 0.3381 (same box, alternating,
+		 * profiles/r04/inplace/r04n_ab_flat_b64.txt) */
 		typedef __attribute__((address_space(1))) const uint32_t gu32;
 		gu32 *w = (gu32 *)((uintptr_t)ih & ~(uintptr_t)3);
 		if (ih != (const uint8_t *)g_zero_chunk &&
@@ -225,31 +226,9 @@ static __device__ uint16_t ip_header_csum(const Frame &f, bool verify)
 	return bswap16(~sum & 0xffffu);
 }
 
-/* the transmit-side udp->check of a well-formed frame from its span sum s
- * (memory order): legacy single fold (checksum.h:100-104), RFC / IPv6 with
- * CSUM_MANGLED_0 (packet.c:23, :115-116) */
-static __device__ __forceinline__ uint16_t tx_wire(const Frame &f, uint32_t s)
-{
-	const uint32_t udp_len = f.udp_len;
-	const uint32_t S = s + 17u + (udp_len >> 16) + (udp_len & 0xffffu);
-	uint32_t r;
-	if (f.mode == 0) {
-		r = ~((S & 0xffffu) + (S >> 16)) & 0xffffu;
-	} else {
-		uint32_t t = (S & 0xffffu) + (S >> 16);
-		t = (t & 0xffffu) + (t >> 16);
-		r = ~t & 0xffffu;
-		if (r == 0)
-			r = 0xffffu;
-	}
-	return bswap16(r);
-}
-
-/* skip (in-place block stores, inplace_blocks()): bit 0 udp->check, bit 1
- * iph->check already stored */
 template <int FEAT>
 static __device__ __forceinline__ void finalize(const CsumArgs &a, const Frame &f, uint32_t p,
-						uint32_t s, uint32_t skip = 0)
+						uint32_t s)
 {
 	uint16_t wire = 0;
 	if (f.mode >= 0) {
@@ -280,11 +259,11 @@ static __device__ __forceinline__ void finalize(const CsumArgs &a, const Frame &
 				}
 			}
 		}
+		uint32_t S = s + 17u + (udp_len >> 16) + (udp_len & 0xffffu);
+		uint32_t r;
 		if (FEAT >= 1 && (a.flags & XCSUM_F_VERIFY)) {
 			/* the frame's check field was summed with everything else:
 			 * a valid RFC checksum folds to 0xffff, i.e. r == 0 */
-			const uint32_t S = s + 17u + (udp_len >> 16) + (udp_len & 0xffffu);
-			uint32_t r;
 			uint32_t t = (S & 0xffffu) + (S >> 16);
 			t = (t & 0xffffu) + (t >> 16);
 			r = ~t & 0xffffu;
@@ -308,21 +287,35 @@ static __device__ __forceinline__ void finalize(const CsumArgs &a, const Frame &
 				st_res(a.out + p, wire);
 			return;
 		}
-		wire = tx_wire(f, s);
+		if (f.mode == 0) {
+			/* checksum.h:100-104: one fold, carry dropped by the u16 cast */
+			r = ~((S & 0xffffu) + (S >> 16)) & 0xffffu;
+		} else {
+			uint32_t t = (S & 0xffffu) + (S >> 16);
+			t = (t & 0xffffu) + (t >> 16);
+			r = ~t & 0xffffu;
+			if (r == 0)
+				r = 0xffffu; /* CSUM_MANGLED_0, packet.c:23, :115-116 */
+		}
+		wire = bswap16(r);
 		/* In place: 2-byte stores from lane 0.  Round 4 A/B (same box,
-		 * alternating, profiles/r04/inplace/r04i_*.log): the lane holding
+		 * alternating, profiles/r04/inplace/r04i_cs16.bundle.txt): the lane holding
 		 * the field's 16-byte chunk storing the whole chunk, patched, ran
 		 * config 2 0.365 ms vs 0.342, config 4 0.397 vs 0.325, xudp's slots
-		 * 0.369 vs 0.358 -- deleted.
+		 * 0.369 vs 0.358 -- deleted.  The four lanes holding the 64-byte
+		 * block around the field storing it whole (a complete block, no
+		 * merge beyond L2; the chunk below the grid loaded for it): config 4
+		 * 0.338 vs 0.3265, config 2 0.358 vs 0.338 (r04n_ab_flat_b64.txt,
+		 * commit d8dab61) -- deleted.
 		 * frame end: eth + hdr + udp_len (udp_len is not re-cut without VERIFY) */
 		const uint8_t *fend = f.eth + (f.mode == 2 ? 54u : 34u) + f.udp_len;
 		(void)fend;
-		if ((a.flags & XCSUM_F_INPLACE) && !(skip & 1u) &&
+		if ((a.flags & XCSUM_F_INPLACE) &&
 		    XB_STORE(f.eth + (f.mode == 2 ? 60 : 40), 2, f.eth, fend, XB_CSUM_INPLACE, p))
 			store_u16(f.eth + (f.mode == 2 ? 60 : 40), wire);
 		if ((a.flags & XCSUM_F_IPHDR) && f.mode != 2) {
 			uint16_t ipc = ip_header_csum<FEAT == 2>(f, false);
-			if ((a.flags & XCSUM_F_INPLACE) && !(skip & 2u) &&
+			if ((a.flags & XCSUM_F_INPLACE) &&
 			    XB_STORE(f.eth + 24, 2, f.eth, fend, XB_CSUM_INPLACE, p))
 				store_u16(f.eth + 24, ipc);
 			if (a.out_ip && XB_IDX(p, a.n, XB_CSUM_OUT))
@@ -348,78 +341,10 @@ static __device__ __forceinline__ uint32_t fidx(const CsumArgs &a, uint32_t p)
 	return ORD ? frame_of(a.ord, p) : p;
 }
 
-/* In place, B64 kernels (xcsum_csum_tl.hip): the 64-byte block holding a
- * check field is written whole -- every lane holding one of its four chunks
- * stores that chunk, the fields patched -- when the block lies inside the
- * frame and all four chunks were loaded (grid chunks 0..G-2, or the chunk
- * below the grid, issue_pre(), held by lane G-1).  A block written in full
- * reaches memory as a plain 64-byte write; a 2-byte field store leaves a
- * partial block that is merged beyond L2 (DESIGN.md 5.3,
- * tools/inplace_probe.py "read+blind64" vs "read+w2").  Bytes other than
- * the fields are written back as loaded.  Aligned chunk grid only (DW =
- * false: chunks at 16-byte addresses).  Returns the fields stored (bit 0
- * udp->check, bit 1 iph->check); every lane of the segment computes the same
- * values. */
-static __device__ __forceinline__ void patch_field(uint32_t (&w)[4], intptr_t pos, uint32_t val)
-{
-#pragma unroll
-	for (int b = 0; b < 2; b++) {
-		const intptr_t q = pos + b;
-		const uint32_t sh = (uint32_t)(q & 3) * 8u;
-		const uint32_t byte = (val >> (8 * b)) & 0xffu;
-#pragma unroll
-		for (int d = 0; d < 4; d++)
-			w[d] = q >= 4 * d && q < 4 * d + 4 ? (w[d] & ~(0xffu << sh)) | (byte << sh) : w[d];
-	}
-}
-
-template <int G, int K, int FEAT, bool PRE>
-static __device__ __forceinline__ uint32_t inplace_blocks(const CsumArgs &a, const Frame &f,
-							  const u32x4 (&vc)[K], u32x4 vp,
-							  uint32_t lane, uint32_t s)
-{
-	if (!(a.flags & XCSUM_F_INPLACE) || f.mode < 0 || (FEAT >= 1 && (a.flags & XCSUM_F_VERIFY)))
-		return 0;
-	const uint8_t *fend = f.eth + (f.mode == 2 ? 54u : 34u) + f.udp_len;
-	const uintptr_t f1 = (uintptr_t)f.eth + (f.mode == 2 ? 60u : 40u);
-	const uintptr_t f2 = (uintptr_t)f.eth + 24u;
-	const bool iph = FEAT == 2 && (a.flags & XCSUM_F_IPHDR) && f.mode != 2;
-	const intptr_t cmin = PRE && f.base - 16 >= f.eth ? -1 : 0;
-	auto whole = [&](uintptr_t fld) {
-		const uintptr_t B = fld & ~(uintptr_t)63;
-		const intptr_t cB = ((intptr_t)B - (intptr_t)f.base) >> 4;
-		return B >= (uintptr_t)f.eth && B + 64 <= (uintptr_t)fend && fld + 2 <= B + 64 &&
-		       cB >= cmin && cB + 3 <= (intptr_t)G - 2 && cB + 3 < (intptr_t)f.nchunks;
-	};
-	const bool e1 = whole(f1), e2 = iph && whole(f2);
-	if (!e1 && !e2)
-		return 0;
-	const uint16_t wire = tx_wire(f, s);
-	const uint16_t ipc = iph ? ip_header_csum<FEAT == 2>(f, false) : (uint16_t)0;
-	const intptr_t c = lane == G - 1 ? -1 : (intptr_t)lane;
-	const uintptr_t ca = (uintptr_t)f.base + 16 * c;
-	const bool in1 = e1 && (ca & ~(uintptr_t)63) == (f1 & ~(uintptr_t)63);
-	const bool in2 = e2 && (ca & ~(uintptr_t)63) == (f2 & ~(uintptr_t)63);
-	if (in1 || in2) {
-		const u32x4 v = PRE && lane == G - 1 ? vp : vc[0];
-		uint32_t w[4] = {v.x, v.y, v.z, v.w};
-		if (e1)
-			patch_field(w, (intptr_t)f1 - (intptr_t)ca, wire);
-		if (e2)
-			patch_field(w, (intptr_t)f2 - (intptr_t)ca, ipc);
-		if (XB_STORE((uint8_t *)ca, 16, f.eth, fend, XB_CSUM_INPLACE, (uint32_t)c))
-			/* a global store: through a generic pointer this is a flat
-			 * store, counted on lgkmcnt too, and every wait in the loop
-			 * became a full vmcnt(0) drain */
-			*((__attribute__((address_space(1))) u32x4 *)ca) = u32x4{w[0], w[1], w[2], w[3]};
-	}
-	return (e1 ? 1u : 0u) | (e2 ? 2u : 0u);
-}
-
-template <int G, int U, int K, bool TAIL, bool ORD, int FEAT, class A, int B64 = 0>
+template <int G, int U, int K, bool TAIL, bool ORD, int FEAT, class A>
 static __device__ __forceinline__ void consume(const A &a, const Frame (&fc)[U],
-					       const u32x4 (&vc)[U][K], const u32x4 (&vp)[U],
-					       uint32_t lane, uint32_t p0, uint32_t nseg)
+					       const u32x4 (&vc)[U][K], uint32_t lane,
+					       uint32_t p0, uint32_t nseg)
 {
 #pragma unroll
 	for (int u = 0; u < U; u++) {
@@ -431,9 +356,6 @@ static __device__ __forceinline__ void consume(const A &a, const Frame (&fc)[U],
 			sum_walk<G, Grid<G, K>::DW>(f, lane, E, O);   /* jumbo frame */
 		uint32_t s = f.odd ? (O << 8) + E : (E << 8) + O;
 		s = seg_sum<G>(s);
-		uint32_t skip = 0;
-		if constexpr (B64 > 0 && !A::kChecked && !Grid<G, K>::DW)
-			skip = inplace_blocks<G, K, FEAT, B64 == 2>(a, f, vc[u], vp[u], lane, s);
 		if (lane == 0 && f.mode != -2) {
 			if constexpr (A::kChecked) {
 				if (f.mode == -4)
@@ -441,7 +363,7 @@ static __device__ __forceinline__ void consume(const A &a, const Frame (&fc)[U],
 				else
 					finalize<FEAT>(a, f, fidx<ORD>(a, p0 + u * nseg), s);
 			} else {
-				finalize<FEAT>(a, f, fidx<ORD>(a, p0 + u * nseg), s, skip);
+				finalize<FEAT>(a, f, fidx<ORD>(a, p0 + u * nseg), s);
 			}
 		}
 	}
@@ -449,19 +371,19 @@ static __device__ __forceinline__ void consume(const A &a, const Frame (&fc)[U],
 
 /* wave-uniform split: the jumbo path lives in its own copy of the body, so
  * its drains never merge into the common path's vmcnt bookkeeping */
-template <int G, int U, int K, bool ORD, int FEAT, class A, int B64 = 0>
+template <int G, int U, int K, bool ORD, int FEAT, class A>
 static __device__ __forceinline__ void consume_any(const A &a, const Frame (&fc)[U],
-						   const u32x4 (&vc)[U][K], const u32x4 (&vp)[U],
-						   uint32_t lane, uint32_t p0, uint32_t nseg)
+						   const u32x4 (&vc)[U][K], uint32_t lane,
+						   uint32_t p0, uint32_t nseg)
 {
 	bool big = false;
 #pragma unroll
 	for (int u = 0; u < U; u++)
 		big |= fc[u].nchunks > K * G;
 	if (__builtin_amdgcn_ballot_w64(big))
-		consume<G, U, K, true, ORD, FEAT, A, B64>(a, fc, vc, vp, lane, p0, nseg);
+		consume<G, U, K, true, ORD, FEAT, A>(a, fc, vc, lane, p0, nseg);
 	else
-		consume<G, U, K, false, ORD, FEAT, A, B64>(a, fc, vc, vp, lane, p0, nseg);
+		consume<G, U, K, false, ORD, FEAT, A>(a, fc, vc, lane, p0, nseg);
 }
 
 /*
@@ -475,7 +397,7 @@ static __device__ __forceinline__ void consume_any(const A &a, const Frame (&fc)
  * at the loop latch, that copy needs the next step's loads to have landed,
  * and the ISA showed a vmcnt(0) there -- one step in flight, not two.
  */
-template <int G, int U, int K, bool ORD, int FEAT, class A, int TL = 0, int B64 = 0>
+template <int G, int U, int K, bool ORD, int FEAT, class A, int TL = 0>
 static __device__ __forceinline__ void csum_loop(const A &a)
 {
 	const uint32_t lane = threadIdx.x & (G - 1);
@@ -506,9 +428,6 @@ static __device__ __forceinline__ void csum_loop(const A &a)
 	 * chunk loads in flight */
 	__builtin_amdgcn_sched_barrier(0);
 	issue<G, U, K, TL>(fa, lane, va);
-	u32x4 pa[U], pb[U];   /* B64: the chunk below each frame's grid */
-	if constexpr (B64 == 2)
-		issue_pre<G, U>(fa, lane, pa);
 
 	Frame fb[U];
 	u32x4 vb[U][K];
@@ -521,9 +440,7 @@ static __device__ __forceinline__ void csum_loop(const A &a)
 			d[u] = load_desc<G == 64>(a, fidx<ORD>(a, p0 + 2 * step + u * nseg));
 		__builtin_amdgcn_sched_barrier(0);
 		issue<G, U, K, TL>(fb, lane, vb);
-		if constexpr (B64 == 2)
-			issue_pre<G, U>(fb, lane, pb);
-		consume_any<G, U, K, ORD, FEAT, A, B64>(a, fa, va, pa, lane, p0, nseg);
+		consume_any<G, U, K, ORD, FEAT, A>(a, fa, va, lane, p0, nseg);
 
 #pragma unroll
 		for (int u = 0; u < U; u++)
@@ -534,23 +451,21 @@ static __device__ __forceinline__ void csum_loop(const A &a)
 			d[u] = load_desc<G == 64>(a, fidx<ORD>(a, p0 + 3 * step + u * nseg));
 		__builtin_amdgcn_sched_barrier(0);
 		issue<G, U, K, TL>(fa, lane, va);
-		if constexpr (B64 == 2)
-			issue_pre<G, U>(fa, lane, pa);
-		consume_any<G, U, K, ORD, FEAT, A, B64>(a, fb, vb, pb, lane, p0 + step, nseg);
+		consume_any<G, U, K, ORD, FEAT, A>(a, fb, vb, lane, p0 + step, nseg);
 	}
 }
 
 /* The identity order gets its own copy of the loop, so descriptor-order
  * batches pay nothing for the region order; which copy runs is decided once
  * per launch (uniform branch, after resolve_order). */
-template <int G, int U, int K, int FEAT, int TL = 0, int B64 = 0>
+template <int G, int U, int K, int FEAT, int TL = 0>
 static __device__ __forceinline__ void csum_body(CsumArgs &a)
 {
 	resolve_order(a);
 	if (a.ord.rshift == 0)
-		csum_loop<G, U, K, false, FEAT, CsumArgs, TL, B64>(a);
+		csum_loop<G, U, K, false, FEAT, CsumArgs, TL>(a);
 	else
-		csum_loop<G, U, K, true, FEAT, CsumArgs, TL, B64>(a);
+		csum_loop<G, U, K, true, FEAT, CsumArgs, TL>(a);
 }
 
 template <int G, int U, int K, int FEAT>

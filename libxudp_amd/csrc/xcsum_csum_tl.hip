@@ -17,30 +17,14 @@ __global__ void __launch_bounds__(256) csum_kernel_tl(CsumArgs a)
 	csum_body<G, U, K, FEAT, TL>(a);
 }
 
-/* B64 (inplace_blocks(), xcsum_csum.h): two waves per SIMD, as the plain
- * kernels -- the copy with IPHDR and the chunk below the grid otherwise
- * allocates 264 registers and runs one */
-template <int G, int U, int K, int FEAT, int TL, int B64>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2)))
-csum_kernel_b64(CsumArgs a)
-{
-	csum_body<G, U, K, FEAT, TL, B64>(a);
-}
-
-template <int G, int U, int K, int FEAT, int TL, int B64 = 0>
+template <int G, int U, int K, int FEAT, int TL>
 static hipError_t launch_tl_t(const CsumArgs &a, int cus, int bpc, hipStream_t s)
 {
 	static std::atomic<int> occ_cache[OCC_MAX_DEVICES];
-	auto kern = [] {
-		if constexpr (B64 > 0)
-			return csum_kernel_b64<G, U, K, FEAT, TL, B64>;
-		else
-			return csum_kernel_tl<G, U, K, FEAT, TL>;
-	}();
-	const int occ = occupancy_cached(occ_cache, [&] {
+	const int occ = occupancy_cached(occ_cache, [] {
 		int nb = 0;
-		if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kern, 256, 0) != hipSuccess ||
-		    nb <= 0)
+		if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, csum_kernel_tl<G, U, K, FEAT, TL>, 256,
+								 0) != hipSuccess || nb <= 0)
 			nb = 4;
 		return nb;
 	});
@@ -53,7 +37,7 @@ static hipError_t launch_tl_t(const CsumArgs &a, int cus, int bpc, hipStream_t s
 	if (blocks == 0)
 		blocks = 1;
 	(void)hipGetLastError();
-	hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(256), 0, s, a);
+	hipLaunchKernelGGL((csum_kernel_tl<G, U, K, FEAT, TL>), dim3((unsigned)blocks), dim3(256), 0, s, a);
 	return hipGetLastError();
 }
 
@@ -63,23 +47,6 @@ hipError_t launch_csum_inplace_tl(const CsumArgs &a, Geometry g, int cus, hipStr
 	if (!(g.G == 16 && g.U == 2 && g.K == 6) || (a.flags & (XCSUM_F_VERIFY | XCSUM_F_IPHDR)))
 		return hipErrorInvalidValue;
 	return launch_tl_t<16, 2, 6, 0, 4>(a, cus, g.B, s);
-}
-
-/* the in-place MTU launch with whole 64-byte block stores (inplace_blocks(),
- * xcsum_csum.h), with or without IPHDR; tl: the temporal-first-chunks loads
- * too (without IPHDR only) */
-hipError_t launch_csum_inplace_b64(const CsumArgs &a, Geometry g, int cus, int tl, int pre,
-				   hipStream_t s)
-{
-	if (!(g.G == 16 && g.U == 2 && g.K == 6) || !(a.flags & XCSUM_F_INPLACE) ||
-	    (a.flags & XCSUM_F_VERIFY))
-		return hipErrorInvalidValue;
-	if (a.flags & XCSUM_F_IPHDR)
-		return pre ? launch_tl_t<16, 2, 6, 2, 0, 2>(a, cus, g.B, s)
-			   : launch_tl_t<16, 2, 6, 2, 0, 1>(a, cus, g.B, s);
-	if (tl)
-		return launch_tl_t<16, 2, 6, 0, 4, 2>(a, cus, g.B, s);
-	return launch_tl_t<16, 2, 6, 0, 0, 2>(a, cus, g.B, s);
 }
 
 } /* namespace xcsum */

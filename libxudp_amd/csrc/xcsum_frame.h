@@ -243,12 +243,25 @@ struct Grid {
 	static constexpr bool DW = !(G == 16 && K >= 6) && !(G == 8 && K >= 12);
 };
 
+/* Frame bytes and result arrays are global memory (device memory or a
+ * registered host UMEM): accessed through address_space(1) pointers, so a
+ * pointer that came from memory (the resident kernel's request words) or
+ * from integer arithmetic still gets global, not flat, instructions -- a
+ * flat access is counted on lgkmcnt too and the waits around it drain the
+ * whole vmcnt queue (csum_kernel<16,2,6,2>, profiles/r04/inplace/
+ * r04n_ab_flat_b64.txt). */
+template <typename T>
+static __device__ __forceinline__ T ld_g(const void *p)
+{
+	return *(const __attribute__((address_space(1))) T *)p;
+}
+
 /* Result and in-place stores are plain (temporal): nontemporal 2-byte stores
  * each became a partial write, config 2 +12 % (profiles/r02) */
 template <typename T>
 static __device__ __forceinline__ void st_res(T *p, T v)
 {
-	*p = v;
+	*(__attribute__((address_space(1))) T *)p = v;
 }
 
 /* a 2-byte check field of the frame (in-place writes) */
@@ -284,26 +297,6 @@ static __device__ __forceinline__ void issue(const Frame (&f)[U], uint32_t lane,
 			else
 				v[u][k] = load_chunk(q);
 		}
-}
-
-/* In-place block stores (xcsum_csum_tl.hip): the 16-byte chunk just below
- * the chunk grid, [base - 16, base), when it lies inside the frame -- the
- * part of the 64-byte block holding a check field that the span does not
- * cover (eth + 0..15 when the span starts at eth + 16).  Loaded by lane G-1,
- * which holds no chunk of a header block (those are chunks 0..6). */
-template <int G, int U>
-static __device__ __forceinline__ void issue_pre(const Frame (&f)[U], uint32_t lane,
-						 u32x4 (&v)[U])
-{
-	const uint8_t *zero = (const uint8_t *)g_zero_chunk;
-#pragma unroll
-	for (int u = 0; u < U; u++) {
-		const uint8_t *pc = f[u].base - 16;
-		const bool need = lane == G - 1 && f[u].nchunks && pc >= f[u].eth;
-		v[u] = load_chunk(need ? XB_LOAD(pc, 16, f[u].eth, f[u].lim, XB_CSUM_CHUNK, 0xffffffffu,
-						 zero)
-				       : zero);
-	}
 }
 
 } /* namespace xcsum */

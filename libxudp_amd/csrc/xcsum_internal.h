@@ -204,9 +204,6 @@ hipError_t launch_csum_f2(const CsumArgs &a, Geometry g, int cus, hipStream_t s)
 /* XCSUM_F_INPLACE without IPHDR at (16,2,6): the kernel with each frame's
  * first 4 chunks loaded temporally (xcsum_csum_tl.hip) */
 hipError_t launch_csum_inplace_tl(const CsumArgs &a, Geometry g, int cus, hipStream_t s);
-/* XCSUM_F_INPLACE at (16,2,6) with whole 64-byte block stores (xcsum_csum_tl.hip) */
-hipError_t launch_csum_inplace_b64(const CsumArgs &a, Geometry g, int cus, int tl, int pre,
-				   hipStream_t s);
 hipError_t launch_gen(uint8_t *d_umem, const struct xcsum_desc *d_desc, uint32_t n,
 		      uint32_t family, uint64_t seed, uint64_t first_index, int max_blocks,
 		      hipStream_t s);
@@ -236,10 +233,6 @@ struct Ctx {
 	 * the first pass writes, 2 x u16 per frame, grown on demand */
 	int inplace_sched;
 	uint32_t inplace_block;        /* second-pass store width (ScatterArgs) */
-	int inplace_b64;               /* in place at MTU: whole 64-byte block
-					  stores (XCSUM_INPLACE_B64=1: blocks of
-					  grid chunks; 2: the chunk below the
-					  grid too; A/B) */
 	int inplace_tl;                /* in place without IPHDR at MTU: the
 					  temporal-first-chunks kernel (1, default)
 					  or the plain one (XCSUM_INPLACE_TL=0, A/B) */

@@ -100,39 +100,6 @@ def test_two_pass_store_widths(torch_cuda, monkeypatch, block, layout):
         e.close()
 
 
-@pytest.mark.parametrize("b64,tl", [(1, 1), (2, 1), (2, 0)])
-@pytest.mark.parametrize("layout", ["packed1", "packed8", "packed16", "slots"])
-def test_fused_block_stores(torch_cuda, monkeypatch, b64, tl, layout):
-    """The fused pass with whole 64-byte block stores (XCSUM_INPLACE_B64=1:
-    blocks of the chunk grid; 2: the chunk below the grid too;
-    XCSUM_INPLACE_TL: with or without the temporal first chunks), at the MTU
-    geometry those kernels exist for: frames at every byte phase and of every
-    size (blocks inside and across the frame's ends), packed and in xudp's
-    slots -- the reference's fields in place and not one other byte changed."""
-    monkeypatch.setenv("XCSUM_INPLACE_B64", str(b64))
-    monkeypatch.setenv("XCSUM_INPLACE_TL", str(tl))
-    e = X.Engine(0)
-    monkeypatch.delenv("XCSUM_INPLACE_B64")
-    monkeypatch.delenv("XCSUM_INPLACE_TL")
-    try:
-        e.set_geometry(16, 2, 6)
-        for fam, mode in ((4, X.MODE_V4_LEGACY), (4, X.MODE_V4_RFC), (6, X.MODE_V6),
-                          (4, X.MODE_AUTO)):
-            kw = {"packed1": dict(align=1), "packed8": dict(align=8),
-                  "packed16": dict(align=16),
-                  "slots": dict(stride=4096, offset=342 if fam == 4 else 322)}[layout]
-            for pmin, pmax in ((0, 1472), (1472, 1472)):
-                umem, desc = X.gen_frames_host(2000, fam, pmin, pmax, seed=90 + fam + pmin, **kw)
-                for flags in (X.F_INPLACE, X.F_INPLACE | X.F_IPHDR):
-                    res, exp_after = expected_frames(umem, desc, mode, flags)
-                    got, after = run_device(torch_cuda, e, umem.copy(), desc, mode, flags, 1500)
-                    assert np.array_equal(got, res)
-                    diff = np.nonzero(after != exp_after)[0]
-                    assert len(diff) == 0, f"{fam} {mode} {flags:#x} {pmin}: {len(diff)} bytes, {diff[:4]}"
-    finally:
-        e.close()
-
-
 @pytest.mark.parametrize("seed", range(12))
 def test_fuzz_schedules_identical(torch_cuda, engine, seed):
     """Random batches (mixed sizes, alignments, shuffled and malformed
@@ -159,33 +126,6 @@ def test_fuzz_schedules_identical(torch_cuda, engine, seed):
             errs_fused = errs
         else:
             assert errs == errs_fused
-
-
-@pytest.mark.parametrize("seed", range(8))
-def test_fuzz_block_stores(torch_cuda, monkeypatch, seed):
-    """Random batches (mixed sizes, alignments, shuffled and malformed
-    descriptors) through the block-store kernels at the MTU geometry: the
-    oracle's fields, every other byte unchanged, malformed frames counted."""
-    rng = np.random.default_rng(7000 + seed)
-    umem, desc = random_batch(rng)
-    mode = MODES[int(rng.integers(len(MODES)))]
-    flags = X.F_INPLACE | int(rng.choice([0, X.F_IPHDR, X.F_IPHDR | X.F_V4_RFC]))
-    res_exp, after_exp = expected_frames(umem, desc, mode, flags)
-    errs = {}
-    for b64 in (0, 2):
-        monkeypatch.setenv("XCSUM_INPLACE_B64", str(b64))
-        e = X.Engine(0)
-        monkeypatch.delenv("XCSUM_INPLACE_B64")
-        try:
-            e.set_geometry(16, 2, 6)
-            got, after = run_device(torch_cuda, e, umem.copy(), desc, mode, flags, 1500)
-            errs[b64] = e.take_errors()
-        finally:
-            e.close()
-        assert np.array_equal(got, res_exp), f"seed {seed} b64 {b64}"
-        diff = np.nonzero(after != after_exp)[0]
-        assert len(diff) == 0, f"seed {seed} b64 {b64}: {len(diff)} bytes differ, first {diff[:4]}"
-    assert errs[0] == errs[2]
 
 
 def test_two_pass_under_graph_capture(torch_cuda):

@@ -21,8 +21,6 @@ frames, packed (1520-B stride) or in xudp's 4096-B slots, 1M frames in a
                   whole by the wave that read it (W = 16/32/64/128)
   lib_fused_tl2/4 the library's fused pass with each frame's first 2 / 4
                   chunks loaded temporally (XCSUM_INPLACE_TL)
-  lib_b64_1/2     the library's fused pass with whole 64-B block stores
-                  (XCSUM_INPLACE_B64; _tl0: without the temporal chunks)
 Prints one JSON line per layout and family."""
 import argparse
 import ctypes
@@ -141,21 +139,6 @@ def main():
                                      stream=sp)
             return 0
         return f
-    engs_b64 = {}
-    for b64, tl in ((1, 1), (2, 1), (2, 0)):
-        os.environ["XCSUM_INPLACE_B64"] = str(b64)
-        os.environ["XCSUM_INPLACE_TL"] = str(tl)
-        engs_b64[b64, tl] = X.Engine(0)
-    del os.environ["XCSUM_INPLACE_B64"], os.environ["XCSUM_INPLACE_TL"]
-
-    def lib_b64(b64, tl):
-        def f(b):
-            engs_b64[b64, tl].batch_device(b, d_desc, len(desc), None, mode, X.F_INPLACE | iph,
-                                           1500, stream=sp)
-            return 0
-        return f
-    for b64, tl in engs_b64:
-        legs[f"lib_b64_{b64}" + ("" if tl else "_tl0")] = lib_b64(b64, tl)
     legs["lib_fused_tl2"] = lib_tl(2)
     legs["lib_fused_tl4"] = lib_tl(4)
     legs["lib_plain"] = lib(X.INPLACE_AUTO, iph, out)

@@ -27,7 +27,7 @@ for r in 1 2; do
   run c4ip_head_$r $V --config 4 --flags inplace
   run c4ip_new_$r "" --config 4 --flags inplace
 done
-L=lib_plain,lib_fused,lib_b64_1,lib_b64_2,lib_b64_2_tl0,read+blind64
+L=lib_plain,lib_fused,read+blind64,read+copy64
 for fam in 4 6; do
   timeout -k 10 240 python -u tools/inplace_probe.py --family $fam --legs $L --rounds 3 \
     >> gpurun_out/$t/probe.log 2>&1 || exit $?
