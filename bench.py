@@ -630,6 +630,8 @@ def main():
                     help="untimed back-to-back K-step bodies before timing (clock ramp)")
     ap.add_argument("--no-ceiling", action="store_true",
                     help="skip the same-run streaming-read ceiling probe")
+    ap.add_argument("--no-calibrate", dest="calibrate", action="store_false",
+                    help="keep the automatic visiting order (no xcsum_ctx_calibrate_order)")
     ap.add_argument("--no-order-ab", dest="order_ab", action="store_false",
                     help="skip the same-run A/B of dense visiting orders (configs 2 and 4)")
     ap.add_argument("--inplace-schedule", default="auto", choices=["auto", "fused", "two_pass"],
@@ -682,6 +684,14 @@ def main():
     for k in range(args.warmup):
         step(k)
     torch.cuda.synchronize(dev)
+    # The library's once-per-context order calibration (xcsum_ctx_calibrate_order)
+    # on this rank's batch, as libxudp would run it once its UMEM is set up:
+    # the automatic order unless a forced one is >= 1 % faster on this box.
+    # Before the graph capture, which bakes the order into the launches.
+    calibrated = None
+    if args.calibrate and count and not args.geometry:
+        calibrated = eng.calibrate_order(bufs[0], d_desc, count, out_arg, cfg["mode"], flags,
+                                         len_hint, stream=sptr)
 
     # The K timed launches are captured once into a HIP graph and replayed:
     # the host enqueues one graph instead of K ctypes launches, so short
@@ -919,7 +929,13 @@ def main():
                        "visiting_order": "automatic (32 regions of 16-frame tiles if the batch "
                                          "is sparse in the UMEM, else the geometry's dense "
                                          "order: 8 regions of 16-frame tiles at MTU, 16 of "
-                                         "4-frame tiles for mixed sizes)",
+                                         "4-frame tiles for mixed sizes)"
+                       if calibrated in (None, (-1, 0)) else
+                       f"forced by xcsum_ctx_calibrate_order: 2^{calibrated[0]} regions of "
+                       f"2^{calibrated[1]}-frame tiles (>= 1 % faster than automatic here)",
+                       "order_calibration": (None if calibrated is None else
+                                             "auto" if calibrated == (-1, 0) else
+                                             f"{calibrated[0]},{calibrated[1]}"),
                        "rotating_buffers": len(bufs),
                        "alg_bytes_per_step": int(alg_all), "parallelism": f"dp{world}"},
             "pct_hbm_peak": round(100 * achieved / HBM_PEAK_GBS, 2),

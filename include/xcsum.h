@@ -112,6 +112,17 @@ int xcsum_ctx_set_launch(xcsum_ctx *ctx, int blocks_per_cu);
  * region_log2 = 0: descriptor order; -1: automatic (default).  Env
  * XCSUM_ORDER="R,T" sets it at context creation. */
 int xcsum_ctx_set_order(xcsum_ctx *ctx, int region_log2, int tile_log2);
+/* Pick the visiting order for this context by timing it on the caller's own
+ * batch (the arguments of xcsum_batch_device; it runs ~200 ordinary calls of
+ * it on `stream` and waits for them): the automatic order and five forced
+ * ones; a forced one is kept only if >= 1 % faster than the automatic one,
+ * else the order is left automatic.  *region_log2 / *tile_log2 (may be NULL)
+ * receive the choice (-1: automatic).  For a caller that sends batches of one
+ * layout (libxudp's TX UMEM): once, after the UMEM is set up.  Not while the
+ * stream is being captured (-XCSUM_ERR_INVAL). */
+int xcsum_ctx_calibrate_order(xcsum_ctx *ctx, uint8_t *d_umem, const struct xcsum_desc *d_desc,
+			      uint32_t n, uint16_t *d_out, uint32_t mode, uint32_t flags,
+			      uint32_t len_hint, void *stream, int *region_log2, int *tile_log2);
 
 /* How xcsum_batch_device writes the check fields with XCSUM_F_INPLACE
  * (results and frame bytes are identical either way):

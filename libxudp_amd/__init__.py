@@ -141,6 +141,13 @@ _SIGS = {
                                               ctypes.c_int]),
     "xcsum_ctx_set_launch": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     "xcsum_ctx_set_order": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int]),
+    "xcsum_ctx_calibrate_order": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p,
+                                                 ctypes.c_void_p, ctypes.c_uint32,
+                                                 ctypes.c_void_p, ctypes.c_uint32,
+                                                 ctypes.c_uint32, ctypes.c_uint32,
+                                                 ctypes.c_void_p,
+                                                 ctypes.POINTER(ctypes.c_int),
+                                                 ctypes.POINTER(ctypes.c_int)]),
     "xcsum_ctx_set_resident": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_uint32]),
     "xcsum_ctx_set_inplace": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     "xcsum_batch_device": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
@@ -356,6 +363,17 @@ class Engine:
     def set_order(self, region_log2=-1, tile_log2=0):
         _check(lib().xcsum_ctx_set_order(self._ctx, region_log2, tile_log2),
                "xcsum_ctx_set_order")
+
+    def calibrate_order(self, d_umem, d_desc, n, d_out, mode, flags=0, len_hint=0, stream=None):
+        """Time the visiting orders on this batch and keep the fastest
+        (xcsum_ctx_calibrate_order); returns (region_log2, tile_log2),
+        (-1, 0) = automatic.  Synchronous."""
+        r, t = ctypes.c_int(0), ctypes.c_int(0)
+        _check(lib().xcsum_ctx_calibrate_order(self._ctx, _ptr(d_umem), _ptr(d_desc), n,
+                                               _ptr(d_out), mode, flags, len_hint,
+                                               _ptr(stream), ctypes.byref(r), ctypes.byref(t)),
+               "xcsum_ctx_calibrate_order")
+        return r.value, t.value
 
     def set_inplace(self, schedule=INPLACE_AUTO):
         """how XCSUM_F_INPLACE writes the check fields (INPLACE_*)"""

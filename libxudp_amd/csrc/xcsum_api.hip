@@ -9,6 +9,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <algorithm>
 #include <new>
 #include <chrono>
 #include <mutex>
@@ -894,6 +895,92 @@ extern "C" int xcsum_batch_device(xcsum_ctx *c, uint8_t *d_umem, const struct xc
 		return 0;
 	}
 	HIPCHK(launch_csum(a, g, c->cus, (hipStream_t)stream));
+	return 0;
+}
+
+/* Calibrate the visiting order once per context, on the caller's own batch
+ * (a box whose HBM prefers another order than the ones
+ * measured here).  The automatic order and five forced ones (descriptor
+ * order; 8, 16, 4 and 32 regions of 16/16/32/16-frame tiles) each run
+ * CAL_PER back-to-back launches between two events, CAL_REPS times, in two
+ * interleaved rounds; a forced order is kept only if its best median beats
+ * the automatic order's by CAL_MARGIN, so noise (~0.3 % between repeats)
+ * never moves the choice.  The launches are ordinary xcsum_batch_device
+ * calls with the caller's arguments: results and in-place fields are what
+ * any call writes.  Synchronous. */
+static const int CAL_PER = 5, CAL_REPS = 3;
+static const double CAL_MARGIN = 0.99;
+
+extern "C" int xcsum_ctx_calibrate_order(xcsum_ctx *c, uint8_t *d_umem,
+					 const struct xcsum_desc *d_desc, uint32_t n, uint16_t *d_out,
+					 uint32_t mode, uint32_t flags, uint32_t len_hint, void *stream,
+					 int *region_log2, int *tile_log2)
+{
+	if (!c || !d_umem || !d_desc || n == 0)
+		return -XCSUM_ERR_INVAL;
+	HIPCHK(hipSetDevice(c->device));
+	hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+	HIPCHK(hipStreamIsCapturing((hipStream_t)stream, &cs));
+	if (cs != hipStreamCaptureStatusNone)
+		return -XCSUM_ERR_INVAL;   /* timing inside a capture means nothing */
+	static const int cand[][2] = {{-1, 0}, {0, 0}, {3, 4}, {4, 4}, {2, 5}, {5, 4}};
+	const int nc = (int)(sizeof(cand) / sizeof(cand[0]));
+	const int old_r = c->order_rlog, old_t = c->order_tlog;
+	float best[sizeof(cand) / sizeof(cand[0])];
+	for (int k = 0; k < nc; k++)
+		best[k] = 1e30f;
+	hipEvent_t e0 = nullptr, e1 = nullptr;
+	int rc = 0;
+	if (hipEventCreate(&e0) != hipSuccess || hipEventCreate(&e1) != hipSuccess)
+		rc = -XCSUM_ERR_HIP;
+	for (int round = 0; round < 2 && !rc; round++)
+		for (int k = 0; k < nc && !rc; k++) {
+			c->order_rlog = cand[k][0];
+			c->order_tlog = cand[k][1];
+			rc = xcsum_batch_device(c, d_umem, d_desc, n, d_out, mode, flags, len_hint,
+						stream);   /* warm-up */
+			float ms[CAL_REPS];
+			for (int r = 0; r < CAL_REPS && !rc; r++) {
+				if (hipEventRecord(e0, (hipStream_t)stream) != hipSuccess) {
+					rc = -XCSUM_ERR_HIP;
+					break;
+				}
+				for (int i = 0; i < CAL_PER && !rc; i++)
+					rc = xcsum_batch_device(c, d_umem, d_desc, n, d_out, mode, flags,
+								len_hint, stream);
+				if (rc)
+					break;
+				if (hipEventRecord(e1, (hipStream_t)stream) != hipSuccess ||
+				    hipEventSynchronize(e1) != hipSuccess ||
+				    hipEventElapsedTime(&ms[r], e0, e1) != hipSuccess)
+					rc = -XCSUM_ERR_HIP;
+			}
+			if (rc)
+				break;
+			std::sort(ms, ms + CAL_REPS);
+			best[k] = std::min(best[k], ms[CAL_REPS / 2]);
+		}
+	if (e0)
+		(void)hipEventDestroy(e0);
+	if (e1)
+		(void)hipEventDestroy(e1);
+	if (rc) {
+		c->order_rlog = old_r;
+		c->order_tlog = old_t;
+		return rc;
+	}
+	int pick = 0;
+	for (int k = 1; k < nc; k++)
+		if (best[k] < best[pick])
+			pick = k;
+	if (pick && !(best[pick] < CAL_MARGIN * best[0]))
+		pick = 0;
+	c->order_rlog = cand[pick][0];
+	c->order_tlog = cand[pick][1];
+	if (region_log2)
+		*region_log2 = c->order_rlog;
+	if (tile_log2)
+		*tile_log2 = c->order_tlog;
 	return 0;
 }
 

@@ -81,6 +81,38 @@ def test_config2_visiting_order_same_digest(torch_cuda, engine, digests, order):
     assert sha(got) == digests["config2"]["sha256_out"]
 
 
+CAL_CANDIDATES = {(-1, 0), (0, 0), (3, 4), (4, 4), (2, 5), (5, 4)}
+
+
+@pytest.mark.parametrize("umem_layout", [False, True])
+def test_config2_calibrated_order_same_digest(torch_cuda, engine, digests, umem_layout):
+    """xcsum_ctx_calibrate_order on config 2 (packed, and in xudp's slots):
+    it picks one of its candidates (automatic unless a forced order is >= 1 %
+    faster), leaves the context on it, and the output digest is unchanged;
+    refused while the stream is being captured."""
+    cfg, desc, d_desc, d_umem = device_batch(torch_cuda, engine, 2, umem_layout=umem_layout)
+    n = len(desc)
+    out = torch_cuda.empty(n, dtype=torch_cuda.int16, device="cuda:0")
+    s = torch_cuda.cuda.current_stream().cuda_stream
+    try:
+        pick = engine.calibrate_order(d_umem, d_desc, n, out, cfg["mode"], 0, 1514, stream=s)
+        assert pick in CAL_CANDIDATES, pick
+        got = run(torch_cuda, engine, d_umem, d_desc, n, cfg["mode"], 0, 1514)
+        assert sha(got) == digests["config2"]["sha256_out"], pick
+        g = torch_cuda.cuda.CUDAGraph()
+        cap = torch_cuda.cuda.Stream()
+        err = None
+        with torch_cuda.cuda.graph(g, stream=cap):
+            try:   # refused before anything is enqueued: the capture ends empty
+                engine.calibrate_order(d_umem, d_desc, n, out, cfg["mode"], 0, 1514,
+                                       stream=torch_cuda.cuda.current_stream().cuda_stream)
+            except X.XcsumError as e:
+                err = e.rc
+        assert err == -X.ERR_INVAL
+    finally:
+        engine.set_order(-1, 0)
+
+
 @pytest.mark.parametrize("cid", [2, 3, 4])
 def test_umem_layout_same_digest(torch_cuda, engine, digests, cid):
     """The same frames in xudp's 4096-byte-chunk UMEM layout: the automatic
