@@ -42,6 +42,10 @@ def main():
         lay = dict(stride=4096, offset=322 if cfg["family"] == 6 else 342)
     umem, desc = X.gen_frames_host(n, cfg["family"], cfg["pmin"], cfg["pmax"],
                                    seed=bench.SEED_BASE ^ args.config, **lay)
+    # in a mapping like libxudp's UMEM (anon_map: MAP_SHARED, no transparent
+    # huge pages), which xcsum_register_umem GPU-maps; a numpy
+    # array of this size is THP-eligible and would be staged instead
+    umem = X.as_umem(umem)
     alg = X.alg_bytes(desc, cfg["family"])
     out = np.zeros(n, dtype=np.uint16)
     eng = X.Engine(0)
@@ -68,6 +72,7 @@ def main():
             flags = X.F_INPLACE if inplace else 0
             if variant != "pageable":
                 eng.register_umem(umem)
+                assert eng.umem_mapped(umem), "registered UMEM not GPU-mapped"
             if variant == "zerocopy":
                 flags |= X.F_ZEROCOPY
             eng.batch_host(umem, desc, out, cfg["mode"], flags)  # warm-up
