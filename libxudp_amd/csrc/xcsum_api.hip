@@ -601,8 +601,12 @@ extern "C" int xcsum_ctx_create(int device, xcsum_ctx **out)
 		c->inplace_sched = strcmp(e, "fused") == 0      ? XCSUM_INPLACE_FUSED
 				   : strcmp(e, "two_pass") == 0 ? XCSUM_INPLACE_TWO_PASS
 								: XCSUM_INPLACE_AUTO;
-	/* XCSUM_INPLACE_BLOCK=0|32|64: the second pass's store width (A/B) */
-	c->inplace_block = 32;
+	/* XCSUM_INPLACE_BLOCK=0|32|64: the second pass's store width (A/B);
+	 * 2-byte stores measured fastest in every case (config 2 0.348 vs
+	 * 0.364 / 0.353 ms for 32 / 64, config 4 0.332 vs 0.342 / 0.345, xudp's
+	 * slots likewise; profiles/r04/inplace/r04wxy_two_pass_widths.txt): the
+	 * whole-block variants load the block first */
+	c->inplace_block = 0;
 	if (const char *e = getenv("XCSUM_INPLACE_BLOCK"))
 		c->inplace_block = (uint32_t)atoi(e) == 64 ? 64u : (uint32_t)atoi(e) == 32 ? 32u : 0u;
 	c->inplace_tl = 1;

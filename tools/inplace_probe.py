@@ -17,6 +17,11 @@ frames, packed (1520-B stride) or in xudp's 4096-B slots, 1M frames in a
                   no load first (after the read pass, or alone)
   [read+]copy64   the 64-B blocks holding the fields copied whole from a
                   compact side array (a first pass's saved blocks)
+  lib_plain+X     the library's plain pass, then second pass X (copy64,
+                  blind64, w2)
+  lib_two_pass_wW[_out]  the library's TWO_PASS schedule with second-pass
+                  store width W (XCSUM_INPLACE_BLOCK; 0: 2-byte stores);
+                  _out: with a result array (no scratch)
   fused_blkW      the read, each W-byte block holding a field stored back
                   whole by the wave that read it (W = 16/32/64/128)
   lib_fused_tl2/4 the library's fused pass with each frame's first 2 / 4
@@ -139,9 +144,39 @@ def main():
                                      stream=sp)
             return 0
         return f
+    engs_blk = {}
+    for w in (0, 32, 64):
+        os.environ["XCSUM_INPLACE_BLOCK"] = str(w)
+        engs_blk[w] = X.Engine(0)
+        engs_blk[w].set_inplace(X.INPLACE_TWO_PASS)
+    del os.environ["XCSUM_INPLACE_BLOCK"]
+
+    def lib_blk(w, o):
+        def f(b):
+            engs_blk[w].batch_device(b, d_desc, len(desc), o, mode, X.F_INPLACE | iph, 1500,
+                                     stream=sp)
+            return 0
+        return f
+    for w in (0, 32, 64):
+        legs[f"lib_two_pass_w{w}"] = lib_blk(w, None)
+        legs[f"lib_two_pass_w{w}_out"] = lib_blk(w, out)
     legs["lib_fused_tl2"] = lib_tl(2)
     legs["lib_fused_tl4"] = lib_tl(4)
     legs["lib_plain"] = lib(X.INPLACE_AUTO, iph, out)
+
+    def lib_plain_then(second):
+        def f(b):
+            eng.set_inplace(X.INPLACE_AUTO)
+            eng.batch_device(b, d_desc, len(desc), out, mode, iph, 1500, stream=sp)
+            return second(b)
+        return f
+    legs["lib_plain+copy64"] = lib_plain_then(lambda b: L.probe_stream_read_copy(
+        b, nb, fstride, a0, len(a), f1, f2, side.data_ptr(), side.numel(), scratch.data_ptr(),
+        blocks, 0, sp))
+    legs["lib_plain+blind64"] = lib_plain_then(lambda b: L.probe_stream_read_blind(
+        b, nb, fstride, a0, len(a), f1, f2, scratch.data_ptr(), blocks, 64, 0, sp))
+    legs["lib_plain+w2"] = lib_plain_then(lambda b: L.probe_scatter_fields(
+        b, nb, fstride, a0, len(a), f1, f2, blocks, sp))
     legs["lib_fused"] = lib(X.INPLACE_FUSED, X.F_INPLACE | iph, None)
     legs["lib_two_pass"] = lib(X.INPLACE_TWO_PASS, X.F_INPLACE | iph, None)
     if args.legs:
