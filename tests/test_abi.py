@@ -133,6 +133,10 @@ def test_argument_validation_without_gpu():
         == -X.ERR_INVAL
     assert L.xcsum_unregister_umem(None, None) == -X.ERR_INVAL
     assert L.xudp_packet_udp_batch(None, None, 0, 0) == 0       # empty batch is a no-op
+    r, t = ctypes.c_int(7), ctypes.c_int(7)
+    assert L.xcsum_ctx_calibrate_order(None, None, None, 1, None, 0, 0, 0, None,
+                                       ctypes.byref(r), ctypes.byref(t)) == -X.ERR_INVAL
+    assert (r.value, t.value) == (7, 7)                         # untouched on error
 
 
 def test_geometry_list_matches_kernel_source():
