@@ -84,6 +84,7 @@ def test_config2_visiting_order_same_digest(torch_cuda, engine, digests, order):
 CAL_CANDIDATES = {(-1, 0), (0, 0), (3, 4), (4, 4), (2, 5), (5, 4)}
 
 
+@pytest.mark.filterwarnings("ignore:The CUDA Graph is empty")
 @pytest.mark.parametrize("umem_layout", [False, True])
 def test_config2_calibrated_order_same_digest(torch_cuda, engine, digests, umem_layout):
     """xcsum_ctx_calibrate_order on config 2 (packed, and in xudp's slots):
