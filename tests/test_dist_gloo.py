@@ -1,4 +1,4 @@
-"""CPU, world_size 2 (gloo): the multi-GPU path's partitioning, exercised
+"""CPU, world_size 2 and 8 (gloo): the multi-GPU path's partitioning, exercised
 exactly as bench.py does it (rank_slice -> per-rank generation -> per-rank
 checksums, no data-path collective), checked against one single-process run.
 Only the timing reduction (MAX of elapsed) and the byte count (SUM) cross
@@ -51,30 +51,43 @@ def worker(rank, world, port, q):
     dist.destroy_process_group()
 
 
-def test_two_rank_partition_matches_single_process():
-    world = 2
+@pytest.mark.parametrize("world", [2, 8])
+def test_partition_matches_single_process(world):
+    """world 2, and 8 as in the driver's 8-GPU run (gloo processes on the CPU)"""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = free_port()
     procs = [ctx.Process(target=worker, args=(r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()
-    got = dict(q.get(timeout=120) for _ in range(world))
+    got = dict(q.get(timeout=180) for _ in range(world))
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    # strong scaling (config-5 style): shards tile the job, outputs concatenate
-    first0, out0, tmax, sums = got[0]["strong"]
-    first1, out1, _, _ = got[1]["strong"]
-    assert first0 == 0 and first1 == len(out0) and tmax == 2.0
+    # strong scaling (config-5 style): shards tile the job in rank order,
+    # outputs concatenate to the single-process run, byte counts sum
+    firsts = [got[r]["strong"][0] for r in range(world)]
+    outs = [got[r]["strong"][1] for r in range(world)]
+    assert firsts == [int(sum(len(o) for o in outs[:r])) for r in range(world)]
+    assert all(got[r]["strong"][2] == float(world) for r in range(world))   # MAX over ranks
     whole = rank_outputs(CFG_SMALL, 0, 1)
-    assert np.array_equal(np.concatenate([out0, out1]), whole[1])
-    assert sums == [float(whole[2]), float(CFG_SMALL["n"])]
+    assert np.array_equal(np.concatenate(outs), whole[1])
+    assert got[0]["strong"][3] == [float(whole[2]), float(CFG_SMALL["n"])]
+    # byte-balanced: no shard carries more than its share plus one frame
+    per = [float(X.alg_bytes(*_shard_desc(CFG_SMALL, r, world))) for r in range(world)]
+    assert max(per) - min(per) <= 2 * (CFG_SMALL["pmax"] + 16)
     # weak scaling: each rank owns its own n frames, rank r starts at r*n
-    assert got[0]["weak"][0] == 0 and got[1]["weak"][0] == CFG_WEAK["n"]
-    big = dict(CFG_WEAK, n=2 * CFG_WEAK["n"])
+    assert [got[r]["weak"][0] for r in range(world)] == [r * CFG_WEAK["n"] for r in range(world)]
+    big = dict(CFG_WEAK, n=world * CFG_WEAK["n"])
     whole = rank_outputs(big, 0, 1)
-    assert np.array_equal(np.concatenate([got[0]["weak"][1], got[1]["weak"][1]]), whole[1])
+    assert np.array_equal(np.concatenate([got[r]["weak"][1] for r in range(world)]), whole[1])
+
+
+def _shard_desc(cfg, rank, world):
+    first, count = bench.rank_slice(cfg, rank, world)
+    desc, _ = X.gen_layout(count, cfg["family"], cfg["pmin"], cfg["pmax"],
+                           seed=bench.SEED_BASE ^ cfg["id"], first_index=first)
+    return desc, cfg["family"]
 
 
 def test_bench_helpers_present_and_real_bytes():
