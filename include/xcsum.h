@@ -113,10 +113,11 @@ int xcsum_ctx_set_launch(xcsum_ctx *ctx, int blocks_per_cu);
  * XCSUM_ORDER="R,T" sets it at context creation. */
 int xcsum_ctx_set_order(xcsum_ctx *ctx, int region_log2, int tile_log2);
 /* Pick the visiting order for this context by timing it on the caller's own
- * batch (the arguments of xcsum_batch_device; it runs ~200 ordinary calls of
- * it on `stream` and waits for them): the automatic order and five forced
- * ones; a forced one is kept only if >= 1 % faster than the automatic one,
- * else the order is left automatic.  *region_log2 / *tile_log2 (may be NULL)
+ * batch (the arguments of xcsum_batch_device; it runs ordinary calls of it on
+ * `stream` -- ~60 ms to bring the clocks up, then three rounds of the
+ * automatic order and five forced ones, each ~6 ms -- and waits for them); a
+ * forced order is kept only if >= 1 % faster than the automatic one in every
+ * round, else the order is left automatic.  *region_log2 / *tile_log2 (may be NULL)
  * receive the choice (-1: automatic).  For a caller that sends batches of one
  * layout (libxudp's TX UMEM): once, after the UMEM is set up.  Not while the
  * stream is being captured (-XCSUM_ERR_INVAL). */

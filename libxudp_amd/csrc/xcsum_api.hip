@@ -904,16 +904,21 @@ extern "C" int xcsum_batch_device(xcsum_ctx *c, uint8_t *d_umem, const struct xc
 
 /* Calibrate the visiting order once per context, on the caller's own batch
  * (a box whose HBM prefers another order than the ones
- * measured here).  The automatic order and five forced ones (descriptor
- * order; 8, 16, 4 and 32 regions of 16/16/32/16-frame tiles) each run
- * CAL_PER back-to-back launches between two events, CAL_REPS times, in two
- * interleaved rounds; a forced order is kept only if its best median beats
- * the automatic order's by CAL_MARGIN, so noise (~0.3 % between repeats)
- * never moves the choice.  The launches are ordinary xcsum_batch_device
- * calls with the caller's arguments: results and in-place fields are what
- * any call writes.  Synchronous. */
-static const int CAL_PER = 5, CAL_REPS = 3;
-static const double CAL_MARGIN = 0.99;
+ * measured here).  First the clocks are brought up (>= CAL_WARM_MS of
+ * back-to-back calls: a cold GPU runs its first ~100 ms slow, which would
+ * reward whichever order happens to run later).  Then the automatic order
+ * and five forced ones (descriptor order; 8, 16, 4 and 32 regions of
+ * 16/16/32/16-frame tiles) are timed in CAL_ROUNDS rounds, each round in a
+ * rotated sequence; a time is the median of CAL_REPS samples of >= CAL_SAMPLE_MS
+ * of back-to-back calls between two events.  A forced order is kept only if
+ * it beats the automatic one by CAL_MARGIN in every round (noise between
+ * repeats is ~0.3 %; a kernel the order does not affect, like the
+ * small-frame stream kernel, never qualifies).  The calls are ordinary
+ * xcsum_batch_device calls with the caller's arguments: results and
+ * in-place fields are what any call writes.  Synchronous. */
+static const int CAL_ROUNDS = 3, CAL_REPS = 3;
+static const float CAL_WARM_MS = 60.0f, CAL_SAMPLE_MS = 2.0f;
+static const float CAL_MARGIN = 0.99f;
 
 extern "C" int xcsum_ctx_calibrate_order(xcsum_ctx *c, uint8_t *d_umem,
 					 const struct xcsum_desc *d_desc, uint32_t n, uint16_t *d_out,
@@ -928,41 +933,55 @@ extern "C" int xcsum_ctx_calibrate_order(xcsum_ctx *c, uint8_t *d_umem,
 	if (cs != hipStreamCaptureStatusNone)
 		return -XCSUM_ERR_INVAL;   /* timing inside a capture means nothing */
 	static const int cand[][2] = {{-1, 0}, {0, 0}, {3, 4}, {4, 4}, {2, 5}, {5, 4}};
-	const int nc = (int)(sizeof(cand) / sizeof(cand[0]));
+	constexpr int NC = (int)(sizeof(cand) / sizeof(cand[0]));
 	const int old_r = c->order_rlog, old_t = c->order_tlog;
-	float best[sizeof(cand) / sizeof(cand[0])];
-	for (int k = 0; k < nc; k++)
-		best[k] = 1e30f;
 	hipEvent_t e0 = nullptr, e1 = nullptr;
 	int rc = 0;
 	if (hipEventCreate(&e0) != hipSuccess || hipEventCreate(&e1) != hipSuccess)
 		rc = -XCSUM_ERR_HIP;
-	for (int round = 0; round < 2 && !rc; round++)
-		for (int k = 0; k < nc && !rc; k++) {
+	/* ms per call over `per` back-to-back calls */
+	auto sample = [&](int per, float *ms) -> int {
+		if (hipEventRecord(e0, (hipStream_t)stream) != hipSuccess)
+			return -XCSUM_ERR_HIP;
+		for (int i = 0; i < per; i++) {
+			const int r = xcsum_batch_device(c, d_umem, d_desc, n, d_out, mode, flags,
+							 len_hint, stream);
+			if (r)
+				return r;
+		}
+		float t = 0;
+		if (hipEventRecord(e1, (hipStream_t)stream) != hipSuccess ||
+		    hipEventSynchronize(e1) != hipSuccess || hipEventElapsedTime(&t, e0, e1) != hipSuccess)
+			return -XCSUM_ERR_HIP;
+		*ms = t / (float)per;
+		return 0;
+	};
+	float t1 = 0;
+	int per = 1;
+	c->order_rlog = -1;
+	c->order_tlog = 0;
+	if (!rc)
+		rc = sample(3, &t1);
+	if (!rc) {
+		t1 = std::max(t1, 1e-4f);
+		per = (int)std::min(2000.0f, std::max(3.0f, CAL_SAMPLE_MS / t1 + 1.0f));
+		const int warm = (int)std::min(20000.0f, CAL_WARM_MS / t1 + 1.0f);
+		rc = sample(warm, &t1);
+	}
+	float ms[CAL_ROUNDS][NC];
+	for (int round = 0; round < CAL_ROUNDS && !rc; round++)
+		for (int j = 0; j < NC && !rc; j++) {
+			const int k = (j + round) % NC;
 			c->order_rlog = cand[k][0];
 			c->order_tlog = cand[k][1];
-			rc = xcsum_batch_device(c, d_umem, d_desc, n, d_out, mode, flags, len_hint,
-						stream);   /* warm-up */
-			float ms[CAL_REPS];
-			for (int r = 0; r < CAL_REPS && !rc; r++) {
-				if (hipEventRecord(e0, (hipStream_t)stream) != hipSuccess) {
-					rc = -XCSUM_ERR_HIP;
-					break;
-				}
-				for (int i = 0; i < CAL_PER && !rc; i++)
-					rc = xcsum_batch_device(c, d_umem, d_desc, n, d_out, mode, flags,
-								len_hint, stream);
-				if (rc)
-					break;
-				if (hipEventRecord(e1, (hipStream_t)stream) != hipSuccess ||
-				    hipEventSynchronize(e1) != hipSuccess ||
-				    hipEventElapsedTime(&ms[r], e0, e1) != hipSuccess)
-					rc = -XCSUM_ERR_HIP;
+			float rep[CAL_REPS];
+			rc = sample(1, &rep[0]);   /* the new order's first call */
+			for (int r = 0; r < CAL_REPS && !rc; r++)
+				rc = sample(per, &rep[r]);
+			if (!rc) {
+				std::sort(rep, rep + CAL_REPS);
+				ms[round][k] = rep[CAL_REPS / 2];
 			}
-			if (rc)
-				break;
-			std::sort(ms, ms + CAL_REPS);
-			best[k] = std::min(best[k], ms[CAL_REPS / 2]);
 		}
 	if (e0)
 		(void)hipEventDestroy(e0);
@@ -974,11 +993,19 @@ extern "C" int xcsum_ctx_calibrate_order(xcsum_ctx *c, uint8_t *d_umem,
 		return rc;
 	}
 	int pick = 0;
-	for (int k = 1; k < nc; k++)
-		if (best[k] < best[pick])
+	float pick_sum = 0;
+	for (int k = 1; k < NC; k++) {
+		bool wins = true;
+		float sum = 0;
+		for (int round = 0; round < CAL_ROUNDS; round++) {
+			wins = wins && ms[round][k] < CAL_MARGIN * ms[round][0];
+			sum += ms[round][k];
+		}
+		if (wins && (!pick || sum < pick_sum)) {
 			pick = k;
-	if (pick && !(best[pick] < CAL_MARGIN * best[0]))
-		pick = 0;
+			pick_sum = sum;
+		}
+	}
 	c->order_rlog = cand[pick][0];
 	c->order_tlog = cand[pick][1];
 	if (region_log2)
