@@ -730,6 +730,13 @@ static void set_order(const xcsum_ctx *c, CsumArgs &a, const Geometry &g)
 		return;
 	}
 	a.ord = order_regions(a.n, 5, 4);
+	/* in place over a sparse batch (libxudp's TX call on its slots): fewer
+	 * regions -- in place + IPHDR 16 regions of 32-frame tiles, IPv6 and
+	 * IPv4 without IPHDR 8 of 16: 0.3522 -> 0.3467, 0.3533 -> 0.3440 and
+	 * 0.3537 -> 0.3472 ms (plain: no order better than 32 x 16; same box,
+	 * alternating, profiles/r04/check/r04so_slot_orders.txt) */
+	if ((a.flags & XCSUM_F_INPLACE) && g.G == 16 && g.U == 2 && g.K == 6)
+		a.ord = (a.flags & XCSUM_F_IPHDR) ? order_regions(a.n, 4, 5) : order_regions(a.n, 3, 4);
 	if (g.G == 16 && g.U == 2 && g.K == 6)
 		a.dense = order_regions(a.n, 3, 4);
 	else if (g.G == 16 && g.U == 1 && (g.K == 2 || g.K == 3))
@@ -907,8 +914,8 @@ extern "C" int xcsum_batch_device(xcsum_ctx *c, uint8_t *d_umem, const struct xc
  * measured here).  First the clocks are brought up (>= CAL_WARM_MS of
  * back-to-back calls: a cold GPU runs its first ~100 ms slow, which would
  * reward whichever order happens to run later).  Then the automatic order
- * and five forced ones (descriptor order; 8, 16, 4 and 32 regions of
- * 16/16/32/16-frame tiles) are timed in CAL_ROUNDS rounds, each round in a
+ * and six forced ones (descriptor order; 8, 16, 4, 32 and 16 regions of
+ * 16/16/32/16/32-frame tiles) are timed in CAL_ROUNDS rounds, each round in a
  * rotated sequence; a time is the median of CAL_REPS samples of >= CAL_SAMPLE_MS
  * of back-to-back calls between two events.  A forced order is kept only if
  * it beats the automatic one by CAL_MARGIN in every round (noise between
@@ -932,7 +939,7 @@ extern "C" int xcsum_ctx_calibrate_order(xcsum_ctx *c, uint8_t *d_umem,
 	HIPCHK(hipStreamIsCapturing((hipStream_t)stream, &cs));
 	if (cs != hipStreamCaptureStatusNone)
 		return -XCSUM_ERR_INVAL;   /* timing inside a capture means nothing */
-	static const int cand[][2] = {{-1, 0}, {0, 0}, {3, 4}, {4, 4}, {2, 5}, {5, 4}};
+	static const int cand[][2] = {{-1, 0}, {0, 0}, {3, 4}, {4, 4}, {2, 5}, {5, 4}, {4, 5}};
 	constexpr int NC = (int)(sizeof(cand) / sizeof(cand[0]));
 	const int old_r = c->order_rlog, old_t = c->order_tlog;
 	hipEvent_t e0 = nullptr, e1 = nullptr;
