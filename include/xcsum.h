@@ -110,8 +110,9 @@ int xcsum_ctx_set_launch(xcsum_ctx *ctx, int blocks_per_cu);
  * round-robin from 2^region_log2 equal regions, so the frames in flight come
  * from regions spread over the whole UMEM rather than one window.
  * region_log2 = 0: descriptor order; -1: automatic (default: per geometry
- * for dense batches; for batches sparse in the UMEM 32 regions of 16-frame
- * tiles, in place at MTU 16 of 32 with XCSUM_F_IPHDR, else 8 of 16).  Env
+ * for dense batches, descriptor order with XCSUM_F_VERIFY at MTU; for
+ * batches sparse in the UMEM 32 regions of 16-frame tiles, in place at MTU
+ * 16 of 32 with XCSUM_F_IPHDR, else 8 of 16).  Env
  * XCSUM_ORDER="R,T" sets it at context creation. */
 int xcsum_ctx_set_order(xcsum_ctx *ctx, int region_log2, int tile_log2);
 /* Pick the visiting order for this context by timing it on the caller's own
