@@ -1,6 +1,6 @@
 #!/bin/bash
-# (Historical: needs libxudp_amd/variants/head/libxcsum.so built from the commit before
-# 784a479, which is not kept in the tree; it produced profiles/r04/inplace/r04n_*.)
+# (Historical: needs libxudp_amd/variants/head/libxcsum.so built from commit
+# 38cefbc, not kept in the tree; it produced profiles/r04/inplace/r04n_* and r04p_*.)
 # Same-box A/B of the in-place passes: HEAD's library (variants/head) vs the
 # working tree's, alternating bench runs, then the interleaved probe.
 set -u
