@@ -57,7 +57,8 @@ CONFIGS = {
             name="8M x U[64,9000]B UDP/IPv4 sharded by bytes over the GPUs (BASELINE config 5)"),
 }
 MODE_NAMES = {0: "v4_legacy", 1: "v4_rfc", 2: "v6", 3: "auto"}
-FLAG_NAMES = {"inplace": X.F_INPLACE, "iphdr": X.F_IPHDR, "rfc": X.F_V4_RFC, "verify": X.F_VERIFY}
+FLAG_NAMES = {"inplace": X.F_INPLACE, "iphdr": X.F_IPHDR, "rfc": X.F_V4_RFC, "verify": X.F_VERIFY,
+              "iphdr_only": X.F_IPHDR_ONLY}
 
 
 def parse_flags(text):
@@ -74,7 +75,13 @@ def alg_bytes_flags(desc, family, flags, with_out):
     """Algorithmic bytes of one launch: the span read (UDP
     length + pseudo-header addresses), plus with XCSUM_F_IPHDR on IPv4 the 12
     header bytes before the addresses; writes: the 2-byte result when there
-    is a result array, and every 2-byte check field written in place."""
+    is a result array, and every 2-byte check field written in place.
+    XCSUM_F_IPHDR_ONLY: 20 header bytes read per frame, nothing else."""
+    if flags & X.F_IPHDR_ONLY:
+        # libxudp's IPv4 TX call: the 20-byte header read, iph->check written
+        # (in place and/or into the result array); no payload byte
+        inplace = (flags & X.F_INPLACE) and not (flags & X.F_VERIFY)
+        return len(desc) * (20 + 2 * ((1 if with_out else 0) + (1 if inplace else 0)))
     span = X.alg_bytes(desc, family) - 2 * len(desc)
     v4 = family == 4
     read = span + (12 * len(desc) if (flags & X.F_IPHDR) and v4 else 0)
@@ -270,26 +277,30 @@ def host_cpu_facts():
     return facts
 
 
-def cpu_baseline(cfg, seconds=15.0):
+def cpu_baseline(cfg, seconds=15.0, flags=0):
     """The reference checksum.h timed on this host over a bounded sample:
     1 thread, 16 threads and os.cpu_count() threads (static frame partition).
     Each leg first runs one untimed repetition (thread creation, caches), then
-    one timed repetition sizes the leg to its share of `seconds`."""
+    one timed repetition sizes the leg to its share of `seconds`.  With
+    XCSUM_F_IPHDR_ONLY: the reference's xudp_checksum_half (packet.c:43-66,
+    ref_batch mode 4), 22 algorithmic bytes per frame as on the GPU."""
     import oracle  # test infrastructure, used here only as the CPU baseline
     seed = SEED_BASE ^ cfg["id"]
     m = min(cfg["n"], 1 << 16)
     umem, desc = X.gen_frames_host(m, cfg["family"], cfg["pmin"], cfg["pmax"], seed=seed)
     out = np.zeros(m, dtype=np.uint16)
-    alg = X.alg_bytes(desc, cfg["family"])
-    mode = 2 if cfg["family"] == 6 else 0
+    hdr_only = bool(flags & X.F_IPHDR_ONLY)
+    alg = 22 * m if hdr_only else X.alg_bytes(desc, cfg["family"])
+    mode = 4 if hdr_only else 2 if cfg["family"] == 6 else 0
     if oracle.have_ref():
         kind, L = "reference", oracle.ref()
         timed = lambda th, reps: L.ref_batch_timed(umem.ctypes.data, desc.ctypes.data, m,
                                                    out.ctypes.data, mode, th, reps)
     else:
         kind, L = "port", oracle.port()
+        pmode, pflags = (0, X.F_IPHDR_ONLY) if hdr_only else (mode, 0)
         timed = lambda th, reps: L.orc_batch_timed(umem.ctypes.data, desc.ctypes.data, m,
-                                                   out.ctypes.data, mode, 0, th, reps)
+                                                   out.ctypes.data, pmode, pflags, th, reps)
     facts = host_cpu_facts()
     usable = min(v for v in (facts.get("affinity_cpus"), facts.get("cgroup_cpu_quota"),
                              facts.get("host_cpus")) if v)
@@ -313,8 +324,10 @@ def cpu_baseline(cfg, seconds=15.0):
         res[th] = alg * reps / t / 2**30
         secs[th] = round(t, 3)
     total = time.perf_counter() - t_start
-    exp = oracle.ref_batch(umem, desc, mode) if kind == "reference" else oracle.batch(umem, desc,
-                                                                                        mode)
+    if kind == "reference":
+        exp = oracle.ref_batch(umem, desc, mode)
+    else:
+        exp = oracle.batch(umem, desc, 0 if hdr_only else mode, X.F_IPHDR_ONLY if hdr_only else 0)
     assert np.array_equal(out, exp)
     best_th = max(res, key=lambda k: res[k])
     legs_txt = ", ".join(f"{th} thread{'s' if th > 1 else ''} {secs[th]:.1f} s"
@@ -325,7 +338,7 @@ def cpu_baseline(cfg, seconds=15.0):
             "seconds_total": round(total, 2),
             "value_1core": round(res[1], 3), **facts,
             "sample": f"{m} frames of the same config ({alg / 1e6:.1f} MB algorithmic), "
-                      f"xudp/checksum.h {'udp_csum6' if mode == 2 else 'udp_checksum'} compiled "
+                      f"xudp/{'packet.c xudp_checksum_half' if hdr_only else 'checksum.h udp_csum6' if mode == 2 else 'checksum.h udp_checksum'} compiled "
                       f"-O2 from the reference, static frame partition; timed legs: {legs_txt} "
                       f"({total:.1f} s in all with the warm-up and sizing runs); "
                       f"{usable:g} CPUs usable by this job (affinity / cgroup quota), so "
@@ -343,7 +356,7 @@ def pmc_traffic(cid, layout, flags, sha):
     traffic is null and the reason says which code the counters came from.
     Returns (bytes, source, reason, kernel hash)."""
     tag = f"{'_umem' if layout == 'umem' else ''}{'_f%x' % flags if flags else ''}"
-    for rnd in ("r04", "r03", "r02", "r01", ""):
+    for rnd in ("r05", "r04", "r03", "r02", "r01", ""):
         path = os.path.join(ROOT, "profiles", rnd, f"pmc_config{cid}{tag}.json")
         if not os.path.exists(path):
             continue
@@ -387,15 +400,20 @@ def gpu_clocks(dev):
         return None
 
 
-def real_bytes(desc):
+def real_bytes(desc, flags=0):
     """HBM bytes a launch cannot avoid: the union of the 64-byte lines the
     frames touch, plus the 16-byte descriptor and the 2-byte result of every
-    frame."""
+    frame.  XCSUM_F_IPHDR_ONLY touches only the lines of the IPv4 header
+    [eth+14, eth+34)."""
     if len(desc) == 0:
         return 0
     a = desc["addr"].astype(np.int64)
-    lo = a // 64
-    hi = (a + desc["len"].astype(np.int64) + 63) // 64
+    if flags & X.F_IPHDR_ONLY:
+        lo = (a + 14) // 64
+        hi = (a + 34 + 63) // 64
+    else:
+        lo = a // 64
+        hi = (a + desc["len"].astype(np.int64) + 63) // 64
     order = np.argsort(lo, kind="stable")
     lo, hi = lo[order], hi[order]
     reach = np.maximum.accumulate(hi)
@@ -523,18 +541,24 @@ ORDER_AB = [(0, 0), (3, 4), (4, 4), (2, 5)]
 
 
 def order_ab(torch, dev, eng, bufs, d_desc, count, out_arg, cfg, flags, len_hint, sptr,
-             real, ceiling_gbps, per=10, reps=6):
+             real, ceiling_gbps, calibrated=None, per=10, reps=6):
     """Same-run A/B of dense visiting orders on the timed workload: for each
     order in ORDER_AB and the automatic one, `per` back-to-back eager launches
     between two events, median of `reps` - 1 (the first is a warm-up); the
     per-launch time and its fraction of the same-run stream-read ceiling (real
-    bytes, as roofline.frac_vs_ceiling).  Leaves the automatic order set."""
+    bytes, as roofline.frac_vs_ceiling).  `calibrated`: the order
+    xcsum_ctx_calibrate_order picked for the timed run, (-1, 0) = automatic;
+    a forced pick outside ORDER_AB gets its own leg, and the line says which
+    leg the timed run used.  Leaves the timed run's order set."""
     s = torch.cuda.current_stream(dev)
     best_ms = {}
+    legs = [None] + ORDER_AB
+    if calibrated not in (None, (-1, 0)) and tuple(calibrated) not in ORDER_AB:
+        legs.append(tuple(calibrated))
     # two rounds with the legs interleaved, the lower median of each leg:
     # the first leg measured after the ceiling probe ran ~10 % slow once
     for rnd in range(2):
-        for order in [None] + ORDER_AB:
+        for order in legs:
             if order is None:
                 eng.set_order(-1, 0)
             else:
@@ -557,16 +581,21 @@ def order_ab(torch, dev, eng, bufs, d_desc, count, out_arg, cfg, flags, len_hint
         res[key] = {"ms": round(ms, 4)}
         if ceiling_gbps:
             res[key]["frac_vs_ceiling"] = round(real / (ms * 1e-3) / 1e9 / ceiling_gbps, 4)
-    eng.set_order(-1, 0)
+    timed_leg = "auto" if calibrated in (None, (-1, 0)) else f"{calibrated[0]},{calibrated[1]}"
+    if timed_leg == "auto":
+        eng.set_order(-1, 0)
+    else:
+        eng.set_order(*calibrated)
     best = min(res, key=lambda k: res[k]["ms"])
-    return {"orders": res, "fastest": best,
+    return {"orders": res, "fastest": best, "timed_run_order": timed_leg,
             "auto_vs_fastest": round(res[best]["ms"] / res["auto"]["ms"], 4),
+            "timed_vs_fastest": round(res[best]["ms"] / res[timed_leg]["ms"], 4),
             "what": f"{per} back-to-back eager launches per order between two events, median "
                     f"of {reps - 1}, the lower of two interleaved rounds; R,T = 2^R regions of "
                     f"2^T-frame tiles (0,0 = descriptor order), auto = the library's choice"}
 
 
-def digest_check(cfg, out, count, world, rank, dist, sdev):
+def digest_check(cfg, out, count, world, rank, dist, sdev, field="sha256_out"):
     """SHA-256 of the timed output against the digest the REFERENCE produced
     over the same synthetic frames (tests/golden/digests.json, made by
     tests/golden/make_golden.py with the compiled checksum.h).  Config 5 is
@@ -578,7 +607,7 @@ def digest_check(cfg, out, count, world, rank, dist, sdev):
     key = f"config{cfg['id']}"
     if not os.path.exists(path):
         return None
-    want = json.load(open(path)).get(key, {}).get("sha256_out")
+    want = json.load(open(path)).get(key, {}).get(field)
     if not want:
         return None
     import torch
@@ -595,12 +624,12 @@ def digest_check(cfg, out, count, world, rank, dist, sdev):
         if rank != 0:
             return None
         blob = b"".join(d2h(torch, p[:2 * int(c)]).tobytes() for p, c in zip(parts, cnts))
-        what = f"{key} sha256_out over the concatenated outputs of {world} ranks"
+        what = f"{key} {field} over the concatenated outputs of {world} ranks"
     else:
         if rank != 0:
             return None
         blob = d2h(torch, mine).tobytes()
-        what = f"{key} sha256_out over rank 0's timed output"
+        what = f"{key} {field} over rank 0's timed output"
     return {"ok": hashlib.sha256(blob).hexdigest() == want, "what": what}
 
 
@@ -803,14 +832,14 @@ def main():
     ceiling = inplace = orders = None
     if rank == 0 and not args.no_ceiling:
         ceiling = stream_ceiling(torch, dev, bufs, sptr)
-        if flags & X.F_INPLACE and with_out is False:
+        if flags & X.F_INPLACE and with_out is False and not flags & X.F_IPHDR_ONLY:
             inplace = inplace_ceiling(torch, dev, bufs, desc, flags, cfg["family"], sptr)
         if args.order_ab and cfg["id"] in (2, 4) and not flags and not args.geometry:
             # after the in-place probe (none here: no flags), before the
             # parity pass: the order never changes results
             orders = order_ab(torch, dev, eng, bufs, d_desc, count, out_arg, cfg, flags,
-                              len_hint, sptr, real_bytes(desc),
-                              ceiling["GBps"] if ceiling else None)
+                              len_hint, sptr, real_bytes(desc, flags),
+                              ceiling["GBps"] if ceiling else None, calibrated)
 
     if not with_out and count:
         # the in-place passes rewrote the check fields of every buffer (and the
@@ -833,7 +862,19 @@ def main():
         got = d2h(torch, out[:m]).view(np.uint16)
         ubytes = int(desc["addr"][m - 1]) + int(desc["len"][m - 1])
         hu = d2h(torch, bufs[0][:ubytes])
-        if flags & X.F_INPLACE and not flags & X.F_VERIFY:
+        if flags & X.F_INPLACE and not flags & X.F_VERIFY and flags & X.F_IPHDR_ONLY:
+            # libxudp's IPv4 call: iph->check written, udp->check still 0
+            fresh = hu.copy()
+            for k in range(m):
+                a0 = int(desc["addr"][k])
+                fresh[a0 + 24:a0 + 26] = 0
+            exp = oracle.batch(fresh, desc[:m], cfg["mode"], flags & ~X.F_INPLACE)
+            ok = bool(np.array_equal(got, exp))
+            for k in range(m):
+                a0 = int(desc["addr"][k])
+                ok = ok and int(hu[a0 + 24:a0 + 26].view("<u2")[0]) == int(exp[k]) \
+                    and not hu[a0 + 40:a0 + 42].any()
+        elif flags & X.F_INPLACE and not flags & X.F_VERIFY:
             fresh = hu.copy()
             off = 60 if cfg["family"] == 6 else 40
             for k in range(m):       # the pristine frames, check fields 0
@@ -851,8 +892,10 @@ def main():
                     ok = ok and int(hu[a0 + 24:a0 + 26].view("<u2")[0]) == oracle.ip_header_rfc(f)
         else:
             ok = bool(np.array_equal(got, oracle.batch(hu, desc[:m], cfg["mode"], flags)))
-    digest = None if flags & X.F_VERIFY else digest_check(cfg, out, count, world, rank, dist,
-                                                          sdev)
+    # IPHDR_ONLY: the reference's xudp_checksum_half over the same frames
+    digest = None if flags & X.F_VERIFY else digest_check(
+        cfg, out, count, world, rank, dist, sdev,
+        "sha256_iphdr" if flags & X.F_IPHDR_ONLY else "sha256_out")
 
     parity_ok = True
     if rank == 0:
@@ -872,7 +915,7 @@ def main():
         # bytes the kernel must move per launch (every 64-byte line holding a
         # frame byte, once, + 16-byte descriptors + 2-byte results): the
         # apples-to-apples numerator for the stream-read ceiling
-        real = real_bytes(desc)
+        real = real_bytes(desc, flags)
         roof["real_bytes_per_launch"] = real
         roof["real_achieved"] = round(real / (kern_ms * 1e-3) / 1e9, 1)
         if ceiling:
@@ -902,7 +945,10 @@ def main():
         parity_ok = ok is not False and (digest is None or digest.get("ok") is not False)
         fl = ",".join(k for k, v in FLAG_NAMES.items() if flags & v)
         line = {
-            "metric": ("device-resident UDP checksum GiB/s + %HBM-peak, 1M x 1472B IPv4 packets"
+            "metric": (f"device-resident IPv4 header checksum GiB/s, libxudp's IPv4 TX call "
+                       f"(iph->check only, packet.c:43-66; config {args.config} frames)"
+                       if flags & X.F_IPHDR_ONLY else
+                       "device-resident UDP checksum GiB/s + %HBM-peak, 1M x 1472B IPv4 packets"
                        if args.config == 2 else f"device-resident UDP checksum GiB/s (config "
                                                 f"{args.config})")
                       + (f" [flags {fl}]" if flags else ""),
@@ -964,7 +1010,7 @@ def main():
             "roofline": roof,
         }
         if world == 1 and not args.no_cpu_baseline:
-            line["cpu_baseline"] = cpu_baseline(cfg, args.cpu_seconds)
+            line["cpu_baseline"] = cpu_baseline(cfg, args.cpu_seconds, flags)
         print(json.dumps(line), flush=True)
 
     eng.close()

@@ -67,6 +67,22 @@ enum xcsum_mode {
 				 IPv6 check 0 = invalid), nonzero otherwise (malformed
 				 frames: 0xffff).  With XCSUM_F_IPHDR the IPv4 header
 				 must verify too for out[i] to be 0.  Never writes. */
+#define XCSUM_F_IPHDR_ONLY 0x80u /* xcsum_batch_device only: libxudp's IPv4 TX
+				 checksum work and nothing else -- iph->check
+				 (xudp_checksum_half, packet.c:43-66) computed from
+				 the 20-byte header, udp->check left as it is (0,
+				 packet.c:125), no payload byte read.  out[i] (if
+				 d_out) = iph->check in wire order; with
+				 XCSUM_F_INPLACE it is stored at eth+24; with
+				 XCSUM_F_VERIFY out[i] = 0 iff the header verifies.
+				 Modes V4_LEGACY / V4_RFC (the same here) and AUTO,
+				 where IPv6 frames are left untouched with out[i] 0
+				 (their checksum is udp_csum6: send them with
+				 XCSUM_MODE_V6).  A frame is malformed under the
+				 rule of the other modes (shorter than 42 bytes, UDP
+				 length > 65535; AUTO: another h_proto): out[i] 0
+				 (0xffff under VERIFY), counted.  XCSUM_MODE_V6 and
+				 the host entry points: -XCSUM_ERR_INVAL. */
 
 /* Error codes (returned negated). */
 enum {
@@ -118,12 +134,16 @@ int xcsum_ctx_set_order(xcsum_ctx *ctx, int region_log2, int tile_log2);
 /* Pick the visiting order for this context by timing it on the caller's own
  * batch (the arguments of xcsum_batch_device; it runs ordinary calls of it on
  * `stream` -- ~60 ms to bring the clocks up, then three rounds of the
- * automatic order and five forced ones, each ~6 ms -- and waits for them); a
- * forced order is kept only if >= 1 % faster than the automatic one in every
- * round, else the order is left automatic.  *region_log2 / *tile_log2 (may be NULL)
- * receive the choice (-1: automatic).  For a caller that sends batches of one
- * layout (libxudp's TX UMEM): once, after the UMEM is set up.  Not while the
- * stream is being captured (-XCSUM_ERR_INVAL). */
+ * automatic order and six forced ones, each order ~6-7 ms per round: ~0.2 s
+ * in all -- and waits for them); a forced order is kept only if >= 1 %
+ * faster than the automatic one in every round, else the order is left
+ * automatic.  *region_log2 / *tile_log2 (may be NULL) receive the choice
+ * (-1: automatic).  The calls write what any call writes (results, in-place
+ * fields), but their malformed frames are counted apart: the count
+ * xcsum_ctx_take_errors returns is unchanged by a calibration.  For a
+ * caller that sends batches of one layout (libxudp's TX UMEM): once, after
+ * the UMEM is set up.  Not while the stream is being captured
+ * (-XCSUM_ERR_INVAL). */
 int xcsum_ctx_calibrate_order(xcsum_ctx *ctx, uint8_t *d_umem, const struct xcsum_desc *d_desc,
 			      uint32_t n, uint16_t *d_out, uint32_t mode, uint32_t flags,
 			      uint32_t len_hint, void *stream, int *region_log2, int *tile_log2);
@@ -134,10 +154,13 @@ int xcsum_ctx_calibrate_order(xcsum_ctx *ctx, uint8_t *d_umem, const struct xcsu
  *   TWO_PASS: the checksum pass writes a result array (d_out, or a scratch
  *     array of the context), then a second launch stores the fields in frame
  *     order -- the stores no longer interleave with the read stream
- *     (DESIGN.md 5.3).  Its scratch is allocated on the first such call, so
- *     make one call before capturing a stream into a graph (a call under
- *     capture that finds no scratch runs FUSED); calls of one context on
- *     different streams are ordered through an event.
+ *     (DESIGN.md 5.3).  Its scratch (a result array of the context, used
+ *     when d_out is NULL or with XCSUM_F_IPHDR) is allocated on the first
+ *     such call and grown by later ones; eager calls of one context on
+ *     different streams are ordered through an event.  A graph never
+ *     references that scratch: a call made while its stream is captured and
+ *     that would need it runs FUSED (the same bytes), so replays of a graph
+ *     stay valid whatever eager calls do to the scratch.
  *   AUTO (default): FUSED.  Measured on config 2, the
  *     second pass costs more than the interleaving it removes: the lines it
  *     writes have left the caches by then and come back from HBM.

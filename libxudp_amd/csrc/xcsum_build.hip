@@ -355,16 +355,16 @@ static __device__ __forceinline__ void build_msg(const BuildArgs &a, const Msg &
  * message i is shifted, stored, summed and headed.  (A "next" set copied into
  * "current" at the loop latch would wait for the in-flight loads there.)
  */
-template <int G, int K, bool TWO>
-__global__ void __launch_bounds__(256) build_kernel(BuildArgs a)
+/* The batch's header template in LDS: tmpl = memory-order halfwords (big-
+ * endian word j of the header is bswap16(tmpl[j])), img = the template
+ * right-aligned in 64 bytes.  Returns the constant parts of the sums: the
+ * UDP checksum's pseudo-header addresses and ports (header halfwords 13..18 /
+ * 11..28) + protocol 17, and the IPv4 header sum without tot_len and check
+ * (halfwords 7..16).  Block-wide (__syncthreads). */
+static __device__ __forceinline__ void load_template(const BuildArgs &a, uint16_t *tmpl, u32x4 *img,
+						     bool v6, uint32_t hdr, uint32_t &sconst,
+						     uint32_t &ipconst)
 {
-	/* header template as memory-order halfwords; big-endian word j of the
-	 * header is bswap16(tmpl[j]) */
-	__shared__ uint16_t tmpl[32];
-	/* the header image: the template right-aligned in 64 bytes */
-	__shared__ __attribute__((aligned(16))) u32x4 img[4];
-	const bool v6 = a.family == 6;
-	const uint32_t hdr = v6 ? 62u : 42u;
 	if (threadIdx.x < 32)
 		tmpl[threadIdx.x] = (uint16_t)(a.tmpl[threadIdx.x / 2] >> (16 * (threadIdx.x & 1)));
 	if (threadIdx.x < 64) {
@@ -373,18 +373,25 @@ __global__ void __launch_bounds__(256) build_kernel(BuildArgs a)
 		reinterpret_cast<uint8_t *>(img)[b] = v;
 	}
 	__syncthreads();
-
-	/* constant part of the UDP checksum: pseudo-header addresses and the
-	 * ports (header halfwords 13..18 / 11..28), protocol 17 */
-	uint32_t sconst = 17u;
+	sconst = 17u;
 	for (uint32_t j = v6 ? 11u : 13u; j < (v6 ? 29u : 19u); j++)
 		sconst += bswap16(tmpl[j]);
-	/* IPv4 header sum without tot_len and check (halfwords 7..16) */
-	uint32_t ipconst = 0;
+	ipconst = 0;
 	if (!v6)
 		for (uint32_t j = 7; j < 17; j++)
 			if (j != 8 && j != 12)
 				ipconst += bswap16(tmpl[j]);
+}
+
+template <int G, int K, bool TWO>
+__global__ void __launch_bounds__(256) build_kernel(BuildArgs a)
+{
+	__shared__ uint16_t tmpl[32];
+	__shared__ __attribute__((aligned(16))) u32x4 img[4];
+	const bool v6 = a.family == 6;
+	const uint32_t hdr = v6 ? 62u : 42u;
+	uint32_t sconst, ipconst;
+	load_template(a, tmpl, img, v6, hdr, sconst, ipconst);
 
 	const uint32_t lane = threadIdx.x & (G - 1);
 	const uint32_t seg = (blockIdx.x * 256u + threadIdx.x) / G;
@@ -431,6 +438,71 @@ __global__ void __launch_bounds__(256) build_kernel(BuildArgs a)
 }
 
 
+/*
+ * IPv4 in place without XCSUM_F_V4_RFC: libxudp's default IPv4 send on
+ * frames whose payload already sits in its slot (the xudp_frame_alloc path,
+ * tx.c:760).  The reference computes only iph->check there (iph_build ->
+ * xudp_checksum_half, packet.c:43-66, :83) and leaves udp->check 0
+ * (packet.c:125), so no payload byte is read: per message the 16-byte
+ * message in, the 42 header bytes and the 16-byte descriptor out.  Four lanes
+ * per message store the header pieces (finish_frame<4>; lane 0 holds no
+ * IPv4 header byte and writes the descriptor); the next message is loaded
+ * while this one is written.
+ */
+__global__ void __launch_bounds__(256) build_hdr_kernel(BuildArgs a)
+{
+	__shared__ uint16_t tmpl[32];
+	__shared__ __attribute__((aligned(16))) u32x4 img[4];
+	uint32_t sconst, ipconst;
+	load_template(a, tmpl, img, false, 42u, sconst, ipconst);
+	const uint32_t lane = threadIdx.x & 3u;
+	const uint32_t seg = (blockIdx.x * 256u + threadIdx.x) / 4u;
+	const uint32_t nseg = gridDim.x * 64u;
+	const uint32_t last = a.n - 1;
+	auto idx = [&](uint32_t q) { return q < a.ord.nlog ? frame_of(a.ord, q) : a.n; };
+	auto msg = [&](uint32_t i) { return *((gu32x4 *)(a.msgs + (i < a.n ? i : last))); };
+	uint32_t i = idx(seg);
+	u32x4 d = msg(i);
+	for (uint32_t p = seg; p < a.ord.nlog; p += nseg) {
+		const uint32_t i2 = idx(p + nseg);
+		const u32x4 d2 = msg(i2);
+		const Msg g = resolve_msg(a, d, i < a.n, true);
+		if (g.present)
+			finish_frame<4>(a, g, i, 0u, lane, img, false, 42u, sconst, ipconst);
+		i = i2;
+		d = d2;
+	}
+}
+
+/* XCSUM_BUILD_HDR=0 (A/B and tests only, read per launch): IPv4 in place
+ * takes the payload-summing build kernel, as before round 5 */
+static bool build_hdr_enabled()
+{
+	const char *e = getenv("XCSUM_BUILD_HDR");
+	return !(e && atoi(e) == 0);
+}
+
+static hipError_t launch_build_hdr(const BuildArgs &a, int cus, hipStream_t s)
+{
+	static std::atomic<int> occ_cache[OCC_MAX_DEVICES];
+	const int occ = occupancy_cached(occ_cache, [] {
+		int nb = 0;
+		if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, build_hdr_kernel, 256, 0) !=
+			    hipSuccess || nb <= 0)
+			nb = 8;
+		return nb;
+	});
+	uint64_t blocks = ((uint64_t)a.ord.nlog * 4 + 255) / 256;
+	const uint64_t cap = (uint64_t)cus * occ;
+	if (blocks > cap)
+		blocks = cap;
+	if (blocks == 0)
+		blocks = 1;
+	(void)hipGetLastError();
+	hipLaunchKernelGGL(build_hdr_kernel, dim3((unsigned)blocks), dim3(256), 0, s, a);
+	return hipGetLastError();
+}
+
 template <int G, int K, bool TWO>
 static hipError_t launch_build_t(const BuildArgs &a, int cus, hipStream_t s)
 {
@@ -461,6 +533,9 @@ hipError_t launch_build(const BuildArgs &a, uint32_t len_hint, int cus, hipStrea
 {
 	if (a.n == 0)
 		return hipSuccess;
+	if (a.family == 4 && (a.flags & XCSUM_F_BUILD_INPLACE) && !(a.flags & XCSUM_F_V4_RFC) &&
+	    build_hdr_enabled())
+		return launch_build_hdr(a, cus, s);
 	/* payloads read from 16-byte aligned addresses need one block per chunk */
 	const bool two = !(a.flags & (XCSUM_F_BUILD_INPLACE | XCSUM_F_SRC_ALIGNED));
 	int G, K;

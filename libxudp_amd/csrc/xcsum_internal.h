@@ -204,6 +204,8 @@ hipError_t launch_csum_f2(const CsumArgs &a, Geometry g, int cus, hipStream_t s)
 /* XCSUM_F_INPLACE without IPHDR at (16,2,6): the kernel with each frame's
  * first 4 chunks loaded temporally (xcsum_csum_tl.hip) */
 hipError_t launch_csum_inplace_tl(const CsumArgs &a, Geometry g, int cus, hipStream_t s);
+/* XCSUM_F_IPHDR_ONLY: iph->check from the header alone (xcsum_iphdr.hip) */
+hipError_t launch_iphdr(const CsumArgs &a, hipStream_t s);
 hipError_t launch_gen(uint8_t *d_umem, const struct xcsum_desc *d_desc, uint32_t n,
 		      uint32_t family, uint64_t seed, uint64_t first_index, int max_blocks,
 		      hipStream_t s);

@@ -108,7 +108,8 @@ int ref_packet_udp_payload(uint8_t *head, const uint8_t *payload, int payload_si
 
 /* Batch driver with the product's descriptor semantics (include/xcsum.h),
  * calling the reference functions per frame.  mode: 0 = IPv4 udp_checksum
- * (legacy, checksum.h:107), 2 = IPv6 udp_csum6 (packet.c:105).  The IPv6
+ * (legacy, checksum.h:107), 2 = IPv6 udp_csum6 (packet.c:105), 4 = IPv4
+ * xudp_checksum_half (packet.c:43, the IPv4 TX call's one checksum).  The IPv6
  * call writes udp->check in place exactly as the reference does, so frames
  * must have check == 0 on entry and are restored to 0 afterwards (the
  * reference's udp_build zeroes it before every call, packet.c:125). */
@@ -116,6 +117,15 @@ struct ref_desc { uint64_t addr; uint32_t len; uint32_t options; };
 
 static uint16_t ref_one(uint8_t *f, uint32_t len, int mode)
 {
+	if (mode == 4) {
+		/* libxudp's IPv4 TX checksum: xudp_checksum_half (packet.c:43-66)
+		 * alone, storing iph->check in place as the reference does (it
+		 * reads neither the old check nor anything past the addresses) */
+		if (len < 42 || len - 34 > 0xffff)
+			return 0;
+		xudp_checksum_half((struct iphdr *)(f + 14));
+		return ((struct iphdr *)(f + 14))->check;
+	}
 	if (mode == 2) {
 		uint8_t *ip6 = f + 14;
 		uint8_t *udp = ip6 + 40;

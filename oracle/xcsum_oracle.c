@@ -278,9 +278,39 @@ static u16 orc_verify(const u8 *frame, u32 len, int fam6, u32 flags)
 	return r;
 }
 
+#define ORC_FLAG_IPHDR_ONLY 0x80u  /* == XCSUM_F_IPHDR_ONLY */
+
+/* XCSUM_F_IPHDR_ONLY (include/xcsum.h): libxudp's IPv4 TX checksum work and
+ * nothing else -- xudp_checksum_half() (packet.c:43-66, called from
+ * iph_build :83; udp->check stays 0, :125), here as the RFC 1071 header sum
+ * orc_ip_header_rfc, equal to it on every header iph_build writes (pinned
+ * in tests/test_oracle.py); VERIFY: the residue with the check field, 0 =
+ * valid.  AUTO: IPv6 frames have no header checksum: 0.  Malformed under
+ * orc_one's rules (frame shorter than its headers, UDP length > 65535,
+ * another h_proto): 0, or 0xffff under VERIFY. */
+static u16 orc_iphdr_only(const u8 *frame, u32 len, int mode, u32 flags)
+{
+	const u16 bad = (flags & ORC_FLAG_VERIFY) ? 0xffff : 0;
+	if (len < 42)
+		return bad;
+	if (mode == ORC_MODE_AUTO) {
+		u16 proto = ((u16)frame[12] << 8) | frame[13];
+		if (proto == 0x86DD)
+			return (len >= 62 && len - 54 <= 0xffff) ? 0 : bad;
+		if (proto != 0x0800)
+			return bad;
+	}
+	if (len - 34 > 0xffff)
+		return bad;
+	return (flags & ORC_FLAG_VERIFY) ? orc_ip_header_verify(frame + 14)
+					 : orc_ip_header_rfc(frame + 14);
+}
+
 static u16 orc_one(const u8 *frame, u32 len, int mode, u32 flags)
 {
 	int fam6;
+	if (flags & ORC_FLAG_IPHDR_ONLY)
+		return orc_iphdr_only(frame, len, mode, flags);
 	if (mode == ORC_MODE_AUTO) {
 		u16 proto = ((u16)frame[12] << 8) | frame[13];
 		if (proto == 0x0800)

@@ -271,6 +271,25 @@ def config_digest(cid, chunk=1 << 18, threads=8):
     return rec
 
 
+def iphdr_digest(cid, chunk=1 << 18):
+    """SHA-256 of the reference's xudp_checksum_half() (packet.c:43-66, the one
+    checksum libxudp's IPv4 TX call computes) over every frame of an IPv4
+    config: the full-size pin of XCSUM_F_IPHDR_ONLY (bench.py --flags
+    iphdr_only).  ref_batch mode 4 runs the reference function in place."""
+    n, fam, pmin, pmax = CONFIGS[cid]
+    assert fam == 4
+    seed = SEED_BASE ^ cid
+    h = hashlib.sha256()
+    R = oracle.ref()
+    for first in range(0, n, chunk):
+        m = min(chunk, n - first)
+        umem, desc = X.gen_frames_host(m, fam, pmin, pmax, seed=seed, first_index=first)
+        out = np.zeros(m, dtype=np.uint16)
+        R.ref_batch(umem.ctypes.data, desc.ctypes.data, m, out.ctypes.data, 4)
+        sha_u16(h, out)
+    return h.hexdigest()
+
+
 def rx_fixtures():
     """rx_fixtures.npz: received frames (tests/golden/rx_frames.py corpus) at
     irregular offsets, the reference's own packet_parse() result for each
@@ -298,6 +317,8 @@ def main():
     ap.add_argument("--no-digests", action="store_true")
     ap.add_argument("--only-build", action="store_true", help="only build_fixtures.npz")
     ap.add_argument("--only-rx", action="store_true", help="only rx_fixtures.npz")
+    ap.add_argument("--only-iphdr", action="store_true",
+                    help="only add the IPv4 header-checksum digests (sha256_iphdr) to digests.json")
     ap.add_argument("--configs", default="1,2,3,4,5")
     args = ap.parse_args()
     if not oracle.have_ref():
@@ -307,6 +328,17 @@ def main():
         return
     if args.only_rx:
         rx_fixtures()
+        return
+    if args.only_iphdr:
+        path = os.path.join(OUT, "digests.json")
+        digests = json.load(open(path))
+        for c in [int(x) for x in args.configs.split(",")]:
+            if CONFIGS[c][1] == 4:
+                digests[f"config{c}"]["sha256_iphdr"] = iphdr_digest(c)
+                digests[f"config{c}"]["iphdr_source"] = \
+                    "reference xudp_checksum_half (packet.c:43-66), oracle/_ref ref_batch mode 4"
+                print(f"config{c}: sha256_iphdr {digests[f'config{c}']['sha256_iphdr']}")
+        json.dump(digests, open(path, "w"), indent=1, sort_keys=True)
         return
     build_fixtures()
     build_frame_fixtures()

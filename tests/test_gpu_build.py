@@ -115,12 +115,46 @@ def test_build_random_routes_vs_oracle(torch_cuda, engine):
                 assert np.array_equal(after[eth:eth + len(exp)], exp)
 
 
-def test_build_rejects_oversized(torch_cuda, engine):
+@pytest.mark.parametrize("slot_size", [4096, FRAME])
+def test_build_ipv4_inplace_header_kernel(torch_cuda, engine, monkeypatch, slot_size):
+    """IPv4 in place without V4_RFC -- libxudp's default send on frames whose
+    payload already sits in its slot -- takes the header-only build kernel
+    (no payload byte read: iph->check only, udp->check 0, packet.c:43-66,
+    :125).  Its slots, descriptors and results equal the payload-summing
+    kernel's (XCSUM_BUILD_HDR=0) and the oracle's frames, for ragged
+    payloads in scattered slots."""
+    rng = np.random.default_rng(23)
+    n = 3001
+    cap = slot_size - DATA_OFF
+    pays = [rng.integers(0, 256, int(L), dtype=np.uint8)
+            for L in rng.integers(0, min(cap, 1500) + 1, n)]
+    slots = rng.permutation(n + 500)[:n].astype(np.uint32)
+    r = ROUTES[4]
+    res = {}
+    for hdr_kernel in ("1", "0"):
+        monkeypatch.setenv("XCSUM_BUILD_HDR", hdr_kernel)
+        engine.take_errors()
+        res[hdr_kernel] = device_build(torch_cuda, engine, route_of(4, r), pays, inplace=True,
+                                       slots=slots, len_hint=700, FRAME=slot_size)[:3]
+        assert engine.take_errors() == 0
+    for a, b in zip(res["1"], res["0"]):
+        assert np.array_equal(a, b)
+    after, desc, out = res["1"]
+    assert not out.any()                                        # udp->check 0
+    for i in rng.choice(n, 60, replace=False):
+        exp = oracle.build_frame(pays[i].tobytes(), 4, r["smac"], r["dmac"], r["saddr"],
+                                 r["sport"], r["daddr"], r["dport"], False)
+        eth = int(slots[i]) * slot_size + DATA_OFF - 42
+        assert np.array_equal(after[eth:eth + len(exp)], exp), i
+
+
+@pytest.mark.parametrize("inplace", [False, True])   # True: the header-only kernel
+def test_build_rejects_oversized(torch_cuda, engine, inplace):
     pays = [np.zeros(100, np.uint8), np.zeros(FRAME - DATA_OFF + 1, np.uint8),
             np.zeros(70000, np.uint8), np.ones(10, np.uint8)]
     engine.take_errors()
     after, desc, out, before = device_build(torch_cuda, engine, route_of(4, ROUTES[4]), pays[:2]
-                                            + pays[3:])
+                                            + pays[3:], inplace=inplace)
     assert list(desc["len"]) == [142, 0, 52]
     assert engine.take_errors() == 1
 

@@ -114,6 +114,39 @@ def test_config2_calibrated_order_same_digest(torch_cuda, engine, digests, umem_
         engine.set_order(-1, 0)
 
 
+@pytest.mark.parametrize("cid,umem_layout", [(2, False), (2, True), (3, False), (5, False)])
+def test_iphdr_only_digest(torch_cuda, engine, digests, cid, umem_layout):
+    """libxudp's IPv4 TX call (XCSUM_F_IPHDR_ONLY) over whole BASELINE
+    configs: the output's SHA-256 equals the digest of the reference's own
+    xudp_checksum_half (packet.c:43-66) over the same frames
+    (digests.json sha256_iphdr, tests/golden/make_golden.py --only-iphdr)."""
+    cfg, desc, d_desc, d_umem = device_batch(torch_cuda, engine, cid, umem_layout=umem_layout)
+    got = run(torch_cuda, engine, d_umem, d_desc, len(desc), cfg["mode"], X.F_IPHDR_ONLY, 0)
+    assert sha(got) == digests[f"config{cid}"]["sha256_iphdr"]
+
+
+def test_calibration_leaves_error_count(torch_cuda, engine):
+    """The thousands of calls xcsum_ctx_calibrate_order makes count their
+    malformed frames apart: take_errors after a calibration is
+    what the caller's own calls produced."""
+    torch = torch_cuda
+    dev = torch.device("cuda:0")
+    umem, desc = X.gen_frames_host(2000, 4, 0, 1472, seed=77)
+    desc["len"][::20] = 10                       # 100 malformed frames
+    d_umem = h2d(torch, umem, dev)
+    d_desc = h2d(torch, desc.view(np.uint8), dev)
+    out = torch.empty(len(desc), dtype=torch.int16, device=dev)
+    s = torch.cuda.current_stream(dev).cuda_stream
+    engine.take_errors()
+    try:
+        engine.calibrate_order(d_umem, d_desc, len(desc), out, X.MODE_V4_LEGACY, 0, 1514, stream=s)
+        assert engine.take_errors() == 0
+        engine.batch_device(d_umem, d_desc, len(desc), out, X.MODE_V4_LEGACY, 0, 1514, stream=s)
+        assert engine.take_errors() == 100
+    finally:
+        engine.set_order(-1, 0)
+
+
 @pytest.mark.parametrize("cid", [2, 3, 4])
 def test_umem_layout_same_digest(torch_cuda, engine, digests, cid):
     """The same frames in xudp's 4096-byte-chunk UMEM layout: the automatic

@@ -128,19 +128,31 @@ def test_fuzz_schedules_identical(torch_cuda, engine, seed):
             assert errs == errs_fused
 
 
-def test_two_pass_under_graph_capture(torch_cuda):
-    """A context whose first in-place call is captured has no scratch yet and
-    runs FUSED inside the graph; after one eager call it runs TWO_PASS inside
-    the graph.  Either way the replayed graph writes the reference's fields."""
+@pytest.mark.parametrize("with_out", [False, True])
+def test_two_pass_under_graph_capture(torch_cuda, with_out):
+    """A TWO_PASS context captured into a graph, with no scratch yet and after
+    an eager call made one; then an eager call with 20x the frames (the
+    scratch is freed and regrown) and the graph replayed again.  A capture
+    that needs the scratch (no d_out, or IPHDR) runs FUSED, so the replay
+    touches no scratch; without IPHDR and with the caller's d_out the two
+    passes are captured as they are.  Every replay writes the reference's
+    fields (a graph that kept the old scratch pointer wrote into
+    freed memory after the regrowth)."""
     torch = torch_cuda
     dev = torch.device("cuda:0")
+    flags = X.F_INPLACE | (0 if with_out else X.F_IPHDR)
     umem, desc = X.gen_frames_host(5000, 4, 0, 1472, seed=31, align=8)
-    _, exp_after = expected_frames(umem, desc, X.MODE_V4_LEGACY, X.F_INPLACE | X.F_IPHDR)
+    exp_out, exp_after = expected_frames(umem, desc, X.MODE_V4_LEGACY, flags)
+    big_u, big_d = X.gen_frames_host(100000, 4, 0, 200, seed=32, align=8)
+    _, big_exp = expected_frames(big_u, big_d, X.MODE_V4_LEGACY, X.F_INPLACE | X.F_IPHDR)
     d_desc = h2d(torch, desc.view(np.uint8), dev)
+    d_big_desc = h2d(torch, big_d.view(np.uint8), dev)
     for eager_first in (False, True):
         e = X.Engine(0)
+        e.set_inplace(X.INPLACE_TWO_PASS)
         try:
             d_umem = h2d(torch, umem, dev)
+            d_out = torch.zeros(len(desc), dtype=torch.int16, device=dev) if with_out else None
             s = torch.cuda.Stream(dev)
             if eager_first:
                 scratch = h2d(torch, umem, dev)
@@ -150,12 +162,24 @@ def test_two_pass_under_graph_capture(torch_cuda):
             g = torch.cuda.CUDAGraph()
             s.wait_stream(torch.cuda.current_stream(dev))
             with torch.cuda.graph(g, stream=s):
-                e.batch_device(d_umem, d_desc, len(desc), None, X.MODE_V4_LEGACY,
-                               X.F_INPLACE | X.F_IPHDR, 1500,
+                e.batch_device(d_umem, d_desc, len(desc), d_out, X.MODE_V4_LEGACY, flags, 1500,
                                stream=torch.cuda.current_stream(dev).cuda_stream)
             g.replay()
             torch.cuda.synchronize(dev)
             assert np.array_equal(d2h(d_umem), exp_after), f"eager_first={eager_first}"
+            # an eager call that regrows the scratch, then the graph again on
+            # fresh frames
+            d_big = h2d(torch, big_u, dev)
+            e.batch_device(d_big, d_big_desc, len(big_d), None, X.MODE_V4_LEGACY,
+                           X.F_INPLACE | X.F_IPHDR, 200, stream=s.cuda_stream)
+            d_umem.copy_(h2d(torch, umem, dev))
+            torch.cuda.synchronize(dev)
+            g.replay()
+            torch.cuda.synchronize(dev)
+            assert np.array_equal(d2h(d_umem), exp_after), f"regrown, eager_first={eager_first}"
+            if with_out:
+                assert np.array_equal(d2h(d_out).view(np.uint16), exp_out)
+            assert np.array_equal(d2h(d_big), big_exp)
         finally:
             e.close()
 

@@ -223,6 +223,58 @@ def test_oracle_reproduces_fullsize_digest_prefix(digests, cid):
     assert out.dtype == np.uint16 and len(out) == 1 << 16
 
 
+# ---- XCSUM_F_IPHDR_ONLY: libxudp's IPv4 TX call (xudp_checksum_half alone) --
+
+IPHDR_ONLY = 0x80
+
+
+def test_iphdr_only_matches_golden(golden):
+    """The oracle's header-only batch equals the reference's exp_iphdr on
+    every IPv4 fixture frame; AUTO gives IPv6 frames 0."""
+    fam = golden["family"]
+    desc = golden_desc(golden)
+    out = oracle.batch(golden["umem"], desc, oracle.MODE_V4_LEGACY, IPHDR_ONLY)
+    assert np.array_equal(out[fam == 4], golden["exp_iphdr"][fam == 4])
+    out = oracle.batch(golden["umem"], desc, oracle.MODE_AUTO, IPHDR_ONLY)
+    assert np.array_equal(out, np.where(fam == 6, 0, golden["exp_iphdr"]))
+
+
+@pytest.mark.parametrize("cid", [1, 2, 3, 5])
+def test_iphdr_only_digests(digests, cid):
+    """digests.json sha256_iphdr: the reference's xudp_checksum_half over
+    every frame of the IPv4 configs (make_golden.py --only-iphdr).  Config
+    1 in full through the oracle; the others on a 64K-frame prefix against
+    the compiled reference where it exists."""
+    d = digests[f"config{cid}"]
+    assert len(d["sha256_iphdr"]) == 64
+    m = d["n"] if cid == 1 else 1 << 16
+    umem, desc = X.gen_frames_host(m, 4, d["pmin"], d["pmax"], seed=d["seed"])
+    out = oracle.batch(umem, desc, oracle.MODE_V4_LEGACY, IPHDR_ONLY)
+    if cid == 1:
+        assert hashlib.sha256(out.astype("<u2").tobytes()).hexdigest() == d["sha256_iphdr"]
+    if oracle.have_ref():
+        ref = np.zeros(m, np.uint16)
+        oracle.ref().ref_batch(umem.ctypes.data, desc.ctypes.data, m, ref.ctypes.data, 4)
+        assert np.array_equal(out, ref)
+
+
+def test_iphdr_only_rules():
+    """Malformed frames and VERIFY in the oracle's header-only mode (the rules
+    include/xcsum.h states for XCSUM_F_IPHDR_ONLY)."""
+    umem, desc = X.gen_frames_host(64, 4, 0, 200, seed=4)
+    good = oracle.batch(umem, desc, oracle.MODE_V4_LEGACY, IPHDR_ONLY)
+    filled = umem.copy()
+    for d, c in zip(desc, good):
+        filled[int(d["addr"]) + 24:int(d["addr"]) + 26] = np.array([c], "<u2").view(np.uint8)
+    assert not oracle.batch(filled, desc, oracle.MODE_V4_LEGACY, IPHDR_ONLY | VERIFY).any()
+    bad = desc.copy()
+    bad["len"][:4] = [0, 41, 65570, 70000]
+    out = oracle.batch(filled, bad, oracle.MODE_V4_LEGACY, IPHDR_ONLY)
+    assert list(out[:4]) == [0, 0, 0, 0] and np.array_equal(out[4:], good[4:])
+    out = oracle.batch(filled, bad, oracle.MODE_V4_LEGACY, IPHDR_ONLY | VERIFY)
+    assert list(out[:4]) == [0xffff] * 4 and not out[4:].any()
+
+
 # ---- receive-side verify (SURVEY 8(f) rank 3; the reference never verifies) --
 
 def filled_golden(golden, v4_col="exp_rfc"):

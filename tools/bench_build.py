@@ -27,6 +27,9 @@ def main():
     ap.add_argument("--family", type=int, default=4)
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--modes", default="copy_aligned,copy_unaligned,inplace")
+    ap.add_argument("--orders", default="auto",
+                    help="comma list of visiting orders to time, 'auto' or R_T "
+                         "(xcsum_ctx_set_order: 2^R regions of 2^T-message tiles)")
     args = ap.parse_args()
     import torch
     dev = torch.device("cuda:0")
@@ -50,50 +53,72 @@ def main():
         msgs["slot"] = np.arange(n, dtype=np.uint32)
         d_msgs = torch.from_numpy(msgs.view(np.uint8)).to(dev)
         d_src = torch.randint(0, 255, (n * stride + 16,), dtype=torch.uint8, device=dev)
-        flags = {"inplace": X.F_BUILD_INPLACE, "copy_aligned": X.F_SRC_ALIGNED}.get(mode, 0)
-        s = torch.cuda.current_stream(dev)
-        # clock ramp: >= 300 ms of launches before anything is timed
-        import time
-        t0 = time.perf_counter()
-        while time.perf_counter() - t0 < 0.3:
-            for _ in range(10):
+        flags = {"inplace": X.F_BUILD_INPLACE, "inplace_sum": X.F_BUILD_INPLACE,
+                 "copy_aligned": X.F_SRC_ALIGNED}.get(mode, 0)
+        # inplace_sum (A/B): IPv4 in place through the payload-summing build
+        # kernel (XCSUM_BUILD_HDR=0, read per launch), as before round 5
+        if mode == "inplace_sum":
+            os.environ["XCSUM_BUILD_HDR"] = "0"
+        else:
+            os.environ.pop("XCSUM_BUILD_HDR", None)
+        for order in args.orders.split(","):
+            if order == "auto":
+                eng.set_order(-1, 0)
+            else:
+                eng.set_order(*[int(v) for v in order.split("_")])
+            s = torch.cuda.current_stream(dev)
+            # clock ramp: >= 300 ms of launches before anything is timed
+            import time
+            t0 = time.perf_counter()
+            while time.perf_counter() - t0 < 0.3:
+                for _ in range(10):
+                    eng.build_device(route, d_src, d_msgs, n, d_umem, FRAME, DATA_OFF, d_desc, d_out,
+                                     flags, L, s.cuda_stream)
+                torch.cuda.synchronize()
+            evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                   for _ in range(args.reps)]
+            for e0, e1 in evs:
+                e0.record(s)
                 eng.build_device(route, d_src, d_msgs, n, d_umem, FRAME, DATA_OFF, d_desc, d_out,
                                  flags, L, s.cuda_stream)
-            torch.cuda.synchronize()
-        evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-               for _ in range(args.reps)]
-        for e0, e1 in evs:
-            e0.record(s)
-            eng.build_device(route, d_src, d_msgs, n, d_umem, FRAME, DATA_OFF, d_desc, d_out,
-                             flags, L, s.cuda_stream)
-            e1.record(s)
-        torch.cuda.synchronize()
-        t = float(np.median([a.elapsed_time(b) for a, b in evs])) * 1e-3
-        moved = n * ((L + hdr + L + 32) if mode != "inplace" else (L + hdr + 32))
-        rec = {"mode": mode, "geometry": os.environ.get("XCSUM_BUILD_GEOMETRY", "auto"),
-               "payload": L, "family": fam, "frames": n, "ms": round(t * 1e3, 4),
-               "mpps": round(n / t / 1e6, 1), "GBps_moved": round(moved / t / 1e9, 1),
-               "pct_hbm_peak": round(100 * moved / t / 8e12, 1)}
-        if mode == "inplace":
-            # the checksum kernel on the frames just built (headers in place):
-            # checksums + in-place writes only, the same slots, same process
-            d_bdesc = d_desc.clone()
-            cs = []
-            for _ in range(args.reps):
-                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                e0.record(s)
-                eng.batch_device(d_umem, d_bdesc, n, d_out,
-                                 X.MODE_V6 if fam == 6 else X.MODE_V4_LEGACY,
-                                 X.F_INPLACE | (X.F_IPHDR if fam == 4 else 0), L + hdr,
-                                 stream=s.cuda_stream)
                 e1.record(s)
-                cs.append((e0, e1))
             torch.cuda.synchronize()
-            tc = float(np.median([a.elapsed_time(b) for a, b in cs])) * 1e-3
-            rec["csum_inplace_ms"] = round(tc * 1e3, 4)
-            rec["vs_csum_inplace"] = round(t / tc, 3)
-        print(json.dumps(rec), flush=True)
+            t = float(np.median([a.elapsed_time(b) for a, b in evs])) * 1e-3
+            if mode == "inplace" and fam == 4:
+                # libxudp's IPv4 send in place: headers only, no payload byte read
+                # (packet.c:43-66, :125; build_hdr_kernel)
+                moved = n * (hdr + 32)
+            elif mode.startswith("inplace"):
+                moved = n * (L + hdr + 32)
+            else:
+                moved = n * (L + hdr + L + 32)
+            rec = {"mode": mode, "order": order,
+                   "geometry": os.environ.get("XCSUM_BUILD_GEOMETRY", "auto"),
+                   "payload": L, "family": fam, "frames": n, "ms": round(t * 1e3, 4),
+                   "mpps": round(n / t / 1e6, 1), "GBps_moved": round(moved / t / 1e9, 1),
+                   "pct_hbm_peak": round(100 * moved / t / 8e12, 1)}
+            if mode == "inplace":
+                # the checksum call on the frames just built (headers in place):
+                # checksums + in-place writes only, the same slots, same process;
+                # IPv4: libxudp's call, iph->check alone (XCSUM_F_IPHDR_ONLY)
+                d_bdesc = d_desc.clone()
+                cs = []
+                for _ in range(args.reps):
+                    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    e0.record(s)
+                    eng.batch_device(d_umem, d_bdesc, n, d_out,
+                                     X.MODE_V6 if fam == 6 else X.MODE_V4_LEGACY,
+                                     X.F_INPLACE | (X.F_IPHDR_ONLY if fam == 4 else 0), L + hdr,
+                                     stream=s.cuda_stream)
+                    e1.record(s)
+                    cs.append((e0, e1))
+                torch.cuda.synchronize()
+                tc = float(np.median([a.elapsed_time(b) for a, b in cs])) * 1e-3
+                rec["csum_inplace_ms"] = round(tc * 1e3, 4)
+                rec["vs_csum_inplace"] = round(t / tc, 3)
+            print(json.dumps(rec), flush=True)
         del d_src, d_msgs
+    eng.set_order(-1, 0)
     eng.close()
 
 

@@ -1,5 +1,7 @@
 #!/usr/bin/env python3
-"""Per-leg PMC summary of tools/r04_inplace_pmc.sh: for every
+"""Per-leg PMC summary of the per-leg rocprofv3 passes (round 4:
+profiles/run_scripts.bundle.txt r04_inplace_pmc.sh; round 5: tools/run_session.sh
+<tag> iphdr_pmc): for every
 <leg>_<counter>/run_counter_collection.csv under a directory, the mean per
 dispatch of each counter, per kernel (FETCH_SIZE / WRITE_SIZE in KiB as
 rocprofv3 reports them; FETCH_SIZE counts half the bytes of a wide streaming
@@ -22,7 +24,8 @@ def main(root):
         per = collections.defaultdict(lambda: collections.defaultdict(float))
         for r in csv.DictReader(open(f)):
             k = r["Kernel_Name"]
-            if not any(t in k for t in ("stream_read", "csum_kernel", "scatter")):
+            if not any(t in k for t in ("stream_read", "csum_kernel", "scatter", "iphdr_kernel",
+                                        "build_hdr_kernel")):
                 continue
             per[(k, r["Dispatch_Id"])][r["Counter_Name"]] += float(r["Counter_Value"])
         agg = collections.defaultdict(lambda: collections.defaultdict(list))

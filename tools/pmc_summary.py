@@ -21,8 +21,9 @@ import os
 import re
 import statistics
 
-# the checksum kernels: csum_kernel<G,U,K,FEAT>, csum_stream_kernel<KC>, csum_seg_kernel<D>
-KERNEL = re.compile(r"csum_(stream_|seg_)?kernel")
+# the checksum kernels: csum_kernel<G,U,K,FEAT>, csum_kernel_tl<...>,
+# csum_stream_kernel<KC>, csum_seg_kernel<D>, iphdr_kernel<FPT> (XCSUM_F_IPHDR_ONLY)
+KERNEL = re.compile(r"csum_(stream_|seg_)?kernel|iphdr_kernel")
 
 
 names = set()
@@ -51,6 +52,7 @@ def main():
     ap.add_argument("--out", default="")
     ap.add_argument("--flags", type=lambda v: int(v, 0), default=0,
                     help="the bench's XCSUM_F_* flags (file name tag _f<hex>)")
+    ap.add_argument("--layout", default="packed", help="bench --layout (file name tag _umem)")
     ap.add_argument("--lib-sha", default="",
                     help="SHA-256 prefix of the profiled libxcsum.so's device code "
                          "(bench.py lib_sha16: its .hip_fatbin section), for the record")
@@ -71,13 +73,14 @@ def main():
            "FETCH_SIZE_KiB_median": f_kib, "WRITE_SIZE_KiB_median": w_kib,
            "hbm_bytes_per_launch": round(hbm), "alg_bytes_per_launch": args.alg_bytes,
            "traffic_over_alg": round(hbm / args.alg_bytes, 4),
-           "flags": args.flags, "lib_sha16": args.lib_sha or None,
+           "flags": args.flags, "layout": args.layout, "lib_sha16": args.lib_sha or None,
            "kernel_sha16": ksha,
            "formula": "(2*FETCH_SIZE + WRITE_SIZE) * 1024  (gfx950 FETCH_SIZE = half of "
                       "wide streaming read bytes, MI355X_MICROARCH.md HBM)"}
     out = args.out or os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(
-        __file__))), "profiles", "r03",
-        f"pmc_config{args.config}{'_f%x' % args.flags if args.flags else ''}.json")
+        __file__))), "profiles", "r05",
+        f"pmc_config{args.config}{'_umem' if args.layout == 'umem' else ''}"
+        f"{'_f%x' % args.flags if args.flags else ''}.json")
     json.dump(rec, open(out, "w"), indent=1)
     print(json.dumps(rec))
 

@@ -1,0 +1,120 @@
+#!/bin/bash
+# One parameterised GPU-box runner for the recurring checks (it replaces the
+# per-round tools/r0x_*.sh scripts, kept verbatim in
+# profiles/run_scripts.bundle.txt).  Every GPU step runs under its own time
+# limit through tools/gpu_run.sh, which stops the chain at a fault, abort or
+# time-out; logs go to gpurun_out/<tag>/.
+#
+#   tools/run_session.sh <tag> <recipe> [<recipe> ...]
+#
+# recipes:
+#   env       read-only box facts bearing on registered host memory (THP,
+#             memlock, compaction, NUMA balancing)
+#   suite     the product GPU suite (XCSUM_REG_TRACE on), smoke, the driver's
+#             bench command
+#   debug     the GPU suite on the bounds-checked build (libxudp_amd/debug,
+#             built beforehand: make -C libxudp_amd debug)
+#   benches   bench.py over its workloads, one summary line each
+#             (BENCH_ARGS: '|'-separated argument lists to replace the default)
+#   e2e       host-resident end-to-end rates (tools/bench_e2e.py)
+#   crossover one host core running the reference's xudp_packet_udp
+#             (tools/crossover.py)
+#   iphdr     the header-only legs of libxudp's IPv4 TX call
+#             (tools/iphdr_probe.py) and the build kernel's (tools/bench_build.py)
+#   iphdr_pmc FETCH/WRITE/request counters of the header-only kernel, one
+#             rocprofv3 pass per counter set and leg (tools/pmc_legs.py
+#             summarises gpurun_out/<tag>/pmc)
+#   profile   tools/profile_round.sh <tag>/profile (bench lines, kernel
+#             stats, PMC summaries)
+set -u
+cd "${GRAFT_REPO_ROOT:-.}"
+export TMPDIR=/tmp
+t="$1"; shift
+mkdir -p "gpurun_out/$t"
+P="python -u -m pytest tests -m gpu -x -q -s --timeout 300 --timeout-method thread"
+DEFAULT_BENCHES="--config 2|--config 2 --layout umem|--config 3|--config 4|--config 5\
+|--config 2 --flags inplace,iphdr_only|--config 2 --flags inplace,iphdr_only --layout umem\
+|--config 2 --flags inplace,iphdr|--config 4 --flags inplace|--config 2 --flags verify"
+
+env_facts() {
+  echo "uname: $(uname -r)"
+  echo "ulimit -l: $(ulimit -l)"
+  for f in /sys/kernel/mm/transparent_hugepage/enabled \
+           /sys/kernel/mm/transparent_hugepage/shmem_enabled \
+           /sys/kernel/mm/transparent_hugepage/defrag \
+           /proc/sys/vm/compact_unevictable_allowed \
+           /proc/sys/kernel/numa_balancing \
+           /sys/module/amdgpu/parameters/noretry \
+           /sys/module/amdgpu/parameters/mtype_local; do
+    [ -r "$f" ] && echo "$f: $(cat "$f" 2>/dev/null)"
+  done
+  grep -E 'thp_|compact_(migrate|stall|success)|pgmigrate' /proc/vmstat 2>/dev/null | tr '\n' ' '
+  echo
+}
+
+for r in "$@"; do
+  case "$r" in
+  env)
+    env_facts > "gpurun_out/$t/env.log" 2>&1 ;;
+  suite)
+    XCSUM_REG_TRACE=$PWD/gpurun_out/$t/regtrace.log tools/gpu_run.sh $t/pytest_gpu 900 $P &&
+    tools/gpu_run.sh $t/smoke 200 python -c "import __graft_entry__ as g; g.smoke()" &&
+    tools/gpu_run.sh $t/bench_driver_cmd 300 python bench.py --gpus 1 --steps 20 --warmup 5 \
+      || exit $? ;;
+  debug)
+    XCSUM_LIB=$PWD/libxudp_amd/debug/libxcsum.so tools/gpu_run.sh $t/pytest_gpu_debug 900 $P \
+      || exit $? ;;
+  benches)
+    IFS='|' read -ra lines <<< "${BENCH_ARGS:-$DEFAULT_BENCHES}"
+    i=0
+    for a in "${lines[@]}"; do
+      i=$((i + 1))
+      tools/gpu_run.sh $t/bench_$i 300 python -u bench.py --steps 100 --warmup 5 \
+        --no-cpu-baseline $a || exit $?
+      python3 - "gpurun_out/$t/bench_$i.log" "$a" >> "gpurun_out/$t/benches.txt" <<'PY'
+import json, sys
+rows = [l for l in open(sys.argv[1]) if l.startswith("{")]
+if not rows:
+    print(sys.argv[2], "| no line")
+    raise SystemExit
+d = json.loads(rows[-1]); r = d["roofline"]
+print(sys.argv[2], "|", d["value"], "GiB/s |", d["kernel_ms"], "ms |", d["mpps"], "Mpps | frac",
+      r["frac"], "| vs ceiling", r.get("frac_vs_ceiling"), "| order",
+      d["config"].get("order_calibration"), "| parity", d.get("parity_ok"))
+PY
+    done ;;
+  e2e)
+    for a in "--config 2" "--config 2 --layout umem" "--config 4"; do
+      tools/gpu_run.sh "$t/e2e_$(echo $a | tr ' -' '__')" 300 python -u tools/bench_e2e.py $a \
+        --reps 5 || exit $?
+    done ;;
+  crossover)
+    tools/gpu_run.sh $t/crossover 300 python -u tools/crossover.py || exit $? ;;
+  iphdr)
+    tools/gpu_run.sh $t/iphdr_probe 400 python -u tools/iphdr_probe.py --rounds 3 &&
+    tools/gpu_run.sh $t/bench_build 300 python -u tools/bench_build.py \
+      --modes inplace,inplace_sum,copy_aligned --reps 30 || exit $? ;;
+  iphdr_pmc)
+    mkdir -p gpurun_out/$t/pmc
+    for lay in packed slots; do
+      for leg in inplace out_only; do
+        for pmc in FETCH_SIZE WRITE_SIZE \
+                   "TCC_EA0_WRREQ_sum TCC_EA0_WRREQ_64B_sum TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum"; do
+          tag=$(echo "$pmc" | cut -d' ' -f1)
+          d=gpurun_out/$t/pmc/${lay}_${leg}_$tag
+          # --warm 0 and one leg: every counted dispatch is that leg's
+          timeout -s KILL 120 rocprofv3 --pmc $pmc --output-format csv -d $d -o run -- \
+            python3 tools/iphdr_probe.py --layouts $lay --legs $leg --rounds 1 --reps 1 \
+            --per 3 --warm 0 --no-ref > $d.log 2>&1
+          rc=$?
+          echo "pmc $lay $leg $tag rc=$rc"
+          [ $rc -eq 0 ] || exit $rc
+        done
+      done
+    done ;;
+  profile)
+    bash tools/profile_round.sh $t/profile || exit $? ;;
+  *)
+    echo "unknown recipe $r"; exit 2 ;;
+  esac
+done
