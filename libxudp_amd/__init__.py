@@ -17,6 +17,11 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 # XCSUM_LIB selects an A/B build variant of the library (tuning only)
 _PRODUCT_LIB = os.path.join(HERE, "libxcsum.so")
 LIB_PATH = os.environ.get("XCSUM_LIB") or _PRODUCT_LIB
+# the void packet.c mirrors (xudp_packet_udp, xudp_packet_udp_payload): the
+# same symbols as libxudp's packet.o, so a library of their own, linked
+# instead of packet.o (include/xudp_packet.h); it binds to
+# whichever libxcsum.so (SONAME) the process loaded first
+PACKET_LIB_PATH = os.path.join(HERE, "libxcsum_packet.so")
 
 # include/xcsum.h
 MODE_V4_LEGACY = 0
@@ -188,8 +193,6 @@ _SIGS = {
                                             ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint32),
                                             ctypes.POINTER(ctypes.c_uint32)]),
     "xudp_packet_build_headers": (None, [ctypes.c_void_p]),
-    "xudp_packet_udp": (None, [ctypes.c_void_p]),
-    "xudp_packet_udp_payload": (None, [ctypes.c_void_p]),
     "xudp_packet_udp_batch": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32,
                                              ctypes.c_uint32]),
 }
@@ -224,6 +227,30 @@ def lib():
             fn.argtypes = args
         _lib = L
     return _lib
+
+
+# libxcsum_packet.so
+_PACKET_SIGS = {
+    "xudp_packet_udp": (None, [ctypes.c_void_p]),
+    "xudp_packet_udp_payload": (None, [ctypes.c_void_p]),
+}
+_packet_lib = None
+
+
+def packet_lib():
+    """Load libxcsum_packet.so (after libxcsum.so, which it needs)."""
+    global _packet_lib
+    if _packet_lib is None:
+        lib()
+        if not os.path.exists(PACKET_LIB_PATH):
+            raise ImportError(f"{PACKET_LIB_PATH} is missing: build it with `make -C libxudp_amd`")
+        L = ctypes.CDLL(PACKET_LIB_PATH)
+        for name, (res, args) in _PACKET_SIGS.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _packet_lib = L
+    return _packet_lib
 
 
 def _check(rc, what):
@@ -542,11 +569,11 @@ def packet_build_headers(pa):
 
 
 def packet_udp_payload(pa):
-    lib().xudp_packet_udp_payload(ctypes.byref(pa.info))
+    packet_lib().xudp_packet_udp_payload(ctypes.byref(pa.info))
 
 
 def packet_udp(pa):
-    lib().xudp_packet_udp(ctypes.byref(pa.info))
+    packet_lib().xudp_packet_udp(ctypes.byref(pa.info))
 
 
 def packet_udp_batch(engine, pas, flags=0):

@@ -158,15 +158,7 @@ extern "C" int xudp_packet_udp_batch(xcsum_ctx *ctx, struct packet_info *infos, 
 	return 0;
 }
 
-extern "C" void xudp_packet_udp(struct packet_info *info)
-{
-	if (xudp_packet_udp_batch(nullptr, info, 1, 0) != 0)
-		errno = EIO;
-}
-
-extern "C" void xudp_packet_udp_payload(struct packet_info *info)
-{
-	info->data = info->head + XUDP_TX_HEADROOM;           /* packet.c:198 */
-	memcpy(info->data, info->payload, info->payload_size); /* packet.c:200 */
-	xudp_packet_udp(info);
-}
+/* xudp_packet_udp / xudp_packet_udp_payload, the void packet.c mirrors, are
+ * not in this library: they would clash with libxudp's own packet.o
+ * (Makefile:41).  They live in libxcsum_packet.so (xudp_packet_mirror.cpp),
+ * which a maintainer links instead of packet.o. */

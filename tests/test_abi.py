@@ -23,21 +23,43 @@ def declared_functions():
     return sorted(names)
 
 
-def exported_symbols():
-    out = subprocess.run(["nm", "-D", "--defined-only", X.LIB_PATH], capture_output=True,
-                         text=True, check=True).stdout
+def exported_symbols(path=None):
+    out = subprocess.run(["nm", "-D", "--defined-only", path or X.LIB_PATH],
+                         capture_output=True, text=True, check=True).stdout
     return {l.split()[-1] for l in out.splitlines() if " T " in l}
 
 
 def test_library_loads():
     assert X.lib() is not None
+    assert X.packet_lib() is not None
 
 
 def test_every_declared_function_is_exported():
+    """libxcsum.so exports every declared function except the two packet.o
+    symbols, which only libxcsum_packet.so defines (so libxcsum.so links
+    beside libxudp's own packet.o, ref Makefile:41)."""
     decl = declared_functions()
-    assert set(decl) == set(X._SIGS), set(decl) ^ set(X._SIGS)
-    missing = sorted(set(decl) - exported_symbols())
+    mirror = set(X._PACKET_SIGS)
+    assert mirror == {"xudp_packet_udp", "xudp_packet_udp_payload"}
+    assert set(decl) == set(X._SIGS) | mirror, set(decl) ^ (set(X._SIGS) | mirror)
+    core = exported_symbols()
+    missing = sorted(set(decl) - mirror - core)
     assert not missing, missing
+    assert not (mirror & core), "libxcsum.so must not define packet.o's symbols"
+    pk = exported_symbols(X.PACKET_LIB_PATH)
+    assert mirror <= pk and not (pk & set(X._SIGS)), pk
+
+
+def test_packet_mirror_needs_libxcsum_by_soname():
+    """libxcsum_packet.so binds to whichever libxcsum.so the process loaded
+    (the product, the debug or the TSan build): DT_NEEDED libxcsum.so, and
+    every build of libxcsum.so carries that SONAME."""
+    out = subprocess.run(["readelf", "-d", X.PACKET_LIB_PATH], capture_output=True, text=True,
+                         check=True).stdout
+    assert "Shared library: [libxcsum.so]" in out
+    out = subprocess.run(["readelf", "-d", X.LIB_PATH], capture_output=True, text=True,
+                         check=True).stdout
+    assert "Library soname: [libxcsum.so]" in out
 
 
 def test_python_binding_covers_the_abi():
