@@ -319,7 +319,16 @@ int xcsum_batch_host(xcsum_ctx *ctx, uint8_t *h_umem, const struct xcsum_desc *h
  * every registered-memory GPU fault of rounds 2-4 was on such memory).
  * libxudp's UMEM (anon_map: MAP_SHARED | MAP_ANONYMOUS | MAP_POPULATE |
  * MAP_LOCKED, include/common.h:37-41) is mapped.  xcsum_umem_mapped() says
- * which: 1 mapped, 0 staged, -XCSUM_ERR_NOT_REGISTERED if base is unknown. */
+ * which: 1 mapped, 0 staged, -XCSUM_ERR_NOT_REGISTERED if base is unknown.
+ *
+ * Contract: eligibility is read ONCE, at registration (the VMA flags in
+ * /proc/self/smaps and the THP sysfs modes; the parser is
+ * libxudp_amd/csrc/xcsum_thp.h).  Until the range is unregistered the caller
+ * must not make it THP-eligible -- madvise(MADV_HUGEPAGE) on it,
+ * prctl(PR_SET_THP_DISABLE, 0) after registering with THP disabled, or a
+ * change of the THP modes -- nor mremap(), munmap() or remap it: the GPU
+ * keeps its mapping of the pages found at registration.  To change any of
+ * that, unregister, change it, register again. */
 int xcsum_register_umem(xcsum_ctx *ctx, void *base, size_t size);
 int xcsum_unregister_umem(xcsum_ctx *ctx, void *base);
 int xcsum_umem_mapped(xcsum_ctx *ctx, const void *base);

@@ -19,6 +19,7 @@
 
 #include "xcsum_internal.h"
 #include "xcsum_gen.h"
+#include "xcsum_thp.h"
 
 using namespace xcsum;
 
@@ -1281,13 +1282,9 @@ static void reg_trace(const char *what, const void *base, size_t size, const voi
 }
 
 /* Can the kernel move the pages of [lo, hi) under a GPU mapping?  The
- * registered-memory faults of rounds 2-4 all hit memory
- * eligible for transparent huge pages (numpy's heap, madvise(MADV_HUGEPAGE)
- * by numpy for arrays of 4 MiB and up: VmFlags "hg"); none hit libxudp's
- * UMEM mapping (anon_map, MAP_LOCKED | MAP_POPULATE, not THP-eligible under
- * THP "madvise"), and the same suite ran clean with THP disabled for the
- * process.  Eligible: a VMA of the range flagged "hg", or THP "always" and
- * not "nh", unless THP is disabled for the process (PR_GET_THP_DISABLE). */
+ * policy and its smaps parser are in xcsum_thp.h; here the process-wide
+ * inputs: THP disabled for the process (PR_GET_THP_DISABLE), the sysfs
+ * modes, /proc/self/smaps.  Read once per registration (include/xcsum.h). */
 /* the bracketed word of a THP sysfs setting ("always", "never", ...) */
 static bool thp_mode_is(const char *path, const char *word)
 {
@@ -1309,33 +1306,16 @@ static bool thp_eligible(uintptr_t lo, uintptr_t hi)
 	 * MAP_SHARED | MAP_ANONYMOUS): "shmem_enabled" */
 	const char *en = "/sys/kernel/mm/transparent_hugepage/enabled";
 	const char *sh = "/sys/kernel/mm/transparent_hugepage/shmem_enabled";
-	const bool never = thp_mode_is(en, "never");
-	const bool always = thp_mode_is(en, "always");
-	const bool sh_always = thp_mode_is(sh, "always") || thp_mode_is(sh, "force") ||
-			       thp_mode_is(sh, "within_size");
-	const bool sh_advise = thp_mode_is(sh, "advise");
+	ThpModes m;
+	m.never = thp_mode_is(en, "never");
+	m.always = thp_mode_is(en, "always");
+	m.sh_always = thp_mode_is(sh, "always") || thp_mode_is(sh, "force") ||
+		      thp_mode_is(sh, "within_size");
+	m.sh_advise = thp_mode_is(sh, "advise");
 	FILE *f = fopen("/proc/self/smaps", "r");
 	if (!f)
 		return true;   /* cannot tell: assume the worst */
-	char line[512];
-	uintptr_t s = 0, e = 0;
-	bool eligible = false;
-	while (fgets(line, sizeof line, f)) {
-		unsigned long a, b;
-		if (sscanf(line, "%lx-%lx ", &a, &b) == 2 && strchr(line, '-') < strchr(line, ' ')) {
-			s = a;
-			e = b;
-			continue;
-		}
-		if (strncmp(line, "VmFlags:", 8) == 0 && s < hi && e > lo) {
-			const bool hg = strstr(line, " hg") != nullptr;
-			const bool nh = strstr(line, " nh") != nullptr;
-			if (strstr(line, " sh") != nullptr)
-				eligible |= !nh && (sh_always || (sh_advise && hg));
-			else
-				eligible |= !never && (hg || (always && !nh));
-		}
-	}
+	const bool eligible = thp_eligible_smaps(f, lo, hi, m);   /* xcsum_thp.h */
 	fclose(f);
 	return eligible;
 }

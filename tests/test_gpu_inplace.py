@@ -100,6 +100,39 @@ def test_two_pass_store_widths(torch_cuda, monkeypatch, block, layout):
         e.close()
 
 
+@pytest.mark.parametrize("block", [0, 32, 64])
+def test_r04d_field_at_block_end(torch_cuda, monkeypatch, block):
+    """profiles/r04/fault/r04d_pytest_gpu_thp_off_scatter_bug.log, pinned: the
+    batch of test_fuzz_host_path_vs_device[3] (seed 3003 draws: odd-address
+    frames, flags INPLACE | IPHDR), whose udp->check high byte (eth+41) fell
+    on a 32-byte boundary in 193 frames.  The round-4 work-in-progress second
+    pass patched such a field into the block holding its first byte and lost
+    the second; store_block (xcsum_scatter.hip) now sends any field that
+    reaches past its block to the 2-byte stores.  Both schedules, every
+    store width: the reference's fields, no other byte changed."""
+    rng = np.random.default_rng(3000 + 3)
+    umem, desc = random_batch(rng)
+    mode = MODES[int(rng.integers(len(MODES)))]
+    flags = int(rng.choice([0, X.F_INPLACE, X.F_INPLACE | X.F_IPHDR, X.F_VERIFY,
+                            X.F_VERIFY | X.F_IPHDR]))
+    assert flags == X.F_INPLACE | X.F_IPHDR
+    straddle = ((desc["addr"].astype(np.int64) + 40) % 32 == 31).sum()
+    assert straddle >= 100, straddle               # the r04d shape is in the batch
+    res, exp_after = expected_frames(umem, desc, mode, flags)
+    monkeypatch.setenv("XCSUM_INPLACE_BLOCK", str(block))
+    e = X.Engine(0)
+    monkeypatch.delenv("XCSUM_INPLACE_BLOCK")
+    try:
+        for sched in ("two_pass", "fused"):
+            e.set_inplace(SCHEDULES[sched])
+            got, after = run_device(torch_cuda, e, umem.copy(), desc, mode, flags)
+            assert np.array_equal(got, res), sched
+            diff = np.nonzero(after != exp_after)[0]
+            assert len(diff) == 0, f"{sched}: {len(diff)} bytes differ, first {diff[:4]}"
+    finally:
+        e.close()
+
+
 @pytest.mark.parametrize("seed", range(12))
 def test_fuzz_schedules_identical(torch_cuda, engine, seed):
     """Random batches (mixed sizes, alignments, shuffled and malformed
