@@ -534,6 +534,46 @@ def inplace_ceiling(torch, dev, bufs, desc, flags, family, sptr):
                     f"{per} back-to-back launches between two events, median of 5"}
 
 
+def header_ceiling(torch, dev, bufs, d_desc, count, write, sptr):
+    """Same-run ceiling of the XCSUM_F_IPHDR_ONLY call: tools/libhbmprobe.so's
+    probe_header_touch over the very frames and descriptors -- per frame the
+    descriptor, the seven header dwords the kernel loads and, in place, a
+    2-byte store at eth+24 -- with none of the kernel's arithmetic.  One
+    scattered line read (+ one partial write) per frame is an access pattern
+    whose bound is the memory system's transaction rate, not the stream
+    rate.  Writes junk into iph->check: run it after timing, before the
+    parity pass regenerates the frames."""
+    path = os.path.join(ROOT, "tools", "libhbmprobe.so")
+    if not os.path.exists(path) or not count:
+        return None
+    L = ctypes.CDLL(path)
+    fn = getattr(L, "probe_header_touch", None)
+    if fn is None:
+        return None
+    fn.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_int,
+                   ctypes.c_void_p, ctypes.c_void_p]
+    scratch = torch.empty(max(1, (count + 1023) // 1024), dtype=torch.int32, device=dev)
+    per = max(20, len(bufs))
+    s = torch.cuda.current_stream(dev)
+    ts = []
+    for r in range(6):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(s)
+        for k in range(per):
+            if fn(bufs[k % len(bufs)].data_ptr(), d_desc.data_ptr(), count, int(write),
+                  scratch.data_ptr(), sptr) != 0:
+                return None
+        e1.record(s)
+        torch.cuda.synchronize(dev)
+        ts.append(e0.elapsed_time(e1) / per)
+    t = float(np.median(ts[1:]))
+    return {"ms": round(t, 5),
+            "what": f"tools/hbm_probe.hip probe_header_touch over the same frames: per frame the "
+                    f"16-byte descriptor and the 28 bytes at (eth+12)&~3"
+                    f"{' plus a 2-byte store at eth+24' if write else ''}, no arithmetic; "
+                    f"{per} back-to-back launches between two events, median of 5"}
+
+
 # Visiting orders the same-run A/B times next to the automatic one
 # (xcsum_ctx_set_order "R,T": 2^R regions of 2^T-frame tiles; 0,0 = descriptor
 # order).  The automatic order of MTU frames is 3,4 (DESIGN.md 5.1).
@@ -666,12 +706,13 @@ def main():
     ap.add_argument("--inplace-schedule", default="auto", choices=["auto", "fused", "two_pass"],
                     help="how --flags inplace writes the check fields (xcsum_ctx_set_inplace)")
     ap.add_argument("--flags", default="",
-                    help="comma list of inplace,iphdr,rfc,verify (XCSUM_F_*); with inplace the "
-                         "checks go into the frames and no result array is written, as in "
-                         "libxudp's TX drop-in (tx.c:696-726)")
+                    help="comma list of inplace,iphdr,rfc,verify,iphdr_only (XCSUM_F_*); with "
+                         "inplace the checks go into the frames and no result array is written, "
+                         "as libxudp's TX path does (tx.c:696-726); libxudp's IPv4 call is "
+                         "inplace,iphdr_only (iph->check only), its IPv6 call inplace on config 4")
     args = ap.parse_args()
     flags = parse_flags(args.flags)
-    # the TX drop-in writes udp->check / iph->check into the frames: no array
+    # in place: the check fields go into the frames, no result array
     with_out = not (flags & X.F_INPLACE) or bool(flags & X.F_VERIFY)
 
     import torch
@@ -829,9 +870,13 @@ def main():
     elapsed_max = float(np.median(walls_max))
     alg_all, frames_all = float(tot[0]), float(tot[1])
 
-    ceiling = inplace = orders = None
+    ceiling = inplace = orders = hdr_probe = None
     if rank == 0 and not args.no_ceiling:
         ceiling = stream_ceiling(torch, dev, bufs, sptr)
+        if flags & X.F_IPHDR_ONLY:
+            hdr_probe = header_ceiling(torch, dev, bufs, d_desc, count,
+                                       bool(flags & X.F_INPLACE) and not flags & X.F_VERIFY,
+                                       sptr)
         if flags & X.F_INPLACE and with_out is False and not flags & X.F_IPHDR_ONLY:
             inplace = inplace_ceiling(torch, dev, bufs, desc, flags, cfg["family"], sptr)
         if args.order_ab and cfg["id"] in (2, 4) and not flags and not args.geometry:
@@ -936,6 +981,12 @@ def main():
             roof["frac_of_layout_bound"] = round(achieved / bound, 4)
         if orders:
             roof["order_ab"] = orders
+        if hdr_probe:
+            # the same descriptor, header and field accesses, no arithmetic:
+            # the bound of one scattered line read (+ write) per frame
+            roof["header_probe_ms"] = hdr_probe["ms"]
+            roof["frac_vs_header_probe"] = round(hdr_probe["ms"] / kern_ms, 4)
+            roof["header_probe"] = hdr_probe["what"]
         if inplace:
             # same buffers, same reads, the same stores per frame, no arithmetic
             roof["inplace_probe_ms"] = inplace["ms"]

@@ -516,3 +516,106 @@ extern "C" int probe_stream_read_copy(void *p, uint64_t nbytes, uint64_t fstride
 			   (const uint8_t *)side, fstride, off, nframes, f1, f2);
 	return hipGetLastError() == hipSuccess ? 0 : -1;
 }
+
+/* Header-only probe (round 5): the memory accesses of the library's
+ * XCSUM_F_IPHDR_ONLY kernel (csrc/xcsum_iphdr.hip) with none of its
+ * arithmetic -- per frame the 16-byte descriptor (coalesced), the seven dwords
+ * at (eth + 12) & ~3 (one dwordx4 + one dwordx3, the header line), and with
+ * `write` a 2-byte store at eth + 24 that depends on them -- FPT = 4 frames per
+ * thread, all loads issued first, one launch per batch.  The same-run ceiling
+ * of an access pattern that is one scattered line read (and one scattered
+ * partial write) per frame, not a stream. */
+struct probe_desc { uint64_t addr; uint32_t len, options; };
+typedef uint32_t u32x3 __attribute__((ext_vector_type(3)));
+
+/* LD: how the header dwords are loaded -- 0 plain (the library's kernel),
+ * 1 nontemporal, 2..4 inline global loads with cache-policy bits "nt",
+ * "sc1", "sc0 sc1" (whether the L2 then requests less than a 128-byte line
+ * per scattered access is what the variants measure) */
+template <int LD>
+static __device__ __forceinline__ void load_hdr(const uint8_t *w, u32x4 &a, u32x3 &b)
+{
+	typedef const __attribute__((address_space(1))) u32x4 g4;
+	typedef const __attribute__((address_space(1))) u32x3 g3;
+	if (LD == 0) {
+		a = *((g4 *)w);
+		b = *((g3 *)(w + 16));
+	} else if (LD == 1) {
+		a = __builtin_nontemporal_load((g4 *)w);
+		b = __builtin_nontemporal_load((g3 *)(w + 16));
+	} else if (LD == 2) {
+		asm volatile("global_load_dwordx4 %0, %2, off nt\n\t"
+			     "global_load_dwordx3 %1, %2, off offset:16 nt"
+			     : "=&v"(a), "=&v"(b) : "v"(w) : "memory");
+	} else if (LD == 3) {
+		asm volatile("global_load_dwordx4 %0, %2, off sc1\n\t"
+			     "global_load_dwordx3 %1, %2, off offset:16 sc1"
+			     : "=&v"(a), "=&v"(b) : "v"(w) : "memory");
+	} else {
+		asm volatile("global_load_dwordx4 %0, %2, off sc0 sc1\n\t"
+			     "global_load_dwordx3 %1, %2, off offset:16 sc0 sc1"
+			     : "=&v"(a), "=&v"(b) : "v"(w) : "memory");
+	}
+}
+
+template <int LD>
+__global__ void __launch_bounds__(256) header_touch(uint8_t *umem, const probe_desc *desc,
+						    uint32_t n, int write, uint32_t *out)
+{
+	constexpr int F = 4;
+	const uint32_t q0 = blockIdx.x * (256u * F) + threadIdx.x;
+	u32x4 d[F];
+#pragma unroll
+	for (int j = 0; j < F; j++) {
+		const uint32_t q = q0 + 256u * j;
+		d[j] = *((gu32x4 *)(desc + (q < n ? q : n - 1)));
+	}
+	__builtin_amdgcn_sched_barrier(0);
+	u32x4 a[F];
+	u32x3 b[F];
+#pragma unroll
+	for (int j = 0; j < F; j++) {
+		const uint8_t *h = umem + ((((uint64_t)d[j].y << 32) | d[j].x) + 12);
+		load_hdr<LD>((const uint8_t *)((uintptr_t)h & ~(uintptr_t)3), a[j], b[j]);
+	}
+	if (LD >= 2)   /* the inline loads are invisible to the waitcnt pass */
+		asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+	uint32_t acc = 0;
+#pragma unroll
+	for (int j = 0; j < F; j++) {
+		const uint32_t v = a[j].x ^ a[j].y ^ a[j].z ^ a[j].w ^ b[j].x ^ b[j].y ^ b[j].z;
+		acc ^= v;
+		if (write && q0 + 256u * j < n) {
+			uint8_t *e = umem + (((uint64_t)d[j].y << 32) | d[j].x);
+			e[24] = (uint8_t)v;
+			e[25] = (uint8_t)(v >> 8);
+		}
+	}
+	if (acc == 0x9e3779b9u)
+		out[blockIdx.x] = acc;
+}
+
+/* load_mode: LD above (0 = the library kernel's loads) */
+extern "C" int probe_header_touch_mode(void *umem, const void *desc, uint32_t n, int write,
+				       int load_mode, uint32_t *out, void *stream)
+{
+	if (!n || load_mode < 0 || load_mode > 4)
+		return -1;
+	const uint32_t blocks = (n + 1023) / 1024;
+	auto *u = (uint8_t *)umem;
+	auto *d = (const probe_desc *)desc;
+	switch (load_mode) {
+	case 0: hipLaunchKernelGGL(header_touch<0>, dim3(blocks), dim3(256), 0, (hipStream_t)stream, u, d, n, write, out); break;
+	case 1: hipLaunchKernelGGL(header_touch<1>, dim3(blocks), dim3(256), 0, (hipStream_t)stream, u, d, n, write, out); break;
+	case 2: hipLaunchKernelGGL(header_touch<2>, dim3(blocks), dim3(256), 0, (hipStream_t)stream, u, d, n, write, out); break;
+	case 3: hipLaunchKernelGGL(header_touch<3>, dim3(blocks), dim3(256), 0, (hipStream_t)stream, u, d, n, write, out); break;
+	default: hipLaunchKernelGGL(header_touch<4>, dim3(blocks), dim3(256), 0, (hipStream_t)stream, u, d, n, write, out); break;
+	}
+	return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+extern "C" int probe_header_touch(void *umem, const void *desc, uint32_t n, int write,
+				  uint32_t *out, void *stream)
+{
+	return probe_header_touch_mode(umem, desc, n, write, 0, out, stream);
+}

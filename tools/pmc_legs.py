@@ -25,6 +25,7 @@ def main(root):
         for r in csv.DictReader(open(f)):
             k = r["Kernel_Name"]
             if not any(t in k for t in ("stream_read", "csum_kernel", "scatter", "iphdr_kernel",
+                                        "header_touch",
                                         "build_hdr_kernel")):
                 continue
             per[(k, r["Dispatch_Id"])][r["Counter_Name"]] += float(r["Counter_Value"])

@@ -112,6 +112,21 @@ PY
         done
       done
     done ;;
+  header_probe)
+    # the header-only access pattern with each load cache policy: timing,
+    # then the L2's memory-side request counters per policy
+    tools/gpu_run.sh $t/header_probe 400 python -u tools/header_probe.py || exit $?
+    mkdir -p gpurun_out/$t/hpmc
+    for m in 0 1 2 3 4; do
+      d=gpurun_out/$t/hpmc/mode${m}_REQ
+      timeout -s KILL 120 rocprofv3 --pmc TCC_EA0_WRREQ_sum TCC_EA0_WRREQ_64B_sum \
+        TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum --output-format csv -d $d -o run -- \
+        python3 tools/header_probe.py --layouts packed --modes $m --writes 1 --rounds 1 \
+        --reps 1 --per 3 --warm 0 > $d.log 2>&1
+      rc=$?
+      echo "hpmc mode $m rc=$rc"
+      [ $rc -eq 0 ] || exit $rc
+    done ;;
   profile)
     bash tools/profile_round.sh $t/profile || exit $? ;;
   *)
