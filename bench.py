@@ -90,6 +90,30 @@ def alg_bytes_flags(desc, family, flags, with_out):
     return read + 2 * len(desc) * ((1 if with_out else 0) + fields)
 
 
+def reference_call(cfg, flags):
+    """Which of the reference's computations a bench line times (VERDICT r4
+    #2: a 'drop-in' number must be a call libxudp makes)."""
+    v6 = cfg["family"] == 6
+    inplace = flags & X.F_INPLACE and not flags & X.F_VERIFY
+    if flags & X.F_VERIFY:
+        return "receive-side verify (new: the reference never verifies, group/channel.c:231-255)"
+    if flags & X.F_IPHDR_ONLY:
+        return ("libxudp's IPv4 TX checksum: xudp_checksum_half (packet.c:43-66), udp->check "
+                "left 0 (packet.c:125)" + (", stored in place" if inplace else ""))
+    if v6:
+        return ("libxudp's IPv6 TX checksum: udp_csum6 (packet.c:105-117)"
+                + (", stored in place as packet.c:188 does" if inplace else ""))
+    if cfg["mode"] == X.MODE_V4_RFC or flags & X.F_V4_RFC:
+        return "IPv4 RFC 768 UDP checksum (an option; the reference leaves udp->check 0)"
+    if inplace:
+        return ("checksum.h udp_checksum stored into udp->check"
+                + (" + iph->check" if flags & X.F_IPHDR else "")
+                + ": not a call libxudp makes (it leaves the IPv4 udp->check 0, packet.c:125; "
+                  "its IPv4 call is --flags inplace,iphdr_only)")
+    return ("checksum.h udp_checksum (checksum.h:107-140, the BASELINE metric's function; no "
+            "caller in the reference)" + (" + xudp_checksum_half" if flags & X.F_IPHDR else ""))
+
+
 def elf_section(path, name):
     """Bytes of one section of an ELF64 little-endian file (None if absent)."""
     import struct
@@ -1019,6 +1043,7 @@ def main():
                        "family": cfg["family"], "mode": MODE_NAMES[cfg["mode"]],
                        "flags": fl or "none",
                        "result_array": with_out,
+                       "reference_call": reference_call(cfg, flags),
                        "inplace_schedule": (args.inplace_schedule if flags & X.F_INPLACE
                                             and not flags & X.F_VERIFY else None),
                        "layout": "packed, 8-byte aligned frames" if args.layout == "packed"
