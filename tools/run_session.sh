@@ -17,6 +17,7 @@
 #   benches   bench.py over its workloads, one summary line each
 #             (BENCH_ARGS: '|'-separated argument lists to replace the default)
 #   e2e       host-resident end-to-end rates (tools/bench_e2e.py)
+#   ring      libxudp's TX loop on its anon_map UMEM (tests/c/umem_ring --bench)
 #   crossover one host core running the reference's xudp_packet_udp
 #             (tools/crossover.py)
 #   iphdr     the header-only legs of libxudp's IPv4 TX call
@@ -90,6 +91,11 @@ PY
     done ;;
   crossover)
     tools/gpu_run.sh $t/crossover 300 python -u tools/crossover.py || exit $? ;;
+  ring)
+    # libxudp's TX loop on its anon_map UMEM, every variant launched and with
+    # 16 resident workgroups (tests/c/umem_ring.c)
+    RING_RESIDENT_WG=16 XCSUM_RESIDENT_TRACE=1 tools/gpu_run.sh $t/ring_bench 400 \
+      tests/c/umem_ring --bench 1,16,100,1024 || exit $? ;;
   iphdr)
     tools/gpu_run.sh $t/iphdr_probe 400 python -u tools/iphdr_probe.py --rounds 3 &&
     tools/gpu_run.sh $t/bench_build 300 python -u tools/bench_build.py \
