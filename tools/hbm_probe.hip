@@ -619,3 +619,36 @@ extern "C" int probe_header_touch(void *umem, const void *desc, uint32_t n, int 
 {
 	return probe_header_touch_mode(umem, desc, n, write, 0, out, stream);
 }
+
+/* Request-size calibration (round 5, MI355X_MICROARCH.md: "other access
+ * widths are uncalibrated"): one thread per line of a strided set, reading
+ * one dword from each 64-byte half of the 128-byte line named by `halves`
+ * (bit 0: +0, bit 1: +64).  The L2's memory-side request counters per line,
+ * for one half vs both, say whether a scattered access fetches 64 or 128
+ * bytes. */
+__global__ void __launch_bounds__(256) line_halves(const uint8_t *p, uint64_t nlines,
+						   uint64_t stride, int halves, uint32_t *out)
+{
+	const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+	if (i >= nlines)
+		return;
+	const uint8_t *l = p + i * stride;
+	uint32_t acc = 0;
+	if (halves & 1)
+		acc ^= *(const __attribute__((address_space(1))) uint32_t *)l;
+	if (halves & 2)
+		acc ^= *(const __attribute__((address_space(1))) uint32_t *)(l + 64);
+	if (acc == 0x9e3779b9u)
+		out[blockIdx.x] = acc;
+}
+
+extern "C" int probe_line_halves(const void *p, uint64_t nlines, uint64_t stride, int halves,
+				 uint32_t *out, void *stream)
+{
+	if (!nlines || (stride & 127) || halves < 1 || halves > 3)
+		return -1;
+	const uint64_t blocks = (nlines + 255) / 256;
+	hipLaunchKernelGGL(line_halves, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream,
+			   (const uint8_t *)p, nlines, stride, halves, out);
+	return hipGetLastError() == hipSuccess ? 0 : -1;
+}

@@ -24,7 +24,7 @@ def main(root):
         per = collections.defaultdict(lambda: collections.defaultdict(float))
         for r in csv.DictReader(open(f)):
             k = r["Kernel_Name"]
-            if not any(t in k for t in ("stream_read", "csum_kernel", "scatter", "iphdr_kernel",
+            if not any(t in k for t in ("stream_read", "csum_kernel", "scatter", "iphdr_kernel", "line_halves",
                                         "header_touch",
                                         "build_hdr_kernel")):
                 continue

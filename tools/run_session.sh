@@ -133,6 +133,42 @@ PY
       echo "hpmc mode $m rc=$rc"
       [ $rc -eq 0 ] || exit $rc
     done ;;
+  line_probe)
+    # how many bytes a scattered access fetches: requests per line for one
+    # 64-byte half vs both (tools/line_probe.py), plus the TCC counter names
+    timeout -s KILL 60 rocprofv3 -L > gpurun_out/$t/counters_list.txt 2>&1 || true
+    tools/gpu_run.sh $t/line_probe 300 python -u tools/line_probe.py || exit $?
+    mkdir -p gpurun_out/$t/lpmc
+    for h in 1 2 3; do
+      for pmc in FETCH_SIZE "TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum"; do
+        tag=$(echo "$pmc" | cut -d' ' -f1)
+        d=gpurun_out/$t/lpmc/halves${h}_$tag
+        timeout -s KILL 120 rocprofv3 --pmc $pmc --output-format csv -d $d -o run -- \
+          python3 tools/line_probe.py --halves $h --per 2 --reps 1 > $d.log 2>&1
+        rc=$?
+        echo "lpmc halves $h $tag rc=$rc"
+        [ $rc -eq 0 ] || exit $rc
+      done
+    done ;;
+  bubble)
+    # TCC_BUBBLE (the 128-byte requests in rocprofv3's FETCH_SIZE formula)
+    # and the DRAM read requests, for one / both line halves, the
+    # header-only kernel and the streaming checksum kernel
+    mkdir -p gpurun_out/$t/bpmc
+    for leg in h1 h3 iphdr stream; do
+      case $leg in
+        h1) cmd="python3 tools/line_probe.py --halves 1 --per 2 --reps 1" ;;
+        h3) cmd="python3 tools/line_probe.py --halves 3 --per 2 --reps 1" ;;
+        iphdr) cmd="python3 tools/iphdr_probe.py --layouts packed --legs inplace --rounds 1 --reps 1 --per 3 --warm 0 --no-ref" ;;
+        stream) cmd="python3 bench.py --steps 3 --warmup 1 --no-graph --ramp-ms 0 --reps 1 --no-ceiling --no-calibrate --no-cpu-baseline --no-order-ab" ;;
+      esac
+      d=gpurun_out/$t/bpmc/${leg}_BUBBLE
+      timeout -s KILL 120 rocprofv3 --pmc TCC_BUBBLE_sum TCC_EA0_RDREQ_DRAM_sum \
+        TCC_EA0_RDREQ_sum --output-format csv -d $d -o run -- $cmd > $d.log 2>&1
+      rc=$?
+      echo "bpmc $leg rc=$rc"
+      [ $rc -eq 0 ] || exit $rc
+    done ;;
   profile)
     bash tools/profile_round.sh $t/profile || exit $? ;;
   *)
