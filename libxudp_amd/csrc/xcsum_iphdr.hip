@@ -21,11 +21,7 @@
  * TTL / protocol / DF words iph_build stores, :73-79); with XCSUM_F_VERIFY
  * the check field is summed too and 0 means valid.
  */
-/* for resolve_order(); the frame-group helpers it brings are unused here */
-#pragma clang diagnostic push
-#pragma clang diagnostic ignored "-Wunneeded-internal-declaration"
-#include "xcsum_csum.h"
-#pragma clang diagnostic pop
+#include "xcsum_frame.h"
 
 namespace xcsum {
 
@@ -65,7 +61,6 @@ static __device__ __forceinline__ uint16_t hdr_csum(const uint32_t (&w)[7], uint
 template <int FPT>
 __global__ void __launch_bounds__(256) iphdr_kernel(CsumArgs a)
 {
-	resolve_order(a);
 	const bool verify = (a.flags & XCSUM_F_VERIFY) != 0;
 	const bool inplace = (a.flags & XCSUM_F_INPLACE) != 0 && !verify;
 	const uint8_t *zero = (const uint8_t *)g_zero_chunk;
