@@ -253,7 +253,7 @@ def d2h(torch, t):
     return h.numpy()
 
 
-def build_batch(cfg, rank, world, torch, dev, eng, stream):
+def build_batch(cfg, rank, world, torch, dev, eng, stream, flags=0):
     """Descriptors + frames for this rank, generated on the device."""
     seed = SEED_BASE ^ cfg["id"]
     first, count = rank_slice(cfg, rank, world)
@@ -268,8 +268,11 @@ def build_batch(cfg, rank, world, torch, dev, eng, stream):
                                     first_index=first)
     d_desc = h2d(torch, desc.view(np.uint8), dev)
     # rotate buffers so each pass streams >= 1 GiB: nothing is served from the
-    # 256 MiB Infinity Cache (SURVEY.md 7 hard part iv)
-    nrot = max(1, math.ceil((1 << 30) / max(nbytes, 1)))
+    # 256 MiB Infinity Cache (SURVEY.md 7 hard part iv).  XCSUM_F_IPHDR_ONLY
+    # touches only the header lines (~120-160 MB of a config-2 batch, which
+    # would stay in the Infinity Cache between launches): rotate by those
+    touched = real_bytes(desc, flags) if flags & X.F_IPHDR_ONLY else nbytes
+    nrot = max(1, math.ceil((1 << 30) / max(touched, 1)))
     bufs = [torch.empty(nbytes + 64, dtype=torch.uint8, device=dev) for _ in range(nrot)]
     eng.gen_fill_device(bufs[0], d_desc, count, cfg["family"], seed, first, stream=stream)
     for b in bufs[1:]:
@@ -766,7 +769,8 @@ def main():
                      "two_pass": X.INPLACE_TWO_PASS}[args.inplace_schedule])
     stream = torch.cuda.current_stream(dev)
     sptr = stream.cuda_stream
-    desc, d_desc, bufs, out, first, count = build_batch(cfg, rank, world, torch, dev, eng, sptr)
+    desc, d_desc, bufs, out, first, count = build_batch(cfg, rank, world, torch, dev, eng, sptr,
+                                                        flags)
     alg = alg_bytes_flags(desc, cfg["family"], flags, with_out)
     len_hint = int(desc["len"].mean()) if count else 0
     out_arg = out if with_out else None

@@ -27,6 +27,7 @@ def main():
     ap.add_argument("--family", type=int, default=4)
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--modes", default="copy_aligned,copy_unaligned,inplace")
+    ap.add_argument("--rot", type=int, default=4, help="UMEM buffers rotated between launches")
     ap.add_argument("--orders", default="auto",
                     help="comma list of visiting orders to time, 'auto' or R_T "
                          "(xcsum_ctx_set_order: 2^R regions of 2^T-message tiles)")
@@ -40,7 +41,9 @@ def main():
     route = X.make_route(fam, b"\x02\0\0\0\0\x01", b"\x02\0\0\0\0\x02",
                          bytes(range(16)) if fam == 6 else bytes([10, 0, 35, 2]), 3486,
                          bytes(range(16, 32)) if fam == 6 else bytes([10, 0, 35, 1]), 40000)
-    d_umem = torch.zeros(n * FRAME, dtype=torch.uint8, device=dev)
+    # rotated UMEMs: the header lines one launch writes (~128 MB for 1M
+    # slots) would otherwise stay in the 256 MiB Infinity Cache between launches
+    d_umems = [torch.zeros(n * FRAME, dtype=torch.uint8, device=dev) for _ in range(args.rot)]
     d_desc = torch.zeros(n * 16, dtype=torch.uint8, device=dev)
     d_out = torch.zeros(n, dtype=torch.int16, device=dev)
     res = {}
@@ -71,16 +74,16 @@ def main():
             import time
             t0 = time.perf_counter()
             while time.perf_counter() - t0 < 0.3:
-                for _ in range(10):
-                    eng.build_device(route, d_src, d_msgs, n, d_umem, FRAME, DATA_OFF, d_desc, d_out,
-                                     flags, L, s.cuda_stream)
+                for k in range(10):
+                    eng.build_device(route, d_src, d_msgs, n, d_umems[k % args.rot], FRAME, DATA_OFF,
+                                     d_desc, d_out, flags, L, s.cuda_stream)
                 torch.cuda.synchronize()
             evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
                    for _ in range(args.reps)]
-            for e0, e1 in evs:
+            for k, (e0, e1) in enumerate(evs):
                 e0.record(s)
-                eng.build_device(route, d_src, d_msgs, n, d_umem, FRAME, DATA_OFF, d_desc, d_out,
-                                 flags, L, s.cuda_stream)
+                eng.build_device(route, d_src, d_msgs, n, d_umems[k % args.rot], FRAME, DATA_OFF,
+                                 d_desc, d_out, flags, L, s.cuda_stream)
                 e1.record(s)
             torch.cuda.synchronize()
             t = float(np.median([a.elapsed_time(b) for a, b in evs])) * 1e-3
@@ -92,7 +95,7 @@ def main():
                 moved = n * (L + hdr + 32)
             else:
                 moved = n * (L + hdr + L + 32)
-            rec = {"mode": mode, "order": order,
+            rec = {"mode": mode, "order": order, "rotating_umems": args.rot,
                    "geometry": os.environ.get("XCSUM_BUILD_GEOMETRY", "auto"),
                    "payload": L, "family": fam, "frames": n, "ms": round(t * 1e3, 4),
                    "mpps": round(n / t / 1e6, 1), "GBps_moved": round(moved / t / 1e9, 1),
@@ -103,10 +106,10 @@ def main():
                 # IPv4: libxudp's call, iph->check alone (XCSUM_F_IPHDR_ONLY)
                 d_bdesc = d_desc.clone()
                 cs = []
-                for _ in range(args.reps):
+                for k in range(args.reps):
                     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                     e0.record(s)
-                    eng.batch_device(d_umem, d_bdesc, n, d_out,
+                    eng.batch_device(d_umems[k % args.rot], d_bdesc, n, d_out,
                                      X.MODE_V6 if fam == 6 else X.MODE_V4_LEGACY,
                                      X.F_INPLACE | (X.F_IPHDR_ONLY if fam == 4 else 0), L + hdr,
                                      stream=s.cuda_stream)
