@@ -522,7 +522,11 @@ extern "C" int probe_stream_read_copy(void *p, uint64_t nbytes, uint64_t fstride
  * arithmetic -- per frame the 16-byte descriptor (coalesced), the seven dwords
  * at (eth + 12) & ~3 (one dwordx4 + one dwordx3, the header line), and with
  * `write` a 2-byte store at eth + 24 that depends on them -- FPT = 4 frames per
- * thread, all loads issued first, one launch per batch.  The same-run ceiling
+ * thread, all loads issued first, one launch per batch.  write 2/3/4 store the
+ * whole 32-byte sector / 64-byte block / 128-byte line holding eth + 24
+ * instead (blind, data not kept): whether a full-sector write-back is
+ * cheaper than a partial one at the memory side; write 5/6/7 the 2-byte
+ * store nontemporal / with sc0 sc1 / with nt (its cache policy).  The same-run ceiling
  * of an access pattern that is one scattered line read (and one scattered
  * partial write) per frame, not a stream. */
 struct probe_desc { uint64_t addr; uint32_t len, options; };
@@ -587,8 +591,29 @@ __global__ void __launch_bounds__(256) header_touch(uint8_t *umem, const probe_d
 		acc ^= v;
 		if (write && q0 + 256u * j < n) {
 			uint8_t *e = umem + (((uint64_t)d[j].y << 32) | d[j].x);
-			e[24] = (uint8_t)v;
-			e[25] = (uint8_t)(v >> 8);
+			typedef __attribute__((address_space(1))) uint16_t w2;
+			if (write == 1) {
+				e[24] = (uint8_t)v;
+				e[25] = (uint8_t)(v >> 8);
+			} else if (write == 5) {
+				__builtin_nontemporal_store((uint16_t)v, (w2 *)(e + 24));
+			} else if (write == 6) {
+				asm volatile("global_store_short %0, %1, off sc0 sc1"
+					     :: "v"(e + 24), "v"(v) : "memory");
+			} else if (write == 7) {
+				asm volatile("global_store_short %0, %1, off nt"
+					     :: "v"(e + 24), "v"(v) : "memory");
+			} else {
+				/* 2: the whole 32-byte sector holding eth + 24, 3: its
+				 * 64-byte block, 4: its 128-byte line -- blind stores
+				 * (the data is not kept; a timing probe) */
+				const int sz = write == 2 ? 32 : write == 3 ? 64 : 128;
+				typedef __attribute__((address_space(1))) u32x4 w4;
+				w4 *s = (w4 *)((uintptr_t)(e + 24) & ~(uintptr_t)(sz - 1));
+				const u32x4 x = {v, v ^ 1u, v ^ 2u, v ^ 3u};
+				for (int k = 0; k < sz / 16; k++)
+					s[k] = x;
+			}
 		}
 	}
 	if (acc == 0x9e3779b9u)

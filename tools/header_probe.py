@@ -1,7 +1,9 @@
 #!/usr/bin/env python3
 """The header-only access pattern alone (tools/hbm_probe.hip
 probe_header_touch_mode): per frame the 16-byte descriptor, the seven header
-dwords at (eth+12)&~3 and optionally a 2-byte store at eth+24, no arithmetic,
+dwords at (eth+12)&~3 and optionally a 2-byte store at eth+24 (write 1) or a blind store of the
+whole 32-byte sector / 64-byte block / 128-byte line holding it (write 2/3/4), or
+the 2-byte store nontemporal / sc0 sc1 / nt (write 5/6/7), no arithmetic,
 over BASELINE config 2's frames packed and in xudp's slots -- with the
 header loads plain (mode 0, as the library's XCSUM_F_IPHDR_ONLY kernel),
 nontemporal (1) or with the cache-policy bits nt / sc1 / sc0 sc1 (2-4).
