@@ -67,7 +67,7 @@ enum xcsum_mode {
 				 IPv6 check 0 = invalid), nonzero otherwise (malformed
 				 frames: 0xffff).  With XCSUM_F_IPHDR the IPv4 header
 				 must verify too for out[i] to be 0.  Never writes. */
-#define XCSUM_F_IPHDR_ONLY 0x80u /* xcsum_batch_device only: libxudp's IPv4 TX
+#define XCSUM_F_IPHDR_ONLY 0x80u /* xcsum_batch_device / _host: libxudp's IPv4 TX
 				 checksum work and nothing else -- iph->check
 				 (xudp_checksum_half, packet.c:43-66) computed from
 				 the 20-byte header, udp->check left as it is (0,
@@ -81,8 +81,11 @@ enum xcsum_mode {
 				 XCSUM_MODE_V6).  A frame is malformed under the
 				 rule of the other modes (shorter than 42 bytes, UDP
 				 length > 65535; AUTO: another h_proto): out[i] 0
-				 (0xffff under VERIFY), counted.  XCSUM_MODE_V6 and
-				 the host entry points: -XCSUM_ERR_INVAL. */
+				 (0xffff under VERIFY), counted.  XCSUM_MODE_V6:
+				 -XCSUM_ERR_INVAL.  On host frames only the first 42
+				 bytes of each cross PCIe (gathered, or read in place
+				 from a mapped UMEM), and a context's resident
+				 workgroups do not take such batches (launched). */
 
 /* Error codes (returned negated). */
 enum {

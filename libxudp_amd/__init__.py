@@ -34,7 +34,7 @@ F_IPHDR = 0x2
 F_V4_RFC = 0x4
 F_ZEROCOPY = 0x8
 F_VERIFY = 0x10
-F_IPHDR_ONLY = 0x80   # libxudp's IPv4 TX call: iph->check alone (xcsum_batch_device)
+F_IPHDR_ONLY = 0x80   # libxudp's IPv4 TX call: iph->check alone (batch_device / batch_host)
 
 ERR_INVAL = 9000
 ERR_HIP = 9001

@@ -117,19 +117,29 @@ extern "C" int xudp_packet_udp_batch(xcsum_ctx *ctx, struct packet_info *infos, 
 			base = r.host;
 	/* IPv4 without XCSUM_F_V4_RFC: udp->check stays 0 (packet.c:125) and
 	 * only iph->check is computed, from the 20-byte header (its tot_len
-	 * field included), so the kernel is handed eth + IP + UDP headers only
-	 * (42 bytes; the UDP result it also returns is not used) */
+	 * field included).  A batch of such frames only is libxudp's IPv4 call,
+	 * XCSUM_F_IPHDR_ONLY: the header kernel on the frames' first 42 bytes.
+	 * In a mixed batch, and on a context with resident workgroups (they run
+	 * the checksum kernel, and serve libxudp's 100-frame batches faster than
+	 * a launch: DESIGN.md 5.10), the checksum kernel is handed eth + IP +
+	 * UDP headers of those frames (42 bytes; the UDP result it also returns
+	 * is unused). */
 	const bool v4_rfc = (flags & XCSUM_F_V4_RFC) != 0;
+	bool v4_hdr = !v4_rfc;   /* every frame needs its IPv4 header only */
+	for (uint32_t i = 0; i < n && v4_hdr; i++)
+		v4_hdr = infos[i].family == AF_INET;
+	const bool hdr_only = v4_hdr && ctx->res_wg == 0;   /* the header kernel */
 	std::vector<struct xcsum_desc> desc(n);
 	std::vector<uint16_t> out(n), out_ip(n);
 	for (uint32_t i = 0; i < n; i++) {
 		desc[i].addr = (uint64_t)((uint8_t *)infos[i].packet - base);
 		desc[i].len = (uint32_t)infos[i].len;
-		if (infos[i].family == AF_INET && !v4_rfc && desc[i].len > 42u)
+		if (!hdr_only && infos[i].family == AF_INET && !v4_rfc && desc[i].len > 42u)
 			desc[i].len = 42u;
 		desc[i].options = 0;
 	}
-	uint32_t kflags = XCSUM_F_IPHDR | (flags & (XCSUM_F_V4_RFC | XCSUM_F_ZEROCOPY));
+	uint32_t kflags = (hdr_only ? XCSUM_F_IPHDR_ONLY : XCSUM_F_IPHDR) |
+			  (flags & (XCSUM_F_V4_RFC | XCSUM_F_ZEROCOPY));
 	if (!base)
 		kflags &= ~XCSUM_F_ZEROCOPY;
 	/* Staged copies gather frame by frame when the frames are the caller's
@@ -137,14 +147,14 @@ extern "C" int xudp_packet_udp_batch(xcsum_ctx *ctx, struct packet_info *infos, 
 	 * could read unmapped pages between them), and when only headers are
 	 * needed (42 of ~1500 bytes per frame).  Whole frames inside one
 	 * registered UMEM go by DMA of the range, no host copy. */
-	bool hdr_only = !v4_rfc;
-	for (uint32_t i = 0; i < n && hdr_only; i++)
-		hdr_only = infos[i].family == AF_INET;
-	const bool gather = !(kflags & XCSUM_F_ZEROCOPY) && (!base || hdr_only);
-	int rc = xcsum::batch_host_impl(ctx, base, desc.data(), n, out.data(), out_ip.data(),
-					XCSUM_MODE_AUTO, kflags, gather);
+	const bool gather = !(kflags & XCSUM_F_ZEROCOPY) && (!base || v4_hdr);
+	int rc = xcsum::batch_host_impl(ctx, base, desc.data(), n, out.data(),
+					hdr_only ? nullptr : out_ip.data(), XCSUM_MODE_AUTO, kflags,
+					gather);
 	if (rc)
 		return rc;
+	if (hdr_only)
+		out_ip.swap(out);   /* the header kernel's result is iph->check */
 	for (uint32_t i = 0; i < n; i++) {
 		uint8_t *eth = (uint8_t *)infos[i].packet;
 		if (infos[i].family == AF_INET) {

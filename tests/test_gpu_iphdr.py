@@ -254,11 +254,119 @@ def test_rejects(torch_cuda, engine):
     with pytest.raises(X.XcsumError) as e:
         engine.batch_device(d, d, 1, o, X.MODE_V6, X.F_IPHDR_ONLY)
     assert e.value.rc == -X.ERR_INVAL
-    umem, desc = X.gen_frames_host(4, 4, 10)
+    umem, desc = X.gen_frames_host(4, 6, 10)
     out = np.zeros(4, np.uint16)
     with pytest.raises(X.XcsumError) as e:
-        engine.batch_host(umem, desc, out, X.MODE_V4_LEGACY, X.F_IPHDR_ONLY)
+        engine.batch_host(umem, desc, out, X.MODE_V6, X.F_IPHDR_ONLY)
     assert e.value.rc == -X.ERR_INVAL
+
+
+def host_call(eng, umem, desc, mode, flags, buf=None):
+    """xcsum_batch_host with XCSUM_F_IPHDR_ONLY on a copy of umem (or in
+    buf, a registered UMEM): (out, frames after)"""
+    if buf is None:
+        buf = umem.copy()
+    else:
+        buf[:len(umem)] = umem
+    out = np.full(len(desc), 0x5a5a, np.uint16)
+    eng.batch_host(buf, desc, out, mode, X.F_IPHDR_ONLY | flags)
+    return out, buf[:len(umem)].copy()
+
+
+@pytest.mark.parametrize("n", [100, 20000, 70000])
+@pytest.mark.parametrize("transport", ["pageable", "registered", "zerocopy", "resident"])
+def test_host_batch_matches_device(torch_cuda, engine, transport, n):
+    """libxudp's IPv4 call on host-resident frames (xcsum_batch_host,
+    XCSUM_F_IPHDR_ONLY): the frames' first 42 bytes gathered into the pinned
+    stage (pageable memory; 100 frames go by the direct path, 70000 span two
+    chunks), or read in place over PCIe from a registered, GPU-mapped UMEM;
+    a context with resident workgroups launches it.  Results and frames
+    after the in-place call are identical to the device call's."""
+    rng = np.random.default_rng(n)
+    umem, desc = random_frames(rng, n, lmax=1000)
+    got_d, after_d = run(torch_cuda, engine, umem, desc, flags=X.F_INPLACE)
+    assert np.array_equal(got_d, hdr_np(umem, desc["addr"]))
+    eng, buf, flags = engine, None, 0
+    if transport == "resident":
+        eng = X.Engine(0)
+        eng.set_resident(8)
+    if transport in ("registered", "zerocopy"):
+        buf = X.umem_buffer(len(umem))
+        engine.register_umem(buf)
+        assert engine.umem_mapped(buf) == 1
+        flags = X.F_ZEROCOPY if transport == "zerocopy" else 0
+    try:
+        for mode in (X.MODE_V4_LEGACY, X.MODE_AUTO):
+            got, after = host_call(eng, umem, desc, mode, X.F_INPLACE | flags, buf)
+            assert np.array_equal(got, got_d), mode
+            assert np.array_equal(after, after_d), mode
+        got, after = host_call(eng, umem, desc, X.MODE_V4_RFC, flags, buf)  # result only
+        assert np.array_equal(got, got_d) and np.array_equal(after, umem)
+        assert eng.take_errors() == 0
+    finally:
+        if buf is not None:
+            engine.unregister_umem(buf)
+        if eng is not engine:
+            eng.close()
+
+
+@pytest.mark.parametrize("register", [False, True])
+def test_host_batch_slots(torch_cuda, engine, register):
+    """xudp's own layout (one frame per 4096-byte chunk, eth at F+342, xudp's
+    headers from the generator): the host call writes iph->check only, the
+    value orc_ip_checksum_half (packet.c:43-66) gives."""
+    n = 3000
+    desc, nbytes = X.gen_layout(n, 4, 0, 1472, seed=9, stride=4096, offset=342)
+    umem = np.zeros(nbytes + 64, np.uint8)
+    X.gen_fill_host(umem, desc, 4, seed=9)
+    for a in desc["addr"]:
+        umem[int(a) + 24:int(a) + 26] = 0
+    buf = None
+    if register:
+        buf = X.umem_buffer(len(umem))
+        engine.register_umem(buf)
+    try:
+        got, after = host_call(engine, umem, desc, X.MODE_V4_LEGACY, X.F_INPLACE, buf)
+    finally:
+        if buf is not None:
+            engine.unregister_umem(buf)
+    P = oracle.port()
+    for i in range(0, n, 11):
+        a = int(desc["addr"][i])
+        ip = np.ascontiguousarray(umem[a + 14:a + 34])
+        assert got[i] == P.orc_ip_checksum_half(ip.ctypes.data)
+    assert np.array_equal(got, hdr_np(umem, desc["addr"]))
+    exp = umem.copy()
+    for a, c in zip(desc["addr"], got):
+        exp[int(a) + 24:int(a) + 26] = np.array([c], "<u2").view(np.uint8)
+    assert np.array_equal(after, exp)
+
+
+def test_host_batch_malformed_verify(torch_cuda, engine):
+    """The host call's rules are the device call's: malformed frames (short,
+    UDP length past 16 bits, another h_proto under AUTO) are counted and left
+    alone, IPv6 frames under AUTO are left alone and not counted, and VERIFY
+    (which never writes) flags exactly the corrupted headers."""
+    rng = np.random.default_rng(8)
+    umem = rng.integers(0, 256, 300000, dtype=np.uint8)
+    lens = [0, 13, 41, 42, 65569, 65570, 100, 61, 100, 100, 1500]
+    protos = [0x0800] * 6 + [0x86DD, 0x86DD, 0x0806, 0x0000, 0x0800]
+    desc = np.zeros(len(lens), X.DESC_DTYPE)
+    addr = 5
+    for i, (ln, proto) in enumerate(zip(lens, protos)):
+        desc["addr"][i], desc["len"][i] = addr, ln
+        umem[addr + 12:addr + 14] = (proto >> 8, proto & 0xff)
+        umem[addr + 24:addr + 26] = 0
+        addr += max(ln, 64) + 3
+    for mode in (X.MODE_AUTO, X.MODE_V4_LEGACY):
+        for flags in (X.F_INPLACE, X.F_VERIFY, X.F_VERIFY | X.F_INPLACE):
+            engine.take_errors()
+            got_d, after_d = run(torch_cuda, engine, umem, desc, mode, flags)
+            err_d = engine.take_errors()
+            got, after = host_call(engine, umem, desc, mode, flags)
+            assert np.array_equal(got, got_d), (mode, flags)
+            assert np.array_equal(after, after_d), (mode, flags)
+            assert engine.take_errors() == err_d > 0
 
 
 @pytest.mark.slow

@@ -11,7 +11,12 @@ frames); then the receive side, xcsum_rx_host with VERIFY on the same frames
 pinned H2D copy rate for context.  One JSON line per variant.
 --layout umem puts one frame per 4096-byte chunk (xudp's UMEM, SURVEY a14;
 256K frames, 1 GiB), the layout an AF_XDP RX ring hands over.
-Usage: python tools/bench_e2e.py [--config 2] [--reps 5] [--layout umem]"""
+--iphdr-only times libxudp's IPv4 TX call instead (XCSUM_F_IPHDR_ONLY:
+iph->check alone; 42 bytes per frame gathered, or read in place over PCIe)
+against the reference's own xudp_checksum_half on the host (oracle/_ref
+through bench.cpu_baseline: 1 and 16 threads on a 65,536-frame sample of
+the config), and skips the receive side.
+Usage: python tools/bench_e2e.py [--config 2] [--reps 5] [--layout umem] [--iphdr-only]"""
 import argparse
 import json
 import os
@@ -32,6 +37,7 @@ def main():
     ap.add_argument("--config", type=int, default=2)
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--layout", default="packed", choices=["packed", "umem"])
+    ap.add_argument("--iphdr-only", action="store_true")
     args = ap.parse_args()
     import torch
     cfg = dict(bench.CONFIGS[args.config], id=args.config)
@@ -50,7 +56,19 @@ def main():
     out = np.zeros(n, dtype=np.uint16)
     eng = X.Engine(0)
     import oracle
-    exp = oracle.batch(umem, desc, cfg["mode"])
+    mode, extra = cfg["mode"], 0
+    if args.iphdr_only:
+        assert cfg["family"] == 4, "--iphdr-only: an IPv4 config"
+        mode, extra = X.MODE_V4_LEGACY, X.F_IPHDR_ONLY
+        alg = 22 * n
+        for a in desc["addr"]:           # as iph_build leaves it
+            umem[int(a) + 24:int(a) + 26] = 0
+    exp = oracle.batch(umem, desc, mode, extra)
+    if args.iphdr_only:
+        # the reference on the host (bench.cpu_baseline's legs, its own
+        # 65,536-frame sample of the config)
+        cb = bench.cpu_baseline(cfg, seconds=10.0, flags=X.F_IPHDR_ONLY)
+        print(json.dumps({"variant": "reference_cpu", "frames": n, **cb}), flush=True)
 
     # raw pinned H2D rate of the same bytes
     pin = torch.empty(umem.nbytes, dtype=torch.uint8).pin_memory()
@@ -69,17 +87,17 @@ def main():
 
     for variant in ("pageable", "registered", "zerocopy"):
         for inplace in (False, True):
-            flags = X.F_INPLACE if inplace else 0
+            flags = (X.F_INPLACE if inplace else 0) | extra
             if variant != "pageable":
                 eng.register_umem(umem)
                 assert eng.umem_mapped(umem), "registered UMEM not GPU-mapped"
             if variant == "zerocopy":
                 flags |= X.F_ZEROCOPY
-            eng.batch_host(umem, desc, out, cfg["mode"], flags)  # warm-up
+            eng.batch_host(umem, desc, out, mode, flags)  # warm-up
             ok = bool(np.array_equal(out, exp))
             t0 = time.perf_counter()
             for _ in range(args.reps):
-                eng.batch_host(umem, desc, out, cfg["mode"], flags)
+                eng.batch_host(umem, desc, out, mode, flags)
             dt = (time.perf_counter() - t0) / args.reps
             if variant != "pageable":
                 eng.unregister_umem(umem)
@@ -87,12 +105,18 @@ def main():
                 umem2, _ = X.gen_frames_host(n, cfg["family"], cfg["pmin"], cfg["pmax"],
                                              seed=bench.SEED_BASE ^ args.config, **lay)
                 umem[:] = umem2
+                if args.iphdr_only:
+                    for a in desc["addr"]:
+                        umem[int(a) + 24:int(a) + 26] = 0
             print(json.dumps({"variant": variant, "inplace": inplace, "frames": n,
                               "layout": args.layout,
                               "ms": round(dt * 1e3, 3),
                               "GiBps_alg": round(alg / dt / 2**30, 1),
                               "GBps_frames": round(umem.nbytes / dt / 1e9, 1),
                               "mpps": round(n / dt / 1e6, 1), "parity": ok}), flush=True)
+    if args.iphdr_only:
+        eng.close()
+        return
 
     # receive side: the same frames with valid checksums written in
     # (RFC rules, IPv4 header too), verified by xcsum_rx_host
