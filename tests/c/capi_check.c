@@ -91,6 +91,25 @@ static void check_batches(xcsum_ctx *c, uint32_t family, uint32_t stride, uint32
 		bad += v != exp[i];
 	}
 	CHECK(bad == 0, "in-place udp->check v%u: %u wrong", family, bad);
+	if (family == 4) {
+		/* libxudp's IPv4 call: iph->check alone (XCSUM_F_IPHDR_ONLY), read
+		 * in place from the UMEM when the GPU maps it, else gathered */
+		uint16_t *exp_ip = calloc(n, 2);
+		orc_batch(umem, desc, n, exp_ip, XCSUM_MODE_V4_LEGACY, (int)XCSUM_F_IPHDR_ONLY);
+		memset(got, 0, 2 * n);
+		CHECK(xcsum_batch_host(c, umem, desc, n, got, XCSUM_MODE_V4_LEGACY,
+				       XCSUM_F_IPHDR_ONLY | XCSUM_F_INPLACE) == 0, "batch_host iphdr only");
+		CHECK(count_diff(got, exp_ip, n) == 0, "iphdr only: %u mismatches",
+		      count_diff(got, exp_ip, n));
+		bad = 0;
+		for (uint32_t i = 0; i < n; i++) {
+			uint16_t v;
+			memcpy(&v, umem + desc[i].addr + 24, 2);
+			bad += v != exp_ip[i];
+		}
+		CHECK(bad == 0, "in-place iph->check: %u wrong", bad);
+		free(exp_ip);
+	}
 	CHECK(xcsum_unregister_umem(c, umem) == 0, "unregister_umem");
 
 	/* receive side on the host frames: write RFC checksums (and the IPv4
