@@ -677,3 +677,43 @@ extern "C" int probe_line_halves(const void *p, uint64_t nlines, uint64_t stride
 			   (const uint8_t *)p, nlines, stride, halves, out);
 	return hipGetLastError() == hipSuccess ? 0 : -1;
 }
+
+/* Scattered-write probe (round 5): the stores of the IPv4 in-place build
+ * (build_hdr_kernel, csrc/xcsum_build.hip) with nothing else -- per xudp
+ * slot the 42 header bytes at F + 342 (2 + 8 + 16 + 16 bytes: one 64-byte
+ * block, F + 320 .. F + 384) and, with `desc`, the frame's 16-byte
+ * descriptor (coalesced), one thread per frame.  `msgs` adds the coalesced
+ * 16-byte message load the build kernel makes per frame.  The same-run
+ * bound of one scattered partial-block write per frame. */
+__global__ void __launch_bounds__(256) slot_write(uint8_t *umem, uint32_t n, int desc, int msgs,
+						  const u32x4 *m, u32x4 *d)
+{
+	typedef __attribute__((address_space(1))) u32x4 w4;
+	typedef __attribute__((address_space(1))) uint64_t w8;
+	typedef __attribute__((address_space(1))) uint16_t w2;
+	const uint32_t q = blockIdx.x * 256u + threadIdx.x;
+	if (q >= n)
+		return;
+	u32x4 v = {q, q ^ 0x55u, q + 7u, 0x0800u};
+	if (msgs)
+		v = *((gu32x4 *)(m + q));
+	uint8_t *e = umem + (uint64_t)q * 4096u + 342u;
+	*(w2 *)e = (uint16_t)v.x;
+	*(w8 *)(e + 2) = ((uint64_t)v.y << 32) | v.z;
+	*(w4 *)(e + 10) = v;
+	*(w4 *)(e + 26) = v;
+	if (desc) {
+		const u32x4 o = {(uint32_t)(q * 4096u + 342u), 0u, 1514u, 0u};
+		*(w4 *)(d + q) = o;
+	}
+}
+
+extern "C" int probe_slot_write(void *umem, uint32_t n, int desc, int msgs, const void *m,
+				void *d, void *stream)
+{
+	if (!n)
+		return -1;
+	hipLaunchKernelGGL(slot_write, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream,
+			   (uint8_t *)umem, n, desc, msgs, (const u32x4 *)m, (u32x4 *)d);
+	return hipGetLastError() == hipSuccess ? 0 : -1;
+}

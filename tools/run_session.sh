@@ -25,6 +25,8 @@
 #   iphdr_pmc FETCH/WRITE/request counters of the header-only kernel, one
 #             rocprofv3 pass per counter set and leg (tools/pmc_legs.py
 #             summarises gpurun_out/<tag>/pmc)
+#   build_pmc FETCH/WRITE/request counters of the IPv4 in-place build
+#             (build_hdr_kernel through tools/bench_build.py)
 #   profile   tools/profile_round.sh <tag>/profile (bench lines, kernel
 #             stats, PMC summaries)
 set -u
@@ -117,6 +119,20 @@ PY
           [ $rc -eq 0 ] || exit $rc
         done
       done
+    done ;;
+  build_pmc)
+    # the IPv4 in-place build (build_hdr_kernel, tools/bench_build.py
+    # inplace): FETCH/WRITE and the L2's memory-side requests, one pass each
+    mkdir -p gpurun_out/$t/bpmc
+    for pmc in FETCH_SIZE WRITE_SIZE \
+               "TCC_EA0_WRREQ_sum TCC_EA0_WRREQ_64B_sum TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum"; do
+      tag=$(echo "$pmc" | cut -d' ' -f1)
+      d=gpurun_out/$t/bpmc/inplace_$tag
+      timeout -s KILL 120 rocprofv3 --pmc $pmc --output-format csv -d $d -o run -- \
+        python3 tools/bench_build.py --modes inplace --reps 2 --rot 1 > $d.log 2>&1
+      rc=$?
+      echo "build pmc $tag rc=$rc"
+      [ $rc -eq 0 ] || exit $rc
     done ;;
   header_probe)
     # the header-only access pattern with each load cache policy: timing,
