@@ -1479,18 +1479,33 @@ static int ensure_gather(xcsum_ctx *c)
 }
 
 /* Gather a host batch frame by frame (one host memcpy per frame into the
- * pinned stage) instead of copying the UMEM range it spans, when the frames
- * fill less than 1/8 of that range and the UMEM is pageable.  A registered
- * UMEM keeps the range copy (pure DMA, no host memcpy).  Measured on xudp's
- * 4096-byte chunks, pageable (tools/bench_e2e.py --layout umem,
- * profiles/r02/session2/rx_gather/): 64-byte frames 23.3 -> 6.9 ms per
- * 256K-frame receive batch; MTU frames 22.7 -> 33.6 ms (the single-thread
- * memcpy of 1.5 KB frames loses to the runtime's pipelined pageable copy of
- * the whole range), hence the 1/8. */
+ * pinned stage, gather_frames) instead of copying the UMEM range it spans,
+ * when the frames fill less than half of that range and the UMEM is
+ * pageable.  A registered UMEM keeps the range copy (pure DMA, no host
+ * memcpy).  Measured on xudp's 4096-byte chunks, pageable
+ * (tools/bench_e2e.py --layout umem): round 2, one thread
+ * (profiles/r02/session2/rx_gather/): 64-byte frames 23.3 -> 6.9 ms per
+ * 256K-frame receive batch, MTU frames 22.7 -> 33.6 ms, hence a 1/8 rule;
+ * round 5, the copies and the in-place stores split over STAGE_THREADS
+ * threads, same-run A/B against the one-thread library
+ * (profiles/r05/host/r05v_*): 256K MTU frames gathered instead of
+ * range-copied, TX 20.3 -> 14.3 ms, in place 24.2 -> 12.2, receive 23.2 ->
+ * 11.4; 64-byte frames TX 4.7 -> 3.8, in place 9.5 -> 4.9, receive 5.8 ->
+ * 3.9. */
+static uint64_t gather_ratio()
+{
+	/* XCSUM_GATHER_RATIO (A/B only): the 2 above.  Read per call; a
+	 * function-local static here was reported as a data race by the
+	 * ThreadSanitizer build (tests/c/tsan, two threads' first calls) */
+	const char *e = getenv("XCSUM_GATHER_RATIO");
+	const int v = e ? atoi(e) : 0;
+	return (uint64_t)(v > 0 ? v : 2);
+}
+
 static bool gather_pays(const xcsum_ctx *c, const uint8_t *h_umem, uint64_t lo, uint64_t hi,
 			uint64_t frame_bytes)
 {
-	return hi - lo > 8 * frame_bytes + 4096 &&
+	return hi - lo > gather_ratio() * frame_bytes + 4096 &&
 	       !find_region(c, h_umem + lo, h_umem + hi);
 }
 
@@ -1528,12 +1543,20 @@ static inline uint64_t stage_off(uint64_t pos, uint64_t addr)
  * (config 2 frames, pageable, tools/bench_e2e.py: 23.0 GiB/s with one thread) */
 static constexpr int STAGE_THREADS = 4;
 
-static void stage_copy(uint8_t *dst, const uint8_t *src, uint64_t n)
+/* threads for a host copy of n bytes in `pieces` memcpys (a gather of
+ * small frames is bound by the latency of each frame's lines, not bytes) */
+static int stage_threads(uint64_t n, uint32_t pieces = 1)
 {
 	const unsigned hw = std::thread::hardware_concurrency();
-	int k = n >= (4u << 20) ? STAGE_THREADS : 1;
+	int k = n >= (4u << 20) || pieces >= 16384u ? STAGE_THREADS : 1;
 	if (hw && (int)hw < 2 * k)
 		k = hw >= 4 ? (int)hw / 2 : 1;
+	return k;
+}
+
+static void stage_copy(uint8_t *dst, const uint8_t *src, uint64_t n)
+{
+	const int k = stage_threads(n);
 	if (k <= 1) {
 		memcpy(dst, src, n);
 		return;
@@ -1557,6 +1580,62 @@ static void stage_copy(uint8_t *dst, const uint8_t *src, uint64_t n)
 	for (int t = 1; t <= started; t++)
 		if (th[t].joinable())
 			th[t].join();
+}
+
+/* Frame-by-frame gather into a pinned stage: frame k at its 16-byte phase
+ * (stage_off), at most `cap` bytes of it; ds[k] = its staged descriptor
+ * (the frame's own length, for the kernel's rules).  From 4 MiB of staged
+ * bytes up the copies are split by bytes over up to STAGE_THREADS threads,
+ * as stage_copy.  Returns the staged bytes. */
+static uint64_t gather_frames(uint8_t *stage, const uint8_t *umem, const struct xcsum_desc *d,
+			      struct xcsum_desc *ds, uint32_t cnt, uint32_t cap)
+{
+	uint64_t pos = 0;
+	for (uint32_t k = 0; k < cnt; k++) {
+		const uint64_t off = stage_off(pos, d[k].addr);
+		ds[k] = xcsum_desc{off, d[k].len, 0};
+		pos = off + (d[k].len < cap ? d[k].len : cap);
+	}
+	auto copy = [stage, umem, d, ds, cap](uint32_t k0, uint32_t k1) {
+		for (uint32_t k = k0; k < k1; k++)
+			memcpy(stage + ds[k].addr, umem + d[k].addr, d[k].len < cap ? d[k].len : cap);
+	};
+	const int nt = stage_threads(pos, cnt);
+	if (nt <= 1) {
+		copy(0, cnt);
+		return pos;
+	}
+	/* thread t copies the frames staged in [pos * t / nt, pos * (t+1) / nt) */
+	uint32_t b[STAGE_THREADS + 1];
+	b[0] = 0;
+	b[nt] = cnt;
+	for (int t = 1; t < nt; t++) {
+		const uint64_t target = pos / nt * t;
+		uint32_t lo = b[t - 1], hi = cnt;
+		while (lo < hi) {   /* first frame staged at or after target */
+			const uint32_t mid = lo + (hi - lo) / 2;
+			if (ds[mid].addr < target)
+				lo = mid + 1;
+			else
+				hi = mid;
+		}
+		b[t] = lo;
+	}
+	std::thread th[STAGE_THREADS];
+	int started = 0;
+	for (int t = 1; t < nt; t++) {
+		try {
+			th[t] = std::thread(copy, b[t], b[t + 1]);
+			started = t;
+		} catch (...) {
+			copy(b[t], b[t + 1]);   /* no thread: copy here */
+		}
+	}
+	copy(b[0], b[1]);
+	for (int t = 1; t <= started; t++)
+		if (th[t].joinable())
+			th[t].join();
+	return pos;
 }
 
 /* The source of a host-to-device copy of caller memory [p, p + n): the
@@ -1605,7 +1684,9 @@ struct Pending {
 	bool gathered;   /* receive: records hold staged offsets, to be fixed up */
 };
 
-/* results of one finished chunk -> caller arrays / host frames */
+/* results of one finished chunk -> caller arrays / host frames.  The
+ * in-place stores touch one line per frame: from 16384 frames up they are
+ * split over up to STAGE_THREADS threads, as the gathers. */
 static void retire(const Pending &pd, const uint16_t *h_res, uint8_t *h_umem,
 		   const struct xcsum_desc *h_desc, uint16_t *h_out, uint16_t *h_out_ip,
 		   uint32_t mode, uint32_t flags)
@@ -1615,8 +1696,10 @@ static void retire(const Pending &pd, const uint16_t *h_res, uint8_t *h_umem,
 		memcpy(h_out + pd.first, res, pd.count * sizeof(uint16_t));
 	if (h_out_ip)
 		memcpy(h_out_ip + pd.first, res_ip, pd.count * sizeof(uint16_t));
-	if (flags & XCSUM_F_INPLACE) {
-		for (uint32_t i = 0; i < pd.count; i++) {
+	if (!(flags & XCSUM_F_INPLACE))
+		return;
+	auto store = [&](uint32_t i0, uint32_t i1) {
+		for (uint32_t i = i0; i < i1; i++) {
 			const struct xcsum_desc &d = h_desc[pd.first + i];
 			uint8_t *eth = h_umem + d.addr;
 			int fam = host_family(eth, mode);
@@ -1638,7 +1721,29 @@ static void retire(const Pending &pd, const uint16_t *h_res, uint8_t *h_umem,
 					memcpy(eth + 24, &res_ip[i], 2);
 			}
 		}
+	};
+	const int nt = stage_threads(0, pd.count);
+	if (nt <= 1) {
+		store(0, pd.count);
+		return;
 	}
+	std::thread th[STAGE_THREADS];
+	int started = 0;
+	const uint32_t part = (pd.count + nt - 1) / nt;
+	for (int t = 1; t < nt; t++) {
+		const uint32_t i0 = part * t < pd.count ? part * t : pd.count;
+		const uint32_t i1 = part * (t + 1) < pd.count ? part * (t + 1) : pd.count;
+		try {
+			th[t] = std::thread(store, i0, i1);
+			started = t;
+		} catch (...) {
+			store(i0, i1);   /* no thread: store here */
+		}
+	}
+	store(0, part < pd.count ? part : pd.count);
+	for (int t = 1; t <= started; t++)
+		if (th[t].joinable())
+			th[t].join();
 }
 
 /* Wait for everything the host path queued on the context's streams.  Every
@@ -1897,14 +2002,9 @@ static int batch_host_run(xcsum_ctx *c, uint8_t *h_umem, const struct xcsum_desc
 		} else if (gather) {
 			/* each frame copied on its own into the pinned stage, then
 			 * one DMA of the packed bytes and one of their descriptors */
-			uint64_t pos = 0;
-			for (uint32_t k = 0; k < cnt; k++) {
-				const struct xcsum_desc &d = h_desc[i + k];
-				const uint64_t off = stage_off(pos, d.addr);
-				memcpy(c->h_stage[slot] + off, h_umem + d.addr, glen(d));
-				c->h_dstage[slot][k] = xcsum_desc{off, d.len, 0};
-				pos = off + glen(d);
-			}
+			const uint64_t pos = gather_frames(c->h_stage[slot], h_umem, h_desc + i,
+							   c->h_dstage[slot], cnt,
+							   hdr_only ? 42u : UINT32_MAX);
 			a.bias = 0;
 			a.flags = flags & (XCSUM_F_IPHDR | XCSUM_F_V4_RFC | XCSUM_F_VERIFY);
 			if (DIRECT_ON && pos <= DIRECT_MAX) {
@@ -2132,14 +2232,8 @@ static int rx_host_run(xcsum_ctx *c, const uint8_t *h_umem, const struct xcsum_d
 		if (zc) {
 			a.umem = zc->dev + (h_umem - zc->host);
 		} else if (gather) {
-			uint64_t pos = 0;
-			for (uint32_t k = 0; k < cnt; k++) {
-				const struct xcsum_desc &d = h_desc[i + k];
-				const uint64_t off = stage_off(pos, d.addr);
-				memcpy(c->h_stage[slot] + off, h_umem + d.addr, d.len);
-				c->h_dstage[slot][k] = xcsum_desc{off, d.len, 0};
-				pos = off + d.len;
-			}
+			const uint64_t pos = gather_frames(c->h_stage[slot], h_umem, h_desc + i,
+							   c->h_dstage[slot], cnt, UINT32_MAX);
 			if (DIRECT_ON && pos <= DIRECT_MAX) {
 				direct = true;
 				a.umem = c->v_stage[slot];
