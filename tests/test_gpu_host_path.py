@@ -133,6 +133,45 @@ def test_host_batch_small_frames_in_slots(engine, n, fam, register):
     assert np.array_equal(umem[mask], before[mask])
 
 
+@pytest.mark.parametrize("fam", [4, 6])
+def test_host_batch_mtu_frames_in_slots_gathered(engine, monkeypatch, fam):
+    """MTU frames one per 4096-byte chunk of a pageable UMEM fill ~1/3 of
+    the range: gathered frame by frame since round 5 (gather_pays), the
+    copies and the in-place stores split over threads (>= 16384 frames),
+    several chunks.  The same results with the range copy
+    (XCSUM_GATHER_RATIO=8, the rule before) and through the receive path."""
+    n = 40000
+    umem, desc = X.gen_frames_host(n, fam, 1000, 1472 if fam == 4 else 1452, seed=77 + fam,
+                                   stride=4096, offset=322 if fam == 6 else 342)
+    mode = X.MODE_V6 if fam == 6 else X.MODE_V4_RFC
+    exp = oracle.batch(umem, desc, mode)
+    before = umem.copy()
+    for ratio in ("8", None):
+        if ratio:
+            monkeypatch.setenv("XCSUM_GATHER_RATIO", ratio)
+        else:
+            monkeypatch.delenv("XCSUM_GATHER_RATIO", raising=False)
+        assert np.array_equal(host_batch(engine, umem, desc, mode), exp), ratio
+        assert np.array_equal(umem, before)
+    flags = X.F_INPLACE | (X.F_IPHDR if fam == 4 else 0)
+    assert np.array_equal(host_batch(engine, umem, desc, mode, flags), exp)
+    a = desc["addr"].astype(np.int64)
+    chk = 60 if fam == 6 else 40
+    assert np.array_equal(umem[a[:, None] + np.array([chk, chk + 1])].copy().view("<u2").ravel(),
+                          exp)
+    mask = np.ones(len(umem), dtype=bool)
+    for o in (chk, chk + 1) + ((24, 25) if fam == 4 else ()):
+        mask[a + o] = False
+    assert np.array_equal(umem[mask], before[mask])
+    # receive side: every frame now verifies; one flipped payload byte fails it
+    umem[a[n // 3] + 100] ^= 0x10
+    msgs = np.zeros(n, dtype=X.RX_MSG_DTYPE)
+    rx_flags = X.F_VERIFY | (X.F_IPHDR if fam == 4 else 0)
+    assert engine.rx_host(umem, desc, msgs, rx_flags) == n - 1
+    assert msgs["status"][n // 3] == X.RX_CSUM
+    assert np.array_equal(msgs.view(np.uint8), oracle.rx_batch(umem, desc, rx_flags).view(np.uint8))
+
+
 # ---- packet.c mirror --------------------------------------------------------
 
 MAC1, MAC2 = bytes.fromhex("020000000001"), bytes.fromhex("020000000002")
