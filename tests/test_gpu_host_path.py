@@ -254,6 +254,56 @@ def test_packet_udp_batch_random(engine, register):
         assert int(f[40:42].view("<u2")[0]) == oracle.batch(z, desc, X.MODE_V4_RFC)[0]
 
 
+@pytest.mark.parametrize("how", ["pageable", "registered", "resident"])
+def test_packet_udp_batch_ipv4_large(engine, how):
+    """An all-IPv4 batch of 70,000 frames through the hook: libxudp's IPv4
+    call (XCSUM_F_IPHDR_ONLY: 42-byte gathers from pageable memory over two
+    chunks, in-place header reads from a registered UMEM); on a context with
+    resident workgroups the checksum kernel on 42-byte headers.  Every
+    iph->check is xudp_checksum_half's value, every udp->check 0, nothing
+    else written but the headers."""
+    from test_gpu_iphdr import hdr_np
+    n, slot = 70000, 2048
+    rng = np.random.default_rng(9)
+    umem = np.zeros(n * slot, dtype=np.uint8)
+    eng = engine
+    if how == "registered":
+        umem = X.umem_buffer(n * slot)
+        engine.register_umem(umem)
+        assert engine.umem_mapped(umem) == 1
+    elif how == "resident":
+        eng = X.Engine(0)
+        eng.set_resident(8)
+    pay = rng.integers(0, 256, (n, 1400), dtype=np.uint8)
+    lens = rng.integers(0, 1401, n)
+    pas = []
+    for i in range(n):
+        off = slot * i + 320
+        umem[off + 64:off + 64 + lens[i]] = pay[i, :lens[i]]
+        pas.append(X.PacketArgs(4, b"", b"\x02\0\0\0\0\x01", b"\x02\0\0\0\0\x02",
+                                bytes([10, 0, 35, i & 255]), 3486 + (i & 1023),
+                                bytes([10, 1, (i >> 8) & 255, 1]), 40000, buf=umem, offset=off))
+        pas[-1].info.payload = umem.ctypes.data + off + 64     # payload already in place
+        pas[-1].info.payload_size = int(lens[i])
+    before = umem.copy()
+    try:
+        X.packet_udp_batch(eng, pas)
+    finally:
+        if how == "registered":
+            engine.unregister_umem(umem)
+        if eng is not engine:
+            eng.close()
+    eth = np.array([p.info.packet - umem.ctypes.data for p in pas], np.int64)
+    assert np.array_equal(np.array([p.info.len for p in pas]), lens + 42)
+    got = umem[eth[:, None] + np.array([24, 25])].copy().view("<u2").ravel()
+    assert np.array_equal(got, hdr_np(umem, eth))
+    assert not umem[eth[:, None] + np.array([40, 41])].any()      # packet.c:125
+    mask = np.ones(len(umem), dtype=bool)
+    for k in range(42):
+        mask[eth + k] = False
+    assert np.array_equal(umem[mask], before[mask])
+
+
 def _guarded_pages(npages=3, hole=1):
     """An anonymous mapping of `npages` pages whose page `hole` is PROT_NONE:
     reading the address range across it faults."""
