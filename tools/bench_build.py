@@ -6,6 +6,8 @@ unaligned sources) and in place (payload already in its slot, the
 xudp_frame_alloc path).  Bytes moved per frame: copy = payload read + frame
 (headers + payload) written + 16-byte message + 16-byte descriptor; in place
 = payload read + headers written + message + descriptor.
+Mode d2d_copy: the payload bytes copied device to device (torch's copy,
+contiguous) into the same UMEMs, the copy modes' bound.
 One JSON line per mode.  Usage: python tools/bench_build.py [--payload 1472]"""
 import argparse
 import json
@@ -56,6 +58,30 @@ def main():
         msgs["slot"] = np.arange(n, dtype=np.uint32)
         d_msgs = torch.from_numpy(msgs.view(np.uint8)).to(dev)
         d_src = torch.randint(0, 255, (n * stride + 16,), dtype=torch.uint8, device=dev)
+        if mode == "d2d_copy":
+            # the copy bound of the copy modes: the payload bytes copied
+            # device to device, contiguous (torch's copy kernel), into the
+            # rotated UMEMs; moved = read + write
+            s = torch.cuda.current_stream(dev)
+            src = d_src[:n * L]
+            for k in range(20):
+                d_umems[k % args.rot][:n * L].copy_(src)
+            torch.cuda.synchronize()
+            evs = []
+            for k in range(args.reps):
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(s)
+                d_umems[k % args.rot][:n * L].copy_(src)
+                e1.record(s)
+                evs.append((e0, e1))
+            torch.cuda.synchronize()
+            t = float(np.median([a.elapsed_time(b) for a, b in evs])) * 1e-3
+            print(json.dumps({"mode": mode, "rotating_umems": args.rot, "payload": L,
+                              "frames": n, "ms": round(t * 1e3, 4),
+                              "GBps_moved": round(2 * n * L / t / 1e9, 1),
+                              "pct_hbm_peak": round(100 * 2 * n * L / t / 8e12, 1)}), flush=True)
+            del d_src
+            continue
         flags = {"inplace": X.F_BUILD_INPLACE, "inplace_sum": X.F_BUILD_INPLACE,
                  "copy_aligned": X.F_SRC_ALIGNED}.get(mode, 0)
         # inplace_sum (A/B): IPv4 in place through the payload-summing build
