@@ -207,3 +207,36 @@ def test_rx_msg_layout_matches_c():
                                                text=True, check=True).stdout.split()]
     assert vals[0] == X.RX_MSG_DTYPE.itemsize == 64
     assert vals[1:] == [X.RX_MSG_DTYPE.fields[n][1] for n in names]
+
+
+def test_constants_match_header():
+    """Every mode, flag, error code, schedule and receive status the Python
+    binding mirrors has the value include/xcsum.h gives it (compiled by gcc
+    and printed, no GPU)."""
+    import subprocess
+    import tempfile
+    names = {
+        "XCSUM_MODE_V4_LEGACY": X.MODE_V4_LEGACY, "XCSUM_MODE_V4_RFC": X.MODE_V4_RFC,
+        "XCSUM_MODE_V6": X.MODE_V6, "XCSUM_MODE_AUTO": X.MODE_AUTO,
+        "XCSUM_F_INPLACE": X.F_INPLACE, "XCSUM_F_IPHDR": X.F_IPHDR,
+        "XCSUM_F_V4_RFC": X.F_V4_RFC, "XCSUM_F_ZEROCOPY": X.F_ZEROCOPY,
+        "XCSUM_F_VERIFY": X.F_VERIFY, "XCSUM_F_IPHDR_ONLY": X.F_IPHDR_ONLY,
+        "XCSUM_F_BUILD_INPLACE": X.F_BUILD_INPLACE, "XCSUM_F_SRC_ALIGNED": X.F_SRC_ALIGNED,
+        "XCSUM_ERR_INVAL": X.ERR_INVAL, "XCSUM_ERR_HIP": X.ERR_HIP,
+        "XCSUM_ERR_NODEV": X.ERR_NODEV, "XCSUM_ERR_NOMEM": X.ERR_NOMEM,
+        "XCSUM_ERR_NOT_REGISTERED": X.ERR_NOT_REGISTERED, "XCSUM_ERR_FRAME": X.ERR_FRAME,
+        "XCSUM_INPLACE_AUTO": X.INPLACE_AUTO, "XCSUM_INPLACE_FUSED": X.INPLACE_FUSED,
+        "XCSUM_INPLACE_TWO_PASS": X.INPLACE_TWO_PASS,
+        "XCSUM_RX_OK": X.RX_OK, "XCSUM_RX_PARSE": X.RX_PARSE, "XCSUM_RX_STATS": X.RX_STATS,
+        "XCSUM_RX_CSUM": X.RX_CSUM,
+    }
+    src = "#include <stdio.h>\n#include \"xcsum.h\"\nint main(void) {\n" + "".join(
+        f'  printf("{k} %lld\\n", (long long)({k}));\n' for k in names) + "  return 0;\n}\n"
+    d = tempfile.mkdtemp()
+    open(os.path.join(d, "c.c"), "w").write(src)
+    subprocess.run(["gcc", "-std=c11", "-I", os.path.join(ROOT, "include"), "-D__HIP_PLATFORM_AMD__",
+                    "-I/opt/rocm/include", os.path.join(d, "c.c"), "-o", os.path.join(d, "c")],
+                   check=True)
+    out = subprocess.run([os.path.join(d, "c")], capture_output=True, text=True, check=True).stdout
+    got = {k: int(v) for k, v in (line.split() for line in out.splitlines())}
+    assert got == names
