@@ -69,8 +69,8 @@ static void stage_copy(uint8_t *dst, const uint8_t *src, uint64_t n)
 /* Frame-by-frame gather into a pinned stage: frame k at its 16-byte phase
  * (stage_off), at most `cap` bytes of it; ds[k] = its staged descriptor
  * (the frame's own length, for the kernel's rules).  From 4 MiB of staged
- * bytes up the copies are split by bytes over up to STAGE_THREADS threads,
- * as stage_copy.  Returns the staged bytes. */
+ * bytes or 16384 frames up the copies are split by staged bytes over up to
+ * STAGE_THREADS threads (stage_threads).  Returns the staged bytes. */
 static uint64_t gather_frames(uint8_t *stage, const uint8_t *umem, const struct xcsum_desc *d,
 			      struct xcsum_desc *ds, uint32_t cnt, uint32_t cap)
 {
