@@ -337,6 +337,16 @@ static void *thread_main(void *arg)
 	uint8_t *umem = calloc(bytes + 64, 1);
 	uint16_t *exp = calloc(n, 2), *got = calloc(n, 2);
 	const uint32_t mode = j->family == 6 ? XCSUM_MODE_V6 : XCSUM_MODE_V4_LEGACY;
+	/* the same frames one per 4096-byte chunk (xudp's slots) in pageable
+	 * memory: gathered frame by frame, the copies and the in-place stores
+	 * split over the library's threads (>= 16384 frames) */
+	struct xcsum_desc *sdesc = calloc(n, sizeof(*sdesc));
+	uint64_t sbytes = 0;
+	j->err |= xcsum_gen_layout(n, j->family, 0, 1472, j->seed, 0, 8, 4096,
+				   j->family == 6 ? 322 : 342, sdesc, &sbytes) != 0;
+	uint8_t *sumem = calloc(sbytes + 64, 1);
+	uint16_t *sexp = calloc(n, 2);
+	const uint32_t chk = j->family == 6 ? 60 : 40;
 	uint8_t *d_umem = NULL;
 	struct xcsum_desc *d_desc = NULL;
 	uint16_t *d_out = NULL;
@@ -349,6 +359,8 @@ static void *thread_main(void *arg)
 		j->err |= xcsum_gen_fill_device(d_umem, d_desc, n, j->family, j->seed, 0, st) != 0;
 		j->err |= xcsum_gen_fill_host(umem, desc, n, j->family, j->seed, 0) != 0;
 		orc_batch(umem, desc, n, exp, (int)mode, 0);
+		j->err |= xcsum_gen_fill_host(sumem, sdesc, n, j->family, j->seed, 0) != 0;
+		orc_batch(sumem, sdesc, n, sexp, (int)mode, 0);
 	}
 	for (int it = 0; it < j->iters && !j->err; it++) {
 		/* device-resident batch on this thread's stream ... */
@@ -362,6 +374,17 @@ static void *thread_main(void *arg)
 		memset(got, 0, 2 * n);
 		j->err |= xcsum_batch_host(c, umem, desc, n, got, mode, 0) != 0;
 		j->bad += count_diff(got, exp, n) != 0;
+		/* ... and the sparse frames in place (check fields zeroed after) */
+		memset(got, 0, 2 * n);
+		j->err |= xcsum_batch_host(c, sumem, sdesc, n, got, mode, XCSUM_F_INPLACE) != 0;
+		uint32_t wrong = count_diff(got, sexp, n);
+		for (uint32_t i = 0; i < n; i++) {
+			uint16_t v;
+			memcpy(&v, sumem + sdesc[i].addr + chk, 2);
+			wrong += v != sexp[i];
+			memset(sumem + sdesc[i].addr + chk, 0, 2);
+		}
+		j->bad += wrong != 0;
 	}
 	/* resident workgroups (xcsum_ctx_set_resident): both threads' servers
 	 * live at once, libxudp-sized batches from different places, device
@@ -386,6 +409,9 @@ static void *thread_main(void *arg)
 	free(umem);
 	free(exp);
 	free(got);
+	free(sdesc);
+	free(sumem);
+	free(sexp);
 	return NULL;
 }
 
@@ -399,7 +425,7 @@ static void check_threads(void)
 		pthread_join(th[k], NULL);
 		CHECK(!jobs[k].err, "thread %d: a call failed", k);
 		CHECK(jobs[k].bad == 0, "thread %d: %d of %d iterations mismatched", k, jobs[k].bad,
-		      2 * jobs[k].iters);
+		      3 * jobs[k].iters);
 	}
 }
 
