@@ -240,3 +240,49 @@ def test_constants_match_header():
     out = subprocess.run([os.path.join(d, "c")], capture_output=True, text=True, check=True).stdout
     got = {k: int(v) for k, v in (line.split() for line in out.splitlines())}
     assert got == names
+
+
+def test_make_install_tree_links():
+    """`make -C libxudp_amd install PREFIX=...`: both
+    libraries, both headers and xcsum.pc land in the tree, and C programs
+    built with the .pc file's flags link and load from it -- setup (a)
+    against -lxcsum (a context without a GPU reports NODEV), setup (b) with
+    -lxcsum_packet -lxcsum (the mirror library finds libxcsum.so by its
+    $ORIGIN rpath).  No GPU."""
+    import tempfile
+    pre = tempfile.mkdtemp()
+    r = subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "libxudp_amd"), "install",
+                        f"PREFIX={pre}"], capture_output=True, text=True, timeout=900)
+    assert r.returncode == 0, r.stderr[-2000:]
+    for f in ("lib/libxcsum.so", "lib/libxcsum_packet.so", "include/xcsum.h",
+              "include/xudp_packet.h", "lib/pkgconfig/xcsum.pc"):
+        assert os.path.exists(os.path.join(pre, f)), f
+    pc = dict(line.split("=", 1) for line in open(os.path.join(pre, "lib/pkgconfig/xcsum.pc"))
+              .read().splitlines() if "=" in line and ":" not in line)
+    fields = dict(line.split(": ", 1) for line in open(os.path.join(pre, "lib/pkgconfig/xcsum.pc"))
+                  .read().splitlines() if ": " in line)
+
+    def expand(v):
+        for _ in range(3):
+            for k, x in pc.items():
+                v = v.replace("${" + k + "}", x)
+        return v.split()
+    assert pc["prefix"] == pre
+    src_a = ('#include <stdio.h>\n#include <xcsum.h>\nint main(void) { xcsum_ctx *c = 0;\n'
+             '  int rc = xcsum_ctx_create(-1, &c); if (!rc) xcsum_ctx_destroy(c);\n'
+             '  printf("%d\\n", rc); return 0; }\n')
+    src_b = ('#include <stdio.h>\n#include <xudp_packet.h>\nint main(void) {\n'
+             '  printf("%d\\n", xudp_packet_udp != 0 && xudp_packet_udp_batch != 0); return 0; }\n')
+    d = tempfile.mkdtemp()
+    outs = []
+    for name, src, extra in (("a", src_a, []), ("b", src_b, ["-lxcsum_packet"])):
+        open(os.path.join(d, name + ".c"), "w").write(src)
+        exe = os.path.join(d, name)
+        libs = expand(fields["Libs"])
+        subprocess.run(["gcc", "-std=c11", *expand(fields["Cflags"]), os.path.join(d, name + ".c"),
+                        "-o", exe, *libs[:1], *extra, *libs[1:]], check=True)
+        env = {k: v for k, v in os.environ.items() if k != "LD_LIBRARY_PATH"}
+        outs.append(subprocess.run([exe], capture_output=True, text=True, check=True,
+                                   env=env, timeout=120).stdout.strip())
+    assert outs[0] in ("0", str(-X.ERR_NODEV))
+    assert outs[1] == "1"
