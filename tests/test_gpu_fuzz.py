@@ -158,3 +158,42 @@ def host_fuzz_case(torch_cuda, engine, seed):
                          f"{exp_after[o]} original {umem[o]}")
         raise AssertionError(f"seed {seed}: {len(diff)} in-place bytes differ "
                              f"(zerocopy {zerocopy}, flags {flags:#x}): " + "; ".join(where))
+
+
+@pytest.mark.parametrize("seed", range(48))
+def test_fuzz_iphdr_only(torch_cuda, engine, monkeypatch, seed):
+    """XCSUM_F_IPHDR_ONLY (libxudp's IPv4 call) on random batches -- IPv6
+    and malformed frames mixed in, random phases, layouts and frames per
+    thread -- on the device against the oracle (orc_iphdr_only), and through
+    xcsum_batch_host (gathered, or in place from a registered UMEM) against
+    the device: results and frame bytes.  In place, only iph->check of the
+    IPv4 frames the rules accept may change."""
+    rng = np.random.default_rng(4000 + seed)
+    umem, desc = random_batch(rng)
+    mode = int(rng.choice([X.MODE_V4_LEGACY, X.MODE_V4_RFC, X.MODE_AUTO]))
+    flags = X.F_IPHDR_ONLY | int(rng.choice([0, X.F_INPLACE, X.F_VERIFY, X.F_VERIFY | X.F_INPLACE]))
+    monkeypatch.setenv("XCSUM_IPHDR_FPT", str(rng.choice(["1", "2", "4", "8"])))
+    exp = oracle.batch(umem, desc, mode, flags & ~X.F_INPLACE)
+    got, after = run_device(torch_cuda, engine, umem, desc, mode, flags)
+    bad = np.nonzero(got != exp)[0]
+    assert len(bad) == 0, f"seed {seed}: mode {mode} flags {flags:#x}: frames {bad[:8].tolist()}"
+    changed = set(np.nonzero(after != umem)[0].tolist())
+    fields = set()
+    for a in desc["addr"].astype(np.int64):
+        fields.update((int(a) + 24, int(a) + 25))
+    assert changed <= fields
+    if not (flags & X.F_INPLACE) or (flags & X.F_VERIFY):
+        assert not changed
+    zerocopy = rng.random() < 0.5
+    host = umem.copy()
+    if zerocopy:
+        host = X.as_umem(host)   # libxudp's UMEM mapping
+        engine.register_umem(host)
+    out = np.full(len(desc), 0x5a5a, dtype=np.uint16)
+    try:
+        engine.batch_host(host, desc, out, mode, flags)
+    finally:
+        if zerocopy:
+            engine.unregister_umem(host)
+    assert np.array_equal(out, exp), f"seed {seed}: host path (zerocopy {zerocopy})"
+    assert np.array_equal(host, after), f"seed {seed}: host in-place bytes (zerocopy {zerocopy})"
