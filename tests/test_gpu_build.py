@@ -148,6 +148,26 @@ def test_build_ipv4_inplace_header_kernel(torch_cuda, engine, monkeypatch, slot_
         assert np.array_equal(after[eth:eth + len(exp)], exp), i
 
 
+@pytest.mark.parametrize("n", [1, 2, 63, 64, 65, 257, 1025, 70001, 300001])
+def test_build_ipv4_header_kernel_batch_edges(torch_cuda, engine, monkeypatch, n):
+    """The header-only build kernel's persistent grid (4 lanes per message,
+    the next message prefetched) at batch tails, and at 300,001 messages
+    more than two rounds of a full grid (256 CUs x 8 blocks x 64 messages):
+    slots, descriptors and results equal the payload-summing kernel's
+    (XCSUM_BUILD_HDR=0), in xudp's 4096-byte slots."""
+    rng = np.random.default_rng(n)
+    pays = [rng.integers(0, 256, int(L), dtype=np.uint8)
+            for L in rng.integers(0, 1473, n)]
+    res = {}
+    for hdr_kernel in ("1", "0"):
+        monkeypatch.setenv("XCSUM_BUILD_HDR", hdr_kernel)
+        res[hdr_kernel] = device_build(torch_cuda, engine, route_of(4, ROUTES[4]), pays,
+                                       inplace=True, len_hint=700, FRAME=4096)[:3]
+    for a, b in zip(res["1"], res["0"]):
+        assert np.array_equal(a, b)
+    assert np.array_equal(res["1"][1]["len"], np.array([len(p) + 42 for p in pays]))
+
+
 @pytest.mark.parametrize("inplace", [False, True])   # True: the header-only kernel
 def test_build_rejects_oversized(torch_cuda, engine, inplace):
     pays = [np.zeros(100, np.uint8), np.zeros(FRAME - DATA_OFF + 1, np.uint8),
