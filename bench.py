@@ -223,6 +223,101 @@ def dist_env():
     return world, rank, local
 
 
+def launch_plan(gpus, environ):
+    """What `bench.py --gpus N` does with the environment it was started in:
+    "launch" -- N > 1 and no WORLD_SIZE: this process starts the N rank
+    processes itself (launch_ranks) and only relays their exit code;
+    "run" -- it is one rank (WORLD_SIZE from torch.distributed.run or from
+    launch_ranks, or N = 1 without one).  A WORLD_SIZE that disagrees with
+    --gpus is an error: the line would otherwise report a GPU count nobody
+    asked for.  Returns ("launch"|"run", message or None)."""
+    if gpus < 1:
+        return "error", f"--gpus {gpus}: need at least one GPU"
+    ws = environ.get("WORLD_SIZE")
+    if ws is None:
+        return ("launch", None) if gpus > 1 else ("run", None)
+    try:
+        world = int(ws)
+    except ValueError:
+        return "error", f"WORLD_SIZE={ws!r} is not a number"
+    if world != gpus:
+        return "error", (f"WORLD_SIZE={world} but --gpus {gpus}: run `bench.py --gpus {gpus}` "
+                         f"bare (it starts its own ranks) or under torch.distributed.run with "
+                         f"--nproc-per-node {gpus}")
+    return "run", None
+
+
+def free_port():
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def rank_env(environ, rank, world, port):
+    """Environment of rank `rank` of a launch_ranks job: the variables
+    torch.distributed.run sets (one node, LOCAL_RANK = RANK = the GPU index)."""
+    env = dict(environ)
+    env.update(RANK=str(rank), LOCAL_RANK=str(rank), WORLD_SIZE=str(world),
+               LOCAL_WORLD_SIZE=str(world), GROUP_RANK="0", ROLE_RANK=str(rank),
+               ROLE_WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
+               TORCHELASTIC_RUN_ID="bench")
+    # dmabuf IPC only on this pool (RCCL's peer mappings)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return env
+
+
+def launch_ranks(world, argv, grace_s=30.0, script=None):
+    """Start `world` rank processes of this script (the same arguments, one
+    per GPU, LOCAL_RANK = GPU) and wait for them.  The parent never imports
+    torch nor touches a GPU, and it starts children rather than replacing
+    itself.  Rank 0 writes the JSON line to the inherited stdout; the other
+    ranks' stdout goes to stderr.  When a rank fails, the rest get `grace_s`
+    to finish (they would block in the next barrier) and are then killed; a
+    SIGTERM/SIGINT to the parent is passed on.  Returns the exit code: 0 if
+    every rank exited 0, else the first failing rank's code (or 1)."""
+    import signal
+    import subprocess
+    port = free_port()
+    script = script or os.path.abspath(__file__)
+    procs = []
+    for r in range(world):
+        procs.append(subprocess.Popen([sys.executable, "-u", script, *argv],
+                                      env=rank_env(os.environ, r, world, port),
+                                      stdout=None if r == 0 else sys.stderr.fileno()))
+
+    def forward(sig, _frame):
+        for p in procs:
+            if p.poll() is None:
+                p.send_signal(sig)
+    old = {s: signal.signal(s, forward) for s in (signal.SIGTERM, signal.SIGINT)}
+    rc, failed_at = 0, None
+    try:
+        live = set(range(world))
+        while live:
+            for r in sorted(live):
+                c = procs[r].poll()
+                if c is None:
+                    continue
+                live.discard(r)
+                if c != 0 and rc == 0:
+                    rc = c if c > 0 else 1
+                    failed_at = time.monotonic()
+                    print(f"bench: rank {r} exited with {c}", file=sys.stderr)
+            if live and failed_at is not None and time.monotonic() - failed_at > grace_s:
+                for r in live:
+                    procs[r].kill()
+                    print(f"bench: rank {r} killed after rank failure", file=sys.stderr)
+                for r in live:
+                    procs[r].wait()
+                break
+            time.sleep(0.05)
+    finally:
+        for s, h in old.items():
+            signal.signal(s, h)
+    return rc
+
+
 def rank_slice(cfg, rank, world):
     """(first global frame index, frame count) owned by `rank`.  Config 5 is
     one 8M-frame job split by bytes over the ranks (strong scaling); the others
@@ -662,23 +757,49 @@ def order_ab(torch, dev, eng, bufs, d_desc, count, out_arg, cfg, flags, len_hint
                     f"2^T-frame tiles (0,0 = descriptor order), auto = the library's choice"}
 
 
-def digest_check(cfg, out, count, world, rank, dist, sdev, field="sha256_out"):
+def parse_shard(text):
+    """--shard r/N -> (r, N), or None for ''."""
+    if not text:
+        return None
+    try:
+        r, n = (int(v) for v in text.split("/"))
+    except ValueError:
+        raise SystemExit(f"--shard {text!r}: expected r/N, e.g. 0/8")
+    if not (n >= 1 and 0 <= r < n):
+        raise SystemExit(f"--shard {text!r}: need 0 <= r < N")
+    return r, n
+
+
+def digest_check(cfg, out, count, world, rank, dist, sdev, field="sha256_out", shard=None):
     """SHA-256 of the timed output against the digest the REFERENCE produced
     over the same synthetic frames (tests/golden/digests.json, made by
     tests/golden/make_golden.py with the compiled checksum.h).  Config 5 is
     one job sharded by bytes: every rank's output is gathered to rank 0 and
     the concatenation must equal the single-job digest.  Weak-scaling configs
-    give rank r frames r*n..: rank 0's batch is the digested one."""
+    give rank r frames r*n..: rank 0's batch is the digested one.  `shard`
+    (r, N): one process timing shard r of N alone (--shard) -- its output
+    against the reference's digest of exactly that shard
+    (sha256_out_shards{N}[r])."""
     import hashlib
     path = os.path.join(ROOT, "tests", "golden", "digests.json")
     key = f"config{cfg['id']}"
     if not os.path.exists(path):
         return None
-    want = json.load(open(path)).get(key, {}).get(field)
-    if not want:
-        return None
+    rec = json.load(open(path)).get(key, {})
     import torch
     mine = out[:count].view(torch.uint8) if count else out[:0].view(torch.uint8)
+    if shard is not None and cfg["shard"]:
+        if field != "sha256_out":
+            return None
+        want = (rec.get(f"sha256_out_shards{shard[1]}") or [None] * shard[1])[shard[0]]
+        if not want:
+            return None
+        return {"ok": hashlib.sha256(d2h(torch, mine).tobytes()).hexdigest() == want,
+                "what": f"{key} sha256_out_shards{shard[1]}[{shard[0]}] over this shard's "
+                        f"timed output"}
+    want = rec.get(field)
+    if not want:
+        return None
     if cfg["shard"] and dist.is_initialized():
         cnt = torch.tensor([count], dtype=torch.int64, device=sdev)
         cnts = [torch.zeros_like(cnt) for _ in range(world)]
@@ -737,17 +858,40 @@ def main():
                          "inplace the checks go into the frames and no result array is written, "
                          "as libxudp's TX path does (tx.c:696-726); libxudp's IPv4 call is "
                          "inplace,iphdr_only (iph->check only), its IPv6 call inplace on config 4")
+    ap.add_argument("--shard", default="",
+                    help="r/N: one process times shard r of N of a sharded config (config 5) "
+                         "alone -- one rank's share of the N-GPU job -- with the full roofline "
+                         "and that shard's reference digest")
     args = ap.parse_args()
     flags = parse_flags(args.flags)
+    shard = parse_shard(args.shard)
     # in place: the check fields go into the frames, no result array
     with_out = not (flags & X.F_INPLACE) or bool(flags & X.F_VERIFY)
+
+    # N > 1 without a launcher: start the N ranks here, before torch or any
+    # GPU call (a bare `bench.py --gpus 8` ran one rank)
+    plan, msg = launch_plan(args.gpus, os.environ)
+    if plan == "error":
+        print(f"bench: {msg}", file=sys.stderr)
+        sys.exit(2)
+    if plan == "launch":
+        if shard is not None:
+            print("bench: --shard times one shard in one process; use --gpus 1", file=sys.stderr)
+            sys.exit(2)
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
 
     import torch
     import torch.distributed as dist
 
     world, rank, local = dist_env()
-    if world != args.gpus and rank == 0:
-        print(f"note: WORLD_SIZE={world} but --gpus {args.gpus}", file=sys.stderr)
+    if shard is not None and (world != 1 or not CONFIGS[args.config]["shard"]):
+        print("bench: --shard needs --gpus 1 and a sharded config (5)", file=sys.stderr)
+        sys.exit(2)
+    ndev = torch.cuda.device_count()
+    if not args.same_device and local >= ndev:
+        print(f"bench: rank {rank} wants cuda:{local} but {ndev} GPU(s) are visible "
+              f"(--same-device rehearses N ranks on one GPU)", file=sys.stderr)
+        sys.exit(2)
     dev = torch.device(f"cuda:{0 if args.same_device else local}")
     torch.cuda.set_device(dev)
     use_dist = world > 1 or args.dist_init
@@ -769,7 +913,9 @@ def main():
                      "two_pass": X.INPLACE_TWO_PASS}[args.inplace_schedule])
     stream = torch.cuda.current_stream(dev)
     sptr = stream.cuda_stream
-    desc, d_desc, bufs, out, first, count = build_batch(cfg, rank, world, torch, dev, eng, sptr,
+    # --shard r/N: this process's batch is shard r of the N-way split
+    srank, sworld = shard if shard is not None else (rank, world)
+    desc, d_desc, bufs, out, first, count = build_batch(cfg, srank, sworld, torch, dev, eng, sptr,
                                                         flags)
     alg = alg_bytes_flags(desc, cfg["family"], flags, with_out)
     len_hint = int(desc["len"].mean()) if count else 0
@@ -968,7 +1114,7 @@ def main():
     # IPHDR_ONLY: the reference's xudp_checksum_half over the same frames
     digest = None if flags & X.F_VERIFY else digest_check(
         cfg, out, count, world, rank, dist, sdev,
-        "sha256_iphdr" if flags & X.F_IPHDR_ONLY else "sha256_out")
+        "sha256_iphdr" if flags & X.F_IPHDR_ONLY else "sha256_out", shard)
 
     parity_ok = True
     if rank == 0:
@@ -1063,7 +1209,10 @@ def main():
                                              "auto" if calibrated == (-1, 0) else
                                              f"{calibrated[0]},{calibrated[1]}"),
                        "rotating_buffers": len(bufs),
-                       "alg_bytes_per_step": int(alg_all), "parallelism": f"dp{world}"},
+                       "alg_bytes_per_step": int(alg_all), "parallelism": f"dp{world}",
+                       "shard": (None if shard is None else
+                                 f"{shard[0]}/{shard[1]}: frames {first}..{first + count - 1} "
+                                 f"of the job, one rank's byte-balanced share, timed alone")},
             "pct_hbm_peak": round(100 * achieved / HBM_PEAK_GBS, 2),
             "mpps": round(frames_all * args.steps / elapsed_max / 1e6, 1),
             "kernel_ms": round(kern_ms, 4),

@@ -106,8 +106,53 @@ enum {
 
 typedef struct xcsum_ctx xcsum_ctx;
 
-/* Create a context bound to HIP device `device` (-1: $XCSUM_DEVICE or 0). */
+/* ---- device placement: libxudp's groups over the node's GPUs --------------
+ * libxudp runs group_num groups (include/xudp.h:196-199, xudp_group_get(x,
+ * gid) at :310-311), each a worker thread or a forked process
+ * (test/case/lib.c:196-221), and checksums are per frame, so a group's
+ * batches can go to any GPU with no exchange between GPUs.  The `device`
+ * argument of xcsum_ctx_create picks one:
+ *   >= 0                that device;
+ *   XCSUM_DEVICE_ENV    $XCSUM_DEVICE (read when the context is created), else
+ *                       device 0 -- the behaviour of rounds 1-5;
+ *   XCSUM_DEVICE_AUTO   round robin over the visible devices, in the order
+ *                       this process creates AUTO contexts (8 group threads
+ *                       creating one context each land on 8 GPUs);
+ *   XCSUM_DEVICE_GROUP(gid)  device gid mod the visible count: the same group
+ *                       on the same GPU whatever the thread timing, and the
+ *                       placement for forked workers (each process's AUTO
+ *                       counter starts at 0).
+ * The thread's default context (xudp_packet_udp_batch with ctx NULL and the
+ * libxcsum_packet.so mirrors) is placed by xcsum_thread_init(gid), or, when
+ * the thread never called it, by $XCSUM_DEVICE if set, else AUTO. */
+#define XCSUM_DEVICE_ENV   (-1)
+#define XCSUM_DEVICE_AUTO  (-2)
+#define XCSUM_DEVICE_GROUP(gid) (-1000 - (int)(gid))   /* gid 0 .. 1000000 */
+/* Devices this process sees (>= 1), or -XCSUM_ERR_NODEV. */
+int xcsum_device_count(void);
+/* The device xcsum_ctx_create(device, ...) takes when `ndev` devices are
+ * visible (ndev <= 0: count them).  An AUTO answer takes a turn of the round
+ * robin.  -XCSUM_ERR_NODEV for a device >= ndev or no device,
+ * -XCSUM_ERR_INVAL for an unknown negative value. */
+int xcsum_device_resolve(int device, int ndev);
+
+/* Create a context bound to HIP device `device` (see above; -1 =
+ * XCSUM_DEVICE_ENV: $XCSUM_DEVICE or 0). */
 int xcsum_ctx_create(int device, xcsum_ctx **out);
+/* xcsum_ctx_create(XCSUM_DEVICE_GROUP(gid), out): libxudp group gid's
+ * context, on device gid mod the visible count. */
+int xcsum_ctx_create_for_group(int gid, xcsum_ctx **out);
+/* Create the calling thread's default context now, on group gid's device
+ * (gid < 0: the default placement above), replacing one made earlier on
+ * another device.  A libxudp worker calls it once when it starts (after any
+ * fork): a missing or unusable device is then an error code at start-up
+ * rather than a failure of the first xudp_packet_udp() call on the send
+ * path, which cannot return one (libxcsum_packet.so aborts there).  Returns
+ * 0 or -XCSUM_ERR_*. */
+int xcsum_thread_init(int gid);
+/* The calling thread's default context (created on first use; NULL if it
+ * cannot be created). */
+xcsum_ctx *xcsum_thread_ctx(void);
 void xcsum_ctx_destroy(xcsum_ctx *ctx);
 int xcsum_ctx_device(const xcsum_ctx *ctx);
 /* Number of malformed frames seen by this context since the last call
@@ -172,6 +217,46 @@ int xcsum_ctx_calibrate_order(xcsum_ctx *ctx, uint8_t *d_umem, const struct xcsu
 #define XCSUM_INPLACE_FUSED    1
 #define XCSUM_INPLACE_TWO_PASS 2
 int xcsum_ctx_set_inplace(xcsum_ctx *ctx, int schedule);
+
+/* Tuning knobs of one context (sweeps, A/B and the parity tests that run
+ * every kernel variant): which kernel or geometry a launch takes, never its
+ * results.  The library reads no tuning from the environment on any batch
+ * path; these setters are the only way in (the `make variant` A/B build also
+ * takes them from XCSUM_<KNOB> at context creation).  Values (a, b, c, d):
+ *   IPHDR_FPT        a = frames per thread of the IPv4 header kernel, 1|2|4|8
+ *                    (default 4);
+ *   BUILD_HDR        a = 0: IPv4 in-place builds take the payload-summing
+ *                    build kernel (superseded in round 5; A/B and tests),
+ *                    1: the header kernel (default);
+ *   BUILD_GEOMETRY   a, b = G, K of the build kernel (a = 0: automatic);
+ *   RX_GEOMETRY      a, b, c, d = G, K, U, blocks per CU of the receive
+ *                    kernel (a = 0: automatic);
+ *   RX_ORDER         a = -1 automatic (sparse batches: 32 regions of 64-frame
+ *                    tiles), 0 descriptor order, else 2^a regions of 2^b
+ *                    frames;
+ *   GATHER_RATIO     a = host path: frames spread over more than a x their
+ *                    bytes are gathered frame by frame (default 2);
+ *   INPLACE_BLOCK    a = 0|32|64: store width of the two-pass scatter;
+ *   INPLACE_TL       a = 0: in place without IPHDR at MTU takes the plain
+ *                    kernel instead of the temporal-first-chunks one;
+ *   RESIDENT_INLINE  a = 0: resident requests carry their descriptors only
+ *                    in the array (A/B of the inline lines);
+ *   RESIDENT_LIMIT_CUT a = bytes: resident requests carry a limit this much
+ *                    short (test hook for the workgroups' descriptor check).
+ * -XCSUM_ERR_INVAL for an unknown knob or a value not compiled in. */
+enum xcsum_tuning {
+	XCSUM_TUNE_IPHDR_FPT = 1,
+	XCSUM_TUNE_BUILD_HDR = 2,
+	XCSUM_TUNE_BUILD_GEOMETRY = 3,
+	XCSUM_TUNE_RX_GEOMETRY = 4,
+	XCSUM_TUNE_RX_ORDER = 5,
+	XCSUM_TUNE_GATHER_RATIO = 6,
+	XCSUM_TUNE_INPLACE_BLOCK = 7,
+	XCSUM_TUNE_INPLACE_TL = 8,
+	XCSUM_TUNE_RESIDENT_INLINE = 9,
+	XCSUM_TUNE_RESIDENT_LIMIT_CUT = 10,
+};
+int xcsum_ctx_set_tuning(xcsum_ctx *ctx, int knob, int a, int b, int c, int d);
 
 /* ---- device-resident batch ------------------------------------------------
  * Replaces the per-frame checksum work of the xudp_frame_send loop
@@ -347,12 +432,23 @@ int xcsum_umem_mapped(xcsum_ctx *ctx, const void *base);
  * Results are the same bytes.  The workgroups leave after `idle_us` (0:
  * 20000) without a batch and come back with the next one.  0 workgroups: off
  * (the default; env XCSUM_RESIDENT="W[,idle_us[,max_frames]]" sets it at
- * context creation).  While they are resident, a device-wide
+ * context creation, e.g. for the packet.c mirrors' default contexts).  While they are resident, a device-wide
  * synchronisation by others (hipDeviceSynchronize, torch.cuda.synchronize)
  * waits until they leave, i.e. up to idle_us after this context's last
  * batch; the library's own device-wide waits (xcsum_ctx_take_errors,
- * xcsum_unregister_umem, xcsum_ctx_destroy) stop them first. */
+ * xcsum_unregister_umem, xcsum_ctx_destroy) stop them first.
+ *
+ * Cost to other GPU work: a live resident grid holds its hardware queue, and
+ * streams beyond GPU_MAX_HW_QUEUES (4) share queues, so a kernel of another
+ * stream on the same GPU may wait behind it.  Every workgroup therefore
+ * leaves after `life_us` alive even while busy (default 2000; the next batch
+ * relaunches them, ~10 us once per life): that wait is at most life_us plus
+ * one batch -- measured 1.9 ms at the default, 200 ms at life_us = 200000
+ * (tests/test_gpu_resident.py::test_resident_queue_sharing). */
 int xcsum_ctx_set_resident(xcsum_ctx *ctx, int workgroups, uint32_t idle_us);
+/* The resident workgroups' life bound in microseconds (0: the default 2000);
+ * running workgroups leave and the next batch launches them with it. */
+int xcsum_ctx_set_resident_life(xcsum_ctx *ctx, uint32_t life_us);
 
 /* Number of the context's host-path slots with copies or kernels still in
  * flight.  Always 0 after xcsum_batch_host / xcsum_rx_host return, on error

@@ -76,7 +76,9 @@ void xudp_packet_build_headers(struct packet_info *info);
  * publishes the frame right after (tx.c:649-671, :500).  If the device path
  * fails these print the error and abort() the process -- a frame without its
  * checksum is never published.  Use xudp_packet_udp_batch() for an error
- * code instead. */
+ * code instead, and call xcsum_thread_init(gid) when a worker starts: a
+ * missing device is then an error code at start-up, not an abort on the
+ * first send. */
 
 /* Replaces xudp/packet.c:156-194.  Builds eth + IPv4/IPv6 + UDP headers in
  * front of info->data and fills info->packet / info->len like the reference;

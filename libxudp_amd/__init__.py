@@ -111,6 +111,25 @@ def variant_geometries():
 # xcsum_ctx_set_inplace schedules
 INPLACE_AUTO, INPLACE_FUSED, INPLACE_TWO_PASS = 0, 1, 2
 
+# xcsum_ctx_set_tuning knobs (enum xcsum_tuning)
+TUNE_IPHDR_FPT, TUNE_BUILD_HDR, TUNE_BUILD_GEOMETRY, TUNE_RX_GEOMETRY, TUNE_RX_ORDER = 1, 2, 3, 4, 5
+TUNE_GATHER_RATIO, TUNE_INPLACE_BLOCK, TUNE_INPLACE_TL = 6, 7, 8
+TUNE_RESIDENT_INLINE, TUNE_RESIDENT_LIMIT_CUT = 9, 10
+
+# device placement (include/xcsum.h)
+DEVICE_ENV, DEVICE_AUTO = -1, -2
+
+
+def DEVICE_GROUP(gid):
+    """xcsum_ctx_create device argument for libxudp group gid"""
+    return -1000 - int(gid)
+
+
+def device_resolve(device, ndev=0):
+    """The device xcsum_ctx_create(device) takes with ndev visible devices
+    (ndev <= 0: count them); negative = -XCSUM_ERR_*"""
+    return lib().xcsum_device_resolve(int(device), int(ndev))
+
 F_BUILD_INPLACE = 0x20
 F_SRC_ALIGNED = 0x40
 
@@ -156,6 +175,14 @@ _SIGS = {
                                                  ctypes.POINTER(ctypes.c_int)]),
     "xcsum_ctx_set_resident": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_uint32]),
     "xcsum_ctx_set_inplace": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
+    "xcsum_ctx_set_tuning": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
+                                            ctypes.c_int, ctypes.c_int, ctypes.c_int]),
+    "xcsum_ctx_set_resident_life": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint32]),
+    "xcsum_device_count": (ctypes.c_int, []),
+    "xcsum_device_resolve": (ctypes.c_int, [ctypes.c_int, ctypes.c_int]),
+    "xcsum_ctx_create_for_group": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]),
+    "xcsum_thread_init": (ctypes.c_int, [ctypes.c_int]),
+    "xcsum_thread_ctx": (ctypes.c_void_p, []),
     "xcsum_batch_device": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                           ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint32,
                                           ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p]),
@@ -411,6 +438,15 @@ class Engine:
         """Resident workgroups for small host batches (0: off), see xcsum.h."""
         _check(lib().xcsum_ctx_set_resident(self._ctx, workgroups, idle_us),
                "xcsum_ctx_set_resident")
+
+    def set_resident_life(self, life_us=0):
+        """The resident workgroups' life bound (0: default 2000 us)."""
+        _check(lib().xcsum_ctx_set_resident_life(self._ctx, life_us),
+               "xcsum_ctx_set_resident_life")
+
+    def set_tuning(self, knob, a=0, b=0, c=0, d=0):
+        """xcsum_ctx_set_tuning (TUNE_*): kernel variant / geometry, never results."""
+        _check(lib().xcsum_ctx_set_tuning(self._ctx, knob, a, b, c, d), "xcsum_ctx_set_tuning")
 
     def take_errors(self):
         c = ctypes.c_uint64(0)

@@ -10,6 +10,7 @@
 #include <stdlib.h>
 #include <string.h>
 #include <algorithm>
+#include <atomic>
 #include <new>
 #include <chrono>
 #include <mutex>
@@ -135,20 +136,10 @@ static void env_resident(xcsum_ctx *c)
 	c->res_live = false;
 	c->res_seq = 0;
 	c->res_gen = 0;
-	c->res_trace = getenv("XCSUM_RESIDENT_TRACE") != nullptr;
-	/* diagnostic: the workgroups' life bound (RES_LIFE_US), to measure what
-	 * a long-lived grid does to streams sharing its hardware queue
-	 * (tests/test_gpu_resident.py::test_resident_queue_sharing) */
-	const char *life = getenv("XCSUM_RESIDENT_LIFE_US");
-	c->res_life_us = life && atoi(life) > 0 ? (uint32_t)atoi(life) : RES_LIFE_US;
-	/* test hook: requests carry a limit this many bytes short, so the
-	 * workgroups' own descriptor check refuses the frames past it
-	 * (tests/test_gpu_resident.py::test_resident_descriptor_check) */
-	const char *cut = getenv("XCSUM_RESIDENT_LIMIT_CUT");
-	c->res_limit_cut = cut ? strtoull(cut, nullptr, 10) : 0;
-	/* diagnostic: descriptors only in the array (A/B of the inline lines) */
-	const char *inl = getenv("XCSUM_RESIDENT_INLINE");
-	c->res_inline = !(inl && strcmp(inl, "0") == 0);
+	c->res_trace = getenv("XCSUM_RESIDENT_TRACE") != nullptr;   /* diagnostic */
+	c->res_life_us = RES_LIFE_US;       /* xcsum_ctx_set_resident_life */
+	c->res_limit_cut = 0;               /* XCSUM_TUNE_RESIDENT_LIMIT_CUT */
+	c->res_inline = true;               /* XCSUM_TUNE_RESIDENT_INLINE */
 	c->res_calls = 0;
 	c->res_spin_us = c->res_call_us = 0;
 	const char *e = getenv("XCSUM_RESIDENT");
@@ -160,6 +151,120 @@ static void env_resident(xcsum_ctx *c)
 		c->res_max_frames = maxf < RB_DESC_CAP ? maxf : RB_DESC_CAP;
 	}
 }
+
+static void tuning_defaults(xcsum_ctx *c)
+{
+	Tuning &t = c->tune;
+	t.iphdr_fpt = 4;
+	t.build_hdr = true;
+	t.build_G = t.build_K = 0;
+	t.rx_G = t.rx_K = t.rx_U = t.rx_B = 0;
+	t.rx_rlog = -1;
+	t.rx_tlog = 0;
+	t.gather_ratio = 2;
+	c->inplace_block = 0;
+	c->inplace_tl = 1;
+}
+
+extern "C" int xcsum_ctx_set_tuning(xcsum_ctx *c, int knob, int a, int b, int cc, int d)
+{
+	if (!c)
+		return -XCSUM_ERR_INVAL;
+	Tuning &t = c->tune;
+	switch (knob) {
+	case XCSUM_TUNE_IPHDR_FPT:
+		if (a != 1 && a != 2 && a != 4 && a != 8)
+			return -XCSUM_ERR_INVAL;
+		t.iphdr_fpt = a;
+		return 0;
+	case XCSUM_TUNE_BUILD_HDR:
+		t.build_hdr = a != 0;
+		return 0;
+	case XCSUM_TUNE_BUILD_GEOMETRY:
+		if (a && !build_geometry_supported(a, b))
+			return -XCSUM_ERR_INVAL;
+		t.build_G = a;
+		t.build_K = a ? b : 0;
+		return 0;
+	case XCSUM_TUNE_RX_GEOMETRY:
+		if (a && (!rx_geometry_supported(a, b, cc) || d < 0 || d > 32))
+			return -XCSUM_ERR_INVAL;
+		t.rx_G = a;
+		t.rx_K = a ? b : 0;
+		t.rx_U = a ? cc : 0;
+		t.rx_B = a ? d : 0;
+		return 0;
+	case XCSUM_TUNE_RX_ORDER:
+		if (a < -1 || a > 12 || (a > 0 && (b < 0 || b > 16)))
+			return -XCSUM_ERR_INVAL;
+		t.rx_rlog = a;
+		t.rx_tlog = a > 0 ? b : 0;
+		return 0;
+	case XCSUM_TUNE_GATHER_RATIO:
+		if (a < 0)
+			return -XCSUM_ERR_INVAL;
+		t.gather_ratio = a ? (uint32_t)a : 2u;
+		return 0;
+	case XCSUM_TUNE_INPLACE_BLOCK:
+		if (a != 0 && a != 32 && a != 64)
+			return -XCSUM_ERR_INVAL;
+		c->inplace_block = (uint32_t)a;
+		return 0;
+	case XCSUM_TUNE_INPLACE_TL:
+		c->inplace_tl = a != 0;
+		return 0;
+	case XCSUM_TUNE_RESIDENT_INLINE:
+		c->res_inline = a != 0;
+		return 0;
+	case XCSUM_TUNE_RESIDENT_LIMIT_CUT:
+		if (a < 0)
+			return -XCSUM_ERR_INVAL;
+		c->res_limit_cut = (uint64_t)a;
+		return 0;
+	default:
+		return -XCSUM_ERR_INVAL;
+	}
+}
+
+#ifdef XCSUM_ENV_TUNING
+/* `make variant` only (A/B sweeps by tools/ scripts): the tuning knobs from
+ * XCSUM_<KNOB> at context creation.  libxcsum.so itself takes them through
+ * xcsum_ctx_set_tuning alone. */
+static void read_env_tuning(xcsum_ctx *c)
+{
+	int a = 0, b = 0, cc = 0, d = 0;
+	const char *e;
+	if ((e = getenv("XCSUM_IPHDR_FPT")))
+		(void)xcsum_ctx_set_tuning(c, XCSUM_TUNE_IPHDR_FPT, atoi(e), 0, 0, 0);
+	if ((e = getenv("XCSUM_BUILD_HDR")))
+		(void)xcsum_ctx_set_tuning(c, XCSUM_TUNE_BUILD_HDR, atoi(e), 0, 0, 0);
+	if ((e = getenv("XCSUM_BUILD_GEOMETRY")) && sscanf(e, "%d,%d", &a, &b) == 2)
+		(void)xcsum_ctx_set_tuning(c, XCSUM_TUNE_BUILD_GEOMETRY, a, b, 0, 0);
+	a = b = 0;
+	if ((e = getenv("XCSUM_RX_GEOMETRY"))) {
+		cc = 1;
+		d = 0;
+		if (sscanf(e, "%d,%d,%d,%d", &a, &b, &cc, &d) >= 2)
+			(void)xcsum_ctx_set_tuning(c, XCSUM_TUNE_RX_GEOMETRY, a, b, cc, d);
+	}
+	a = b = 0;
+	if ((e = getenv("XCSUM_RX_ORDER"))) {
+		b = 6;
+		if (sscanf(e, "%d,%d", &a, &b) >= 1)
+			(void)xcsum_ctx_set_tuning(c, XCSUM_TUNE_RX_ORDER, a, b, 0, 0);
+	}
+	if ((e = getenv("XCSUM_GATHER_RATIO")))
+		(void)xcsum_ctx_set_tuning(c, XCSUM_TUNE_GATHER_RATIO, atoi(e), 0, 0, 0);
+	if ((e = getenv("XCSUM_INPLACE_BLOCK")))
+		(void)xcsum_ctx_set_tuning(c, XCSUM_TUNE_INPLACE_BLOCK, atoi(e), 0, 0, 0);
+	if ((e = getenv("XCSUM_INPLACE_TL")))
+		(void)xcsum_ctx_set_tuning(c, XCSUM_TUNE_INPLACE_TL, atoi(e), 0, 0, 0);
+	if ((e = getenv("XCSUM_RESIDENT_INLINE")))
+		(void)xcsum_ctx_set_tuning(c, XCSUM_TUNE_RESIDENT_INLINE, atoi(e), 0, 0, 0);
+	if ((e = getenv("XCSUM_RESIDENT_LIFE_US")) && atoi(e) > 0)
+		c->res_life_us = (uint32_t)atoi(e);
+}
+#endif
 
 /* ---- resident server (xcsum_resident.hip) ----------------------------------
  * W workgroups poll a doorbell in pinned host memory; a small host batch is a
@@ -373,6 +478,17 @@ extern "C" int xcsum_ctx_set_resident(xcsum_ctx *c, int workgroups, uint32_t idl
 	return rc;
 }
 
+extern "C" int xcsum_ctx_set_resident_life(xcsum_ctx *c, uint32_t life_us)
+{
+	if (!c)
+		return -XCSUM_ERR_INVAL;
+	HIPCHK(hipSetDevice(c->device));
+	/* the running workgroups leave; the next batch launches them with it */
+	const int rc = resident_stop(c);
+	c->res_life_us = life_us ? life_us : RES_LIFE_US;
+	return rc;
+}
+
 /* One request: the batch `a` describes (device addresses of the frames,
  * descriptors and result slots) served by the resident workgroups.  Returns
  * when every workgroup has answered.  A workgroup that left at its idle
@@ -544,20 +660,52 @@ static int resident_call(xcsum_ctx *c, const CsumArgs &a, uint64_t limit)
 	}
 }
 
-extern "C" int xcsum_ctx_create(int device, xcsum_ctx **out)
+/* ---- device placement (include/xcsum.h) ---------------------------------- */
+
+static std::atomic<unsigned> g_auto_turn{0};   /* XCSUM_DEVICE_AUTO round robin */
+
+extern "C" int xcsum_device_count(void)
 {
 	int count = 0;
+	if (hipGetDeviceCount(&count) != hipSuccess || count <= 0)
+		return -XCSUM_ERR_NODEV;
+	return count;
+}
+
+extern "C" int xcsum_device_resolve(int device, int ndev)
+{
+	if (ndev <= 0) {
+		ndev = xcsum_device_count();
+		if (ndev < 0)
+			return ndev;
+	}
+	if (device == XCSUM_DEVICE_ENV) {
+		/* read when a context is created, never on a batch path */
+		const char *e = getenv("XCSUM_DEVICE");
+		device = e ? atoi(e) : 0;
+		if (device < 0)
+			return -XCSUM_ERR_NODEV;
+	} else if (device == XCSUM_DEVICE_AUTO) {
+		device = (int)(g_auto_turn.fetch_add(1u, std::memory_order_relaxed) % (unsigned)ndev);
+	} else if (device <= XCSUM_DEVICE_GROUP(0) && device >= XCSUM_DEVICE_GROUP(1000000)) {
+		device = (XCSUM_DEVICE_GROUP(0) - device) % ndev;
+	} else if (device < 0) {
+		return -XCSUM_ERR_INVAL;
+	}
+	return device < ndev ? device : -XCSUM_ERR_NODEV;
+}
+
+extern "C" int xcsum_ctx_create(int device, xcsum_ctx **out)
+{
 	if (!out)
 		return -XCSUM_ERR_INVAL;
 	*out = nullptr;
-	if (device < 0) {
-		const char *e = getenv("XCSUM_DEVICE");
-		device = e ? atoi(e) : 0;
-	}
-	if (hipGetDeviceCount(&count) != hipSuccess || count <= 0)
-		return -XCSUM_ERR_NODEV;
-	if (device >= count)
-		return -XCSUM_ERR_NODEV;
+	const int count = xcsum_device_count();
+	if (count < 0)
+		return count;
+	device = xcsum_device_resolve(device, count);
+	if (device < 0)
+		return device;
 	HIPCHK(hipSetDevice(device));
 	xcsum_ctx *c = new (std::nothrow) xcsum_ctx();
 	if (!c)
@@ -605,17 +753,12 @@ extern "C" int xcsum_ctx_create(int device, xcsum_ctx **out)
 		c->inplace_sched = strcmp(e, "fused") == 0      ? XCSUM_INPLACE_FUSED
 				   : strcmp(e, "two_pass") == 0 ? XCSUM_INPLACE_TWO_PASS
 								: XCSUM_INPLACE_AUTO;
-	/* XCSUM_INPLACE_BLOCK=0|32|64: the second pass's store width (A/B);
+	/* XCSUM_TUNE_INPLACE_BLOCK 0|32|64: the second pass's store width (A/B);
 	 * 2-byte stores measured fastest in every case (config 2 0.348 vs
 	 * 0.364 / 0.353 ms for 32 / 64, config 4 0.332 vs 0.342 / 0.345, xudp's
 	 * slots likewise; profiles/r04/inplace/r04wxy_two_pass_widths.txt): the
 	 * whole-block variants load the block first */
-	c->inplace_block = 0;
-	if (const char *e = getenv("XCSUM_INPLACE_BLOCK"))
-		c->inplace_block = (uint32_t)atoi(e) == 64 ? 64u : (uint32_t)atoi(e) == 32 ? 32u : 0u;
-	c->inplace_tl = 1;
-	if (const char *e = getenv("XCSUM_INPLACE_TL"))
-		c->inplace_tl = atoi(e) != 0;
+	tuning_defaults(c);
 	c->d_inplace = nullptr;
 	c->inplace_cap = 0;
 	c->inplace_done = nullptr;
@@ -625,6 +768,10 @@ extern "C" int xcsum_ctx_create(int device, xcsum_ctx **out)
 	c->blocks_per_cu = 0;
 	env_order(c);
 	env_resident(c);
+#ifdef XCSUM_ENV_TUNING
+	read_env_tuning(c);
+#endif
+	c->stage_pool = new (std::nothrow) StagePool();   /* threads start on first use */
 	*out = c;
 	return 0;
 }
@@ -661,10 +808,19 @@ static void free_staging(xcsum_ctx *c)
 	c->desc_cap = 0;
 }
 
+extern "C" int xcsum_ctx_create_for_group(int gid, xcsum_ctx **out)
+{
+	if (gid < 0 || gid > 1000000)
+		return -XCSUM_ERR_INVAL;
+	return xcsum_ctx_create(XCSUM_DEVICE_GROUP(gid), out);
+}
+
 extern "C" void xcsum_ctx_destroy(xcsum_ctx *c)
 {
 	if (!c)
 		return;
+	delete c->stage_pool;   /* joins its copy threads */
+	c->stage_pool = nullptr;
 	(void)hipSetDevice(c->device);
 	if (c->res_trace && c->res_calls)
 		fprintf(stderr, "xcsum resident: %llu calls, %.2f us per call, %.2f us of it "
@@ -911,7 +1067,7 @@ extern "C" int xcsum_batch_device(xcsum_ctx *c, uint8_t *d_umem, const struct xc
 		a.ord = c->order_rlog >= 0 ? order_regions(n, c->order_rlog, c->order_tlog)
 					   : order_identity(n);
 		a.dense = a.ord;
-		HIPCHK(launch_iphdr(a, (hipStream_t)stream));
+		HIPCHK(launch_iphdr(a, c->tune.iphdr_fpt, (hipStream_t)stream));
 		return 0;
 	}
 	a.flags = flags & (XCSUM_F_INPLACE | XCSUM_F_IPHDR | XCSUM_F_V4_RFC | XCSUM_F_VERIFY);
@@ -1096,7 +1252,7 @@ extern "C" int xcsum_rx_device(xcsum_ctx *c, const uint8_t *d_umem, const struct
 	a.count = d_count;
 	a.part = c->d_rx_part;
 	note_stream(c, stream);
-	HIPCHK(launch_rx(a, len_hint, c->cus, (hipStream_t)stream));
+	HIPCHK(launch_rx(a, len_hint, c->cus, c->tune, (hipStream_t)stream));
 	return 0;
 }
 
@@ -1176,7 +1332,7 @@ extern "C" int xcsum_build_device(xcsum_ctx *c, const struct xcsum_route *route,
 		a.ord = frame_size >= 2u * typ ? order_regions(n, 5, 4) : order_identity(n);
 	}
 	note_stream(c, stream);
-	HIPCHK(launch_build(a, len_hint, c->cus, (hipStream_t)stream));
+	HIPCHK(launch_build(a, len_hint, c->cus, c->tune, (hipStream_t)stream));
 	return 0;
 }
 
@@ -1492,21 +1648,12 @@ static int ensure_gather(xcsum_ctx *c)
  * (profiles/r05/host/r05v_*): 256K MTU frames gathered instead of
  * range-copied, TX 20.3 -> 14.3 ms, in place 24.2 -> 12.2, receive 23.2 ->
  * 11.4; 64-byte frames TX 4.7 -> 3.8, in place 9.5 -> 4.9, receive 5.8 ->
- * 3.9. */
-static uint64_t gather_ratio()
-{
-	/* XCSUM_GATHER_RATIO (A/B only): the 2 above.  Read per call; a
-	 * function-local static here was reported as a data race by the
-	 * ThreadSanitizer build (tests/c/tsan, two threads' first calls) */
-	const char *e = getenv("XCSUM_GATHER_RATIO");
-	const int v = e ? atoi(e) : 0;
-	return (uint64_t)(v > 0 ? v : 2);
-}
-
+ * 3.9; the ratio is the context's Tuning::gather_ratio (2; A/B through
+ * XCSUM_TUNE_GATHER_RATIO). */
 static bool gather_pays(const xcsum_ctx *c, const uint8_t *h_umem, uint64_t lo, uint64_t hi,
 			uint64_t frame_bytes)
 {
-	return hi - lo > gather_ratio() * frame_bytes + 4096 &&
+	return hi - lo > (uint64_t)c->tune.gather_ratio * frame_bytes + 4096 &&
 	       !find_region(c, h_umem + lo, h_umem + hi);
 }
 
@@ -1547,7 +1694,7 @@ static const void *host_dma_src(xcsum_ctx *c, int slot, const uint8_t *p, uint64
 {
 	if (find_region(c, p, p + n))
 		return p;
-	stage_copy(c->h_stage[slot], p, n);
+	stage_copy(c->stage_pool, c->h_stage[slot], p, n);
 	return c->h_stage[slot];
 }
 
@@ -1581,7 +1728,7 @@ struct Pending {
 /* results of one finished chunk -> caller arrays / host frames.  The
  * in-place stores touch one line per frame: from 16384 frames up they are
  * split over up to STAGE_THREADS threads, as the gathers. */
-static void retire(const Pending &pd, const uint16_t *h_res, uint8_t *h_umem,
+static void retire(StagePool *pool, const Pending &pd, const uint16_t *h_res, uint8_t *h_umem,
 		   const struct xcsum_desc *h_desc, uint16_t *h_out, uint16_t *h_out_ip,
 		   uint32_t mode, uint32_t flags)
 {
@@ -1621,23 +1768,12 @@ static void retire(const Pending &pd, const uint16_t *h_res, uint8_t *h_umem,
 		store(0, pd.count);
 		return;
 	}
-	std::thread th[STAGE_THREADS];
-	int started = 0;
 	const uint32_t part = (pd.count + nt - 1) / nt;
-	for (int t = 1; t < nt; t++) {
+	stage_run(pool, nt, [&](int t) {
 		const uint32_t i0 = part * t < pd.count ? part * t : pd.count;
 		const uint32_t i1 = part * (t + 1) < pd.count ? part * (t + 1) : pd.count;
-		try {
-			th[t] = std::thread(store, i0, i1);
-			started = t;
-		} catch (...) {
-			store(i0, i1);   /* no thread: store here */
-		}
-	}
-	store(0, part < pd.count ? part : pd.count);
-	for (int t = 1; t <= started; t++)
-		if (th[t].joinable())
-			th[t].join();
+		store(i0, i1);
+	});
 }
 
 /* Wait for everything the host path queued on the context's streams.  Every
@@ -1745,7 +1881,7 @@ static int batch_host_resident(xcsum_ctx *c, uint8_t *h_umem, const struct xcsum
 	Pending pd;
 	pd.first = 0;
 	pd.count = n;
-	retire(pd, c->h_out[0], h_umem, h_desc, h_out, h_out_ip, mode, flags);
+	retire(c->stage_pool, pd, c->h_out[0], h_umem, h_desc, h_out, h_out_ip, mode, flags);
 	if (c->res_trace) {
 		c->res_calls++;
 		c->res_call_us += std::chrono::duration<double, std::micro>(
@@ -1769,6 +1905,11 @@ static int batch_host_run(xcsum_ctx *c, uint8_t *h_umem, const struct xcsum_desc
 	 * place over PCIe from a mapped UMEM */
 	const bool hdr_only = (flags & XCSUM_F_IPHDR_ONLY) != 0;
 	if (hdr_only && mode == XCSUM_MODE_V6)
+		return -XCSUM_ERR_INVAL;
+	/* the header kernel's one result per frame goes to h_out (it is
+	 * iph->check): a second array would only get stale slot contents
+	 *  */
+	if (hdr_only && h_out_ip)
 		return -XCSUM_ERR_INVAL;
 	if (hdr_only)
 		flags &= XCSUM_F_IPHDR_ONLY | XCSUM_F_INPLACE | XCSUM_F_VERIFY | XCSUM_F_ZEROCOPY;
@@ -1846,10 +1987,12 @@ static int batch_host_run(xcsum_ctx *c, uint8_t *h_umem, const struct xcsum_desc
 		/* grow a chunk: <= desc_cap frames, UMEM range (or gathered bytes)
 		 * <= frame_cap */
 		uint64_t lo = h_desc[i].addr, hi = h_desc[i].addr + h_desc[i].len;
-		if (!zc && hi - lo > c->frame_cap - 16)
+		uint64_t gpos = stage_off(0, lo) + glen(h_desc[i]);   /* gathered bytes so far */
+		/* the first frame must fit a stage: gathered, only its glen() bytes
+		 * are staged (42 of a header-only frame), else its range */
+		if (!zc && (gather ? gpos > c->frame_cap : hi - lo > c->frame_cap - 16))
 			return -XCSUM_ERR_INVAL;
 		uint32_t cnt = 1;
-		uint64_t gpos = stage_off(0, lo) + glen(h_desc[i]);   /* gathered bytes so far */
 		while (gather && i + cnt < n && cnt < c->desc_cap) {
 			const struct xcsum_desc &d = h_desc[i + cnt];
 			const uint64_t e = stage_off(gpos, d.addr) + glen(d);
@@ -1870,7 +2013,7 @@ static int batch_host_run(xcsum_ctx *c, uint8_t *h_umem, const struct xcsum_desc
 		}
 		if (pend[slot].busy) {
 			HIPCHK(wait_slot(c->done[slot]));
-			retire(pend[slot], c->h_out[slot], h_umem, h_desc, h_out, h_out_ip, mode, rflags);
+			retire(c->stage_pool, pend[slot], c->h_out[slot], h_umem, h_desc, h_out, h_out_ip, mode, rflags);
 			pend[slot].busy = false;
 		}
 		hipStream_t st = c->streams[slot];
@@ -1896,7 +2039,7 @@ static int batch_host_run(xcsum_ctx *c, uint8_t *h_umem, const struct xcsum_desc
 		} else if (gather) {
 			/* each frame copied on its own into the pinned stage, then
 			 * one DMA of the packed bytes and one of their descriptors */
-			const uint64_t pos = gather_frames(c->h_stage[slot], h_umem, h_desc + i,
+			const uint64_t pos = gather_frames(c->stage_pool, c->h_stage[slot], h_umem, h_desc + i,
 							   c->h_dstage[slot], cnt,
 							   hdr_only ? 42u : UINT32_MAX);
 			a.bias = 0;
@@ -1934,7 +2077,7 @@ static int batch_host_run(xcsum_ctx *c, uint8_t *h_umem, const struct xcsum_desc
 					      cnt * sizeof(struct xcsum_desc), hipMemcpyHostToDevice, st));
 		uint32_t avg = (uint32_t)((gather ? gpos : hi - lo) / cnt);
 		if (hdr_only)
-			HIPCHK(launch_iphdr(a, st));
+			HIPCHK(launch_iphdr(a, c->tune.iphdr_fpt, st));
 		else
 			HIPCHK(launch_csum(a, geometry_for(c, avg, a.flags), c->cus, st));
 		if (!direct)
@@ -1952,7 +2095,7 @@ static int batch_host_run(xcsum_ctx *c, uint8_t *h_umem, const struct xcsum_desc
 		int s = (slot + k) % Ctx::NSLOT;
 		if (pend[s].busy) {
 			HIPCHK(wait_slot(c->done[s]));
-			retire(pend[s], c->h_out[s], h_umem, h_desc, h_out, h_out_ip, mode, rflags);
+			retire(c->stage_pool, pend[s], c->h_out[s], h_umem, h_desc, h_out, h_out_ip, mode, rflags);
 			pend[s].busy = false;
 		}
 	}
@@ -2126,7 +2269,7 @@ static int rx_host_run(xcsum_ctx *c, const uint8_t *h_umem, const struct xcsum_d
 		if (zc) {
 			a.umem = zc->dev + (h_umem - zc->host);
 		} else if (gather) {
-			const uint64_t pos = gather_frames(c->h_stage[slot], h_umem, h_desc + i,
+			const uint64_t pos = gather_frames(c->stage_pool, c->h_stage[slot], h_umem, h_desc + i,
 							   c->h_dstage[slot], cnt, UINT32_MAX);
 			if (DIRECT_ON && pos <= DIRECT_MAX) {
 				direct = true;
@@ -2155,7 +2298,7 @@ static int rx_host_run(xcsum_ctx *c, const uint8_t *h_umem, const struct xcsum_d
 		a.flags = flags & (XCSUM_F_VERIFY | XCSUM_F_IPHDR);
 		a.count = nullptr;
 		a.part = c->d_rx_part;
-		HIPCHK(launch_rx(a, (uint32_t)((gather ? gpos : hi - lo) / cnt), c->cus, st));
+		HIPCHK(launch_rx(a, (uint32_t)((gather ? gpos : hi - lo) / cnt), c->cus, c->tune, st));
 		if (!direct)
 			HIPCHK(hipMemcpyAsync(c->h_rx_msgs[slot], c->d_rx_msgs[slot],
 					      (size_t)cnt * sizeof(struct xcsum_rx_msg),

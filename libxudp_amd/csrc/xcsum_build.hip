@@ -474,14 +474,6 @@ __global__ void __launch_bounds__(256) build_hdr_kernel(BuildArgs a)
 	}
 }
 
-/* XCSUM_BUILD_HDR=0 (A/B and tests only, read per launch): IPv4 in place
- * takes the payload-summing build kernel, as before round 5 */
-static bool build_hdr_enabled()
-{
-	const char *e = getenv("XCSUM_BUILD_HDR");
-	return !(e && atoi(e) == 0);
-}
-
 static hipError_t launch_build_hdr(const BuildArgs &a, int cus, hipStream_t s)
 {
 	static std::atomic<int> occ_cache[OCC_MAX_DEVICES];
@@ -529,18 +521,21 @@ static hipError_t launch_build_t(const BuildArgs &a, int cus, hipStream_t s)
 #define XCSUM_BUILD_GEOMETRIES(X) \
 	X(4, 1) X(8, 2) X(16, 2) X(16, 3) X(16, 6) X(32, 3) X(64, 2) X(64, 9)
 
-hipError_t launch_build(const BuildArgs &a, uint32_t len_hint, int cus, hipStream_t s)
+/* t: the context's tuning -- build_hdr false (A/B, tests) sends IPv4 in
+ * place through the payload-summing build kernel, as before round 5;
+ * build_G/K force a geometry (sweeps) */
+hipError_t launch_build(const BuildArgs &a, uint32_t len_hint, int cus, const Tuning &t,
+			hipStream_t s)
 {
 	if (a.n == 0)
 		return hipSuccess;
 	if (a.family == 4 && (a.flags & XCSUM_F_BUILD_INPLACE) && !(a.flags & XCSUM_F_V4_RFC) &&
-	    build_hdr_enabled())
+	    t.build_hdr)
 		return launch_build_hdr(a, cus, s);
 	/* payloads read from 16-byte aligned addresses need one block per chunk */
 	const bool two = !(a.flags & (XCSUM_F_BUILD_INPLACE | XCSUM_F_SRC_ALIGNED));
-	int G, K;
-	const char *e = getenv("XCSUM_BUILD_GEOMETRY"); /* "G,K" for sweeps */
-	if (!(e && sscanf(e, "%d,%d", &G, &K) == 2)) {
+	int G = t.build_G, K = t.build_K;
+	if (!G) {
 		/* lanes x chunks to cover a typical payload in one preload */
 		uint32_t chunks = (len_hint + 15) / 16;
 		if (chunks <= 4) { G = 4; K = 1; }
@@ -560,6 +555,15 @@ hipError_t launch_build(const BuildArgs &a, uint32_t len_hint, int cus, hipStrea
 	XCSUM_BUILD_GEOMETRIES(X)
 #undef X
 	return hipErrorInvalidValue;
+}
+
+/* xcsum_ctx_set_tuning(XCSUM_TUNE_BUILD_GEOMETRY): compiled in? */
+bool build_geometry_supported(int G, int K)
+{
+#define X(g_, k_) if (G == g_ && K == k_) return true;
+	XCSUM_BUILD_GEOMETRIES(X)
+#undef X
+	return false;
 }
 
 } /* namespace xcsum */

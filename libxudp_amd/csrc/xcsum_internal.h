@@ -154,7 +154,24 @@ struct BuildArgs {
 	Order ord;                     /* over messages */
 };
 
-hipError_t launch_build(const BuildArgs &a, uint32_t len_hint, int cus, hipStream_t s);
+/* Per-context tuning (xcsum_ctx_set_tuning, include/xcsum.h): which kernel
+ * variant or geometry a launch takes, never its results.  Set at context
+ * creation to the defaults (and, in the variant and debug builds only, from
+ * the A/B environment variables: read_env_tuning), read by the launches from
+ * the context -- no launch or batch reads the environment. */
+struct Tuning {
+	int iphdr_fpt;                 /* IPv4 header kernel: frames per thread, 1|2|4|8 */
+	bool build_hdr;                /* IPv4 in-place build: header kernel (true) or
+					  the payload-summing build kernel (A/B) */
+	int build_G, build_K;          /* build kernel geometry, G == 0: automatic */
+	int rx_G, rx_K, rx_U, rx_B;    /* receive kernel geometry, G == 0: automatic */
+	int rx_rlog, rx_tlog;          /* receive visiting order: rlog -1 automatic,
+					  0 descriptor order, else 2^R regions of 2^T tiles */
+	uint32_t gather_ratio;         /* host path: gather when the span > ratio x bytes */
+};
+
+hipError_t launch_build(const BuildArgs &a, uint32_t len_hint, int cus, const Tuning &t,
+			hipStream_t s);
 
 /* Receive-path kernel arguments (xcsum_rx.hip). */
 struct RxArgs {
@@ -171,7 +188,10 @@ struct RxArgs {
 /* per-block delivered counts of one receive launch: >= CUs x blocks per CU */
 constexpr uint32_t RX_PART_MAX = 4096;
 
-hipError_t launch_rx(const RxArgs &a, uint32_t len_hint, int cus, hipStream_t s);
+hipError_t launch_rx(const RxArgs &a, uint32_t len_hint, int cus, const Tuning &t, hipStream_t s);
+/* the build and receive kernel geometries compiled in (xcsum_ctx_set_tuning) */
+bool build_geometry_supported(int G, int K);
+bool rx_geometry_supported(int G, int K, int U);
 
 /* Kernel geometry: G lanes cooperate on one frame, each segment keeps U frames
  * in flight, and each lane preloads K 16-byte chunks per frame. */
@@ -205,7 +225,7 @@ hipError_t launch_csum_f2(const CsumArgs &a, Geometry g, int cus, hipStream_t s)
  * first 4 chunks loaded temporally (xcsum_csum_tl.hip) */
 hipError_t launch_csum_inplace_tl(const CsumArgs &a, Geometry g, int cus, hipStream_t s);
 /* XCSUM_F_IPHDR_ONLY: iph->check from the header alone (xcsum_iphdr.hip) */
-hipError_t launch_iphdr(const CsumArgs &a, hipStream_t s);
+hipError_t launch_iphdr(const CsumArgs &a, int fpt, hipStream_t s);
 hipError_t launch_gen(uint8_t *d_umem, const struct xcsum_desc *d_desc, uint32_t n,
 		      uint32_t family, uint64_t seed, uint64_t first_index, int max_blocks,
 		      hipStream_t s);
@@ -220,10 +240,14 @@ struct Region {
 			  the GPU never touches it; batches in it are staged */
 };
 
+struct StagePool;   /* xcsum_stage.h: the context's host copy threads */
+
 /* Per-thread context.  Owns only scratch: the error counter and the staging
  * ring of the host-resident path. */
 struct Ctx {
 	int device;
+	Tuning tune;                   /* xcsum_ctx_set_tuning */
+	StagePool *stage_pool;         /* host copies split over threads (lazy threads) */
 	int cus;
 	int max_blocks;
 	Geometry geom;                 /* forced geometry, G == 0: automatic */

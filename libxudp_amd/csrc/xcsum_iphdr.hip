@@ -125,15 +125,6 @@ __global__ void __launch_bounds__(256) iphdr_kernel(CsumArgs a)
 	}
 }
 
-/* frames per thread: XCSUM_IPHDR_FPT=1|2|4|8 (tuning sweeps and tests;
- * default 4), read per launch like XCSUM_BUILD_GEOMETRY */
-static int iphdr_fpt()
-{
-	const char *e = getenv("XCSUM_IPHDR_FPT");
-	const int k = e ? atoi(e) : 4;
-	return k == 1 || k == 2 || k == 8 ? k : 4;
-}
-
 template <int FPT>
 static hipError_t launch_iphdr_t(const CsumArgs &a, hipStream_t s)
 {
@@ -145,11 +136,12 @@ static hipError_t launch_iphdr_t(const CsumArgs &a, hipStream_t s)
 	return hipGetLastError();
 }
 
-hipError_t launch_iphdr(const CsumArgs &a, hipStream_t s)
+/* fpt: frames per thread, the context's Tuning::iphdr_fpt (default 4) */
+hipError_t launch_iphdr(const CsumArgs &a, int fpt, hipStream_t s)
 {
 	if (a.n == 0)
 		return hipSuccess;
-	switch (iphdr_fpt()) {
+	switch (fpt) {
 	case 1: return launch_iphdr_t<1>(a, s);
 	case 2: return launch_iphdr_t<2>(a, s);
 	case 8: return launch_iphdr_t<8>(a, s);

@@ -1387,15 +1387,24 @@ static hipError_t launch_rx_t(const RxArgs &a, int cus, int bpc, hipStream_t s)
 	X(4, 2, 0) X(8, 2, 0) X(16, 3, 0) X(16, 6, 0) X(32, 3, 0) X(64, 2, 0) X(64, 9, 0) \
 	X(64, 8, 3)
 
-hipError_t launch_rx(const RxArgs &a, uint32_t len_hint, int cus, hipStream_t s)
+/* xcsum_ctx_set_tuning(XCSUM_TUNE_RX_GEOMETRY): compiled in? */
+bool rx_geometry_supported(int G, int K, int U)
+{
+#define X(g_, k_, u_) if (G == g_ && K == k_ && U == u_) return true;
+	XCSUM_RX_GEOMETRIES(X)
+#undef X
+	return false;
+}
+
+hipError_t launch_rx(const RxArgs &a, uint32_t len_hint, int cus, const Tuning &t, hipStream_t s)
 {
 	if (a.n == 0)
 		return hipSuccess;
 	RxArgs b = a;
-	int G, K, U = 1, B = 0;
-	/* "G,K[,U[,B]]" for sweeps and tests; B = blocks per CU (0: occupancy) */
-	const char *e = getenv("XCSUM_RX_GEOMETRY");
-	if (!(e && sscanf(e, "%d,%d,%d,%d", &G, &K, &U, &B) >= 2)) {
+	/* the context's forced geometry (sweeps and tests); B = blocks per CU
+	 * (0: occupancy) */
+	int G = t.rx_G, K = t.rx_K, U = t.rx_U, B = t.rx_B;
+	if (!G) {
 		U = 1;
 		B = 0;
 		/* chunks of a typical frame from eth+12 to its end: cover it in
@@ -1440,11 +1449,10 @@ hipError_t launch_rx(const RxArgs &a, uint32_t len_hint, int cus, hipStream_t s)
 	 * (tools/sweep_rx_order.sh, profiles/r02/rx_order/): config 2 VERIFY
 	 * 0.345 -> 0.321 ms, header-only 0.0755 -> 0.069, config 3 VERIFY
 	 * 0.070 -> 0.067; 8 or 128 regions and 16-frame tiles were slower.
-	 * XCSUM_RX_ORDER=0 turns it off, "R,T" sets it (A/B). */
-	const char *oe = getenv("XCSUM_RX_ORDER");
-	int rlog = 5, tlog = 6;
+	 * The context's tuning turns it off (rx_rlog 0) or forces "R,T" (A/B). */
+	int rlog = t.rx_rlog < 0 ? 5 : t.rx_rlog, tlog = t.rx_rlog < 0 ? 6 : t.rx_tlog;
 	b.dense = order_identity(a.n);
-	if (oe && sscanf(oe, "%d,%d", &rlog, &tlog) == 1 && rlog == 0) {
+	if (rlog == 0) {
 		b.ord = order_identity(a.n);   /* "0": off */
 	} else {
 		/* "R,T": 2^R regions of 2^T-frame tiles (sweeps) */

@@ -76,15 +76,57 @@ extern "C" void xudp_packet_build_headers(struct packet_info *info)
 	info->packet = (char *)eth;
 }
 
-/* Lazily created per-thread default context (device $XCSUM_DEVICE or 0);
- * created on first use, i.e. after any fork of the caller. */
-static thread_local xcsum_ctx *t_ctx = nullptr;
+/* Lazily created per-thread default context, created on first use (i.e.
+ * after any fork of the caller) or by xcsum_thread_init: on the thread's
+ * group device, else $XCSUM_DEVICE if set, else the next device of the
+ * process's round robin (include/xcsum.h, device placement).  Kept for the
+ * life of the process, as before: a destructor at thread or process exit
+ * could run after the HIP runtime's own teardown. */
+namespace {
+struct ThreadCtx {
+	xcsum_ctx *ctx = nullptr;
+};
+thread_local ThreadCtx t_ctx;
+} /* namespace */
+
+static int default_device()
+{
+	return getenv("XCSUM_DEVICE") ? XCSUM_DEVICE_ENV : XCSUM_DEVICE_AUTO;
+}
+
+extern "C" int xcsum_thread_init(int gid)
+{
+	if (gid > 1000000)
+		return -XCSUM_ERR_INVAL;
+	const int want = gid >= 0 ? XCSUM_DEVICE_GROUP(gid) : default_device();
+	const int ndev = xcsum_device_count();
+	if (ndev < 0)
+		return ndev;
+	if (t_ctx.ctx) {
+		/* already there: keep it if it is on the wanted device */
+		if (gid < 0 || xcsum_ctx_device(t_ctx.ctx) == xcsum_device_resolve(want, ndev))
+			return 0;
+		xcsum_ctx_destroy(t_ctx.ctx);
+		t_ctx.ctx = nullptr;
+	}
+	xcsum_ctx *c = nullptr;
+	const int rc = xcsum_ctx_create(want, &c);
+	if (rc)
+		return rc;
+	t_ctx.ctx = c;
+	return 0;
+}
+
+extern "C" xcsum_ctx *xcsum_thread_ctx(void)
+{
+	if (!t_ctx.ctx && xcsum_thread_init(-1) != 0)
+		return nullptr;
+	return t_ctx.ctx;
+}
 
 static xcsum_ctx *default_ctx()
 {
-	if (!t_ctx && xcsum_ctx_create(-1, &t_ctx) != 0)
-		t_ctx = nullptr;
-	return t_ctx;
+	return xcsum_thread_ctx();
 }
 
 extern "C" int xudp_packet_udp_batch(xcsum_ctx *ctx, struct packet_info *infos, uint32_t n,

@@ -18,6 +18,13 @@
  * device path these functions print the error and abort() the process
  * before returning -- the frame is never published.  Callers that want an
  * error code instead use xudp_packet_udp_batch(), which returns it.
+ *
+ * A device that is missing altogether is a start-up problem, not a send-path
+ * one: a worker calls xcsum_thread_init(gid) once when it starts (after any
+ * fork), which creates its thread's default context on its group's GPU and
+ * returns -XCSUM_ERR_NODEV (or another code) then -- before any frame is
+ * built.  Without that call the first xudp_packet_udp() creates the context
+ * and a missing device ends the process there.
  */
 #include <stdio.h>
 #include <stdlib.h>

@@ -12,6 +12,10 @@
  *   - two host threads, each with its own context and stream on device 0
  *     (and later its own resident workgroups),
  *     running concurrently (one TX channel per thread, xudp/xsk.c:303-304);
+ *   - eight group threads (libxudp's group_num groups, test/case/lib.c:196-221)
+ *     creating contexts under each device placement policy (AUTO round
+ *     robin, XCSUM_DEVICE_GROUP, the thread's default context via
+ *     xcsum_thread_init) and checking a batch on each;
  *   - the UMEM allocated exactly as xudp does (anon_map, include/common.h:37-41,
  *     xudp/xsk.c:234), registered, checksummed staged / zero-copy / in place.
  *
@@ -429,6 +433,103 @@ static void check_threads(void)
 	}
 }
 
+/* ---- placement: 8 group threads, contexts under each policy ------------ */
+
+struct place_job {
+	int gid, ndev;
+	int dev_auto, dev_group, dev_thread;
+	int bad, err;
+};
+
+/* one 2000-frame host batch through ctx against the oracle */
+static int place_batch(xcsum_ctx *c, uint32_t family, uint64_t seed)
+{
+	const uint32_t n = 2000;
+	struct xcsum_desc *desc = calloc(n, sizeof(*desc));
+	uint64_t bytes = 0;
+	int bad = xcsum_gen_layout(n, family, 0, 1472, seed, 0, 8, 0, 0, desc, &bytes) != 0;
+	uint8_t *umem = calloc(bytes + 64, 1);
+	uint16_t *exp = calloc(n, 2), *got = calloc(n, 2);
+	const int mode = family == 6 ? XCSUM_MODE_V6 : XCSUM_MODE_V4_LEGACY;
+	bad |= xcsum_gen_fill_host(umem, desc, n, family, seed, 0) != 0;
+	orc_batch(umem, desc, n, exp, mode, 0);
+	bad |= xcsum_batch_host(c, umem, desc, n, got, (uint32_t)mode, 0) != 0;
+	bad |= count_diff(got, exp, n) != 0;
+	free(desc);
+	free(umem);
+	free(exp);
+	free(got);
+	return bad;
+}
+
+static void *place_main(void *arg)
+{
+	struct place_job *j = arg;
+	xcsum_ctx *a = NULL, *g = NULL;
+	/* XCSUM_DEVICE_AUTO: the process's round robin */
+	if (xcsum_ctx_create(XCSUM_DEVICE_AUTO, &a) != 0) {
+		j->err = 1;
+		return NULL;
+	}
+	j->dev_auto = xcsum_ctx_device(a);
+	j->bad += place_batch(a, 4, 500 + (uint64_t)j->gid);
+	/* the group's own device, gid mod the device count */
+	if (xcsum_ctx_create_for_group(j->gid, &g) != 0) {
+		j->err = 1;
+		xcsum_ctx_destroy(a);
+		return NULL;
+	}
+	j->dev_group = xcsum_ctx_device(g);
+	j->bad += place_batch(g, 6, 600 + (uint64_t)j->gid);
+	/* the thread's default context (the packet.c mirrors'), placed at the
+	 * worker's start-up */
+	if (xcsum_thread_init(j->gid) != 0 || !xcsum_thread_ctx()) {
+		j->err = 1;
+	} else {
+		j->dev_thread = xcsum_ctx_device(xcsum_thread_ctx());
+		j->bad += place_batch(xcsum_thread_ctx(), 4, 700 + (uint64_t)j->gid);
+	}
+	xcsum_ctx_destroy(a);
+	xcsum_ctx_destroy(g);
+	return NULL;
+}
+
+static void check_placement(void)
+{
+	const int ndev = xcsum_device_count();
+	CHECK(ndev >= 1, "xcsum_device_count %d", ndev);
+	if (ndev < 1)
+		return;
+	struct place_job jobs[8];
+	pthread_t th[8];
+	for (int k = 0; k < 8; k++) {
+		memset(&jobs[k], 0, sizeof(jobs[k]));
+		jobs[k].gid = k;
+		jobs[k].ndev = ndev;
+		CHECK(pthread_create(&th[k], NULL, place_main, &jobs[k]) == 0, "pthread_create");
+	}
+	int per_dev[64] = {0};
+	for (int k = 0; k < 8; k++) {
+		pthread_join(th[k], NULL);
+		CHECK(!jobs[k].err, "placement thread %d: a call failed", k);
+		CHECK(jobs[k].bad == 0, "placement thread %d: %d batches mismatched", k, jobs[k].bad);
+		CHECK(jobs[k].dev_group == k % ndev, "group %d on device %d, want %d", k,
+		      jobs[k].dev_group, k % ndev);
+		CHECK(jobs[k].dev_thread == k % ndev, "group %d default context on device %d", k,
+		      jobs[k].dev_thread);
+		CHECK(jobs[k].dev_auto >= 0 && jobs[k].dev_auto < ndev, "auto device %d",
+		      jobs[k].dev_auto);
+		if (jobs[k].dev_auto >= 0 && jobs[k].dev_auto < 64)
+			per_dev[jobs[k].dev_auto]++;
+	}
+	/* 8 AUTO contexts over ndev devices: as even as a round robin makes them */
+	for (int d = 0; d < ndev && d < 64; d++)
+		CHECK(per_dev[d] >= 8 / ndev && per_dev[d] <= (8 + ndev - 1) / ndev,
+		      "device %d got %d of 8 AUTO contexts", d, per_dev[d]);
+	printf("capi_check: placement over %d device(s): 8 groups, auto/group/thread contexts ok\n",
+	       ndev);
+}
+
 int main(int argc, char **argv)
 {
 	const int threads_only = argc > 1 && strcmp(argv[1], "--threads") == 0;
@@ -456,6 +557,7 @@ int main(int argc, char **argv)
 		check_errors(c);
 	}
 	check_threads();
+	check_placement();   /* threaded too: in the TSan run as well */
 	xcsum_ctx_destroy(c);
 	printf("capi_check: %d checks, %d failures\n", checks, failures);
 	return failures ? 1 : 0;

@@ -290,6 +290,37 @@ def iphdr_digest(cid, chunk=1 << 18):
     return h.hexdigest()
 
 
+def shard_digests(cid, worlds=(2, 4, 8), chunk=1 << 18, threads=8):
+    """Per-shard SHA-256 of the reference's udp_checksum outputs for a sharded
+    config (5): the job split by bytes into N shards (xcsum_shard_by_bytes,
+    bench.rank_slice), one digest per shard, so `bench.py --shard r/N` can pin
+    one rank's share timed alone.  The concatenation is checked against the
+    whole-job sha256_out on the way."""
+    n, fam, pmin, pmax = CONFIGS[cid]
+    seed = SEED_BASE ^ cid
+    mode = 2 if fam == 6 else 0
+    R = oracle.ref()
+    out = np.zeros(n, dtype=np.uint16)
+    for first in range(0, n, chunk):
+        m = min(chunk, n - first)
+        umem, desc = X.gen_frames_host(m, fam, pmin, pmax, seed=seed, first_index=first)
+        R.ref_batch_timed(umem.ctypes.data, desc.ctypes.data, m, out[first:].ctypes.data, mode,
+                          threads, 1)
+    whole = hashlib.sha256(out.astype("<u2").tobytes()).hexdigest()
+    full, _ = X.gen_layout(n, fam, pmin, pmax, seed=seed)
+    res = {}
+    for w in worlds:
+        hs, end = [], 0
+        for r in range(w):
+            first, count = X.shard_by_bytes(full, w, r)
+            assert first == end
+            end = first + count
+            hs.append(hashlib.sha256(out[first:end].astype("<u2").tobytes()).hexdigest())
+        assert end == n
+        res[f"sha256_out_shards{w}"] = hs
+    return whole, res
+
+
 def rx_fixtures():
     """rx_fixtures.npz: received frames (tests/golden/rx_frames.py corpus) at
     irregular offsets, the reference's own packet_parse() result for each
@@ -320,9 +351,22 @@ def main():
     ap.add_argument("--only-iphdr", action="store_true",
                     help="only add the IPv4 header-checksum digests (sha256_iphdr) to digests.json")
     ap.add_argument("--configs", default="1,2,3,4,5")
+    ap.add_argument("--only-shards", action="store_true",
+                    help="only add config 5's per-shard digests (sha256_out_shards{2,4,8})")
     args = ap.parse_args()
     if not oracle.have_ref():
         sys.exit("oracle/_ref/libxudpref.so missing: run `make -C oracle` next to /root/reference")
+    if args.only_shards:
+        path = os.path.join(OUT, "digests.json")
+        digests = json.load(open(path))
+        whole, res = shard_digests(5)
+        assert whole == digests["config5"]["sha256_out"], "config 5 whole-job digest moved"
+        digests["config5"].update(res)
+        digests["config5"]["shards_source"] = \
+            "reference checksum.h udp_checksum (oracle/_ref), split by xcsum_shard_by_bytes"
+        json.dump(digests, open(path, "w"), indent=1, sort_keys=True)
+        print({k: v[:1] for k, v in res.items()})
+        return
     if args.only_build:
         build_frame_fixtures()
         return

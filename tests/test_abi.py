@@ -159,6 +159,9 @@ def test_argument_validation_without_gpu():
     assert L.xcsum_ctx_calibrate_order(None, None, None, 1, None, 0, 0, 0, None,
                                        ctypes.byref(r), ctypes.byref(t)) == -X.ERR_INVAL
     assert (r.value, t.value) == (7, 7)                         # untouched on error
+    assert L.xcsum_ctx_set_tuning(None, X.TUNE_IPHDR_FPT, 4, 0, 0, 0) == -X.ERR_INVAL
+    assert L.xcsum_ctx_set_resident_life(None, 100) == -X.ERR_INVAL
+    assert L.xcsum_ctx_create_for_group(-1, None) == -X.ERR_INVAL
 
 
 def test_geometry_list_matches_kernel_source():
@@ -229,6 +232,16 @@ def test_constants_match_header():
         "XCSUM_INPLACE_TWO_PASS": X.INPLACE_TWO_PASS,
         "XCSUM_RX_OK": X.RX_OK, "XCSUM_RX_PARSE": X.RX_PARSE, "XCSUM_RX_STATS": X.RX_STATS,
         "XCSUM_RX_CSUM": X.RX_CSUM,
+        "XCSUM_TUNE_IPHDR_FPT": X.TUNE_IPHDR_FPT, "XCSUM_TUNE_BUILD_HDR": X.TUNE_BUILD_HDR,
+        "XCSUM_TUNE_BUILD_GEOMETRY": X.TUNE_BUILD_GEOMETRY,
+        "XCSUM_TUNE_RX_GEOMETRY": X.TUNE_RX_GEOMETRY, "XCSUM_TUNE_RX_ORDER": X.TUNE_RX_ORDER,
+        "XCSUM_TUNE_GATHER_RATIO": X.TUNE_GATHER_RATIO,
+        "XCSUM_TUNE_INPLACE_BLOCK": X.TUNE_INPLACE_BLOCK,
+        "XCSUM_TUNE_INPLACE_TL": X.TUNE_INPLACE_TL,
+        "XCSUM_TUNE_RESIDENT_INLINE": X.TUNE_RESIDENT_INLINE,
+        "XCSUM_TUNE_RESIDENT_LIMIT_CUT": X.TUNE_RESIDENT_LIMIT_CUT,
+        "XCSUM_DEVICE_ENV": X.DEVICE_ENV, "XCSUM_DEVICE_AUTO": X.DEVICE_AUTO,
+        "XCSUM_DEVICE_GROUP(7)": X.DEVICE_GROUP(7),
     }
     src = "#include <stdio.h>\n#include \"xcsum.h\"\nint main(void) {\n" + "".join(
         f'  printf("{k} %lld\\n", (long long)({k}));\n' for k in names) + "  return 0;\n}\n"
@@ -238,7 +251,7 @@ def test_constants_match_header():
                     "-I/opt/rocm/include", os.path.join(d, "c.c"), "-o", os.path.join(d, "c")],
                    check=True)
     out = subprocess.run([os.path.join(d, "c")], capture_output=True, text=True, check=True).stdout
-    got = {k: int(v) for k, v in (line.split() for line in out.splitlines())}
+    got = {k: int(v) for k, v in (line.rsplit(" ", 1) for line in out.splitlines())}
     assert got == names
 
 

@@ -121,7 +121,7 @@ def test_build_ipv4_inplace_header_kernel(torch_cuda, engine, monkeypatch, slot_
     payload already sits in its slot -- takes the header-only build kernel
     (no payload byte read: iph->check only, udp->check 0, packet.c:43-66,
     :125).  Its slots, descriptors and results equal the payload-summing
-    kernel's (XCSUM_BUILD_HDR=0) and the oracle's frames, for ragged
+    kernel's (XCSUM_TUNE_BUILD_HDR 0) and the oracle's frames, for ragged
     payloads in scattered slots."""
     rng = np.random.default_rng(23)
     n = 3001
@@ -131,12 +131,16 @@ def test_build_ipv4_inplace_header_kernel(torch_cuda, engine, monkeypatch, slot_
     slots = rng.permutation(n + 500)[:n].astype(np.uint32)
     r = ROUTES[4]
     res = {}
-    for hdr_kernel in ("1", "0"):
-        monkeypatch.setenv("XCSUM_BUILD_HDR", hdr_kernel)
-        engine.take_errors()
-        res[hdr_kernel] = device_build(torch_cuda, engine, route_of(4, r), pays, inplace=True,
-                                       slots=slots, len_hint=700, FRAME=slot_size)[:3]
-        assert engine.take_errors() == 0
+    try:
+        for hdr_kernel in ("1", "0"):
+            engine.set_tuning(X.TUNE_BUILD_HDR, int(hdr_kernel))
+            engine.take_errors()
+            res[hdr_kernel] = device_build(torch_cuda, engine, route_of(4, r), pays,
+                                           inplace=True, slots=slots, len_hint=700,
+                                           FRAME=slot_size)[:3]
+            assert engine.take_errors() == 0
+    finally:
+        engine.set_tuning(X.TUNE_BUILD_HDR, 1)
     for a, b in zip(res["1"], res["0"]):
         assert np.array_equal(a, b)
     after, desc, out = res["1"]
@@ -154,15 +158,18 @@ def test_build_ipv4_header_kernel_batch_edges(torch_cuda, engine, monkeypatch, n
     the next message prefetched) at batch tails, and at 300,001 messages
     more than two rounds of a full grid (256 CUs x 8 blocks x 64 messages):
     slots, descriptors and results equal the payload-summing kernel's
-    (XCSUM_BUILD_HDR=0), in xudp's 4096-byte slots."""
+    (XCSUM_TUNE_BUILD_HDR 0), in xudp's 4096-byte slots."""
     rng = np.random.default_rng(n)
     pays = [rng.integers(0, 256, int(L), dtype=np.uint8)
             for L in rng.integers(0, 1473, n)]
     res = {}
-    for hdr_kernel in ("1", "0"):
-        monkeypatch.setenv("XCSUM_BUILD_HDR", hdr_kernel)
-        res[hdr_kernel] = device_build(torch_cuda, engine, route_of(4, ROUTES[4]), pays,
-                                       inplace=True, len_hint=700, FRAME=4096)[:3]
+    try:
+        for hdr_kernel in ("1", "0"):
+            engine.set_tuning(X.TUNE_BUILD_HDR, int(hdr_kernel))
+            res[hdr_kernel] = device_build(torch_cuda, engine, route_of(4, ROUTES[4]), pays,
+                                           inplace=True, len_hint=700, FRAME=4096)[:3]
+    finally:
+        engine.set_tuning(X.TUNE_BUILD_HDR, 1)
     for a, b in zip(res["1"], res["0"]):
         assert np.array_equal(a, b)
     assert np.array_equal(res["1"][1]["len"], np.array([len(p) + 42 for p in pays]))

@@ -36,6 +36,43 @@ def run_dist(config, steps=2, extra=(), nproc=2, backend="gloo"):
     return json.loads(lines[0])
 
 
+def run_bare(config, nproc=2, steps=2, extra=()):
+    """The command the driver runs, bare: no torch.distributed.run around it,
+    no WORLD_SIZE in the environment -- bench.py starts its own ranks."""
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(nproc), "--same-device",
+           "--dist-backend", "gloo", "--config", str(config), "--steps", str(steps),
+           "--warmup", "1", "--reps", "2", "--ramp-ms", "0", "--no-ceiling", "--no-cpu-baseline",
+           *extra]
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, cwd=ROOT, env=env)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    return json.loads(lines[0])
+
+
+def test_bare_command_launches_its_ranks():
+    """`bench.py --gpus 2` with no launcher runs 2 ranks and
+    reports them; config 5's shards concatenate to the reference's digest."""
+    line = run_bare(5)
+    assert line["n_gpus"] == 2 and line["per_rank"]["ranks"] == 2
+    assert line["config"]["parallelism"] == "dp2"
+    assert line["config"]["frames_total"] == 8 << 20
+    assert line["parity_digest"]["ok"] is True, line["parity_digest"]
+    assert "concatenated outputs of 2 ranks" in line["parity_digest"]["what"]
+
+
+def test_shard_alone_digest():
+    """`--shard 7/8`: one process times the last rank's share of the 8-GPU
+    job alone; its output equals the reference's digest of that shard."""
+    line = run_bare(5, nproc=1, extra=("--shard", "7/8"))
+    assert line["n_gpus"] == 1 and line["config"]["shard"].startswith("7/8")
+    assert line["parity_digest"]["ok"] is True, line["parity_digest"]
+    assert "sha256_out_shards8[7]" in line["parity_digest"]["what"]
+    assert line["parity_spot_check"] is True
+
+
 def test_two_ranks_config5_sharded_digest():
     line = run_dist(5)
     assert line["n_gpus"] == 2 and line["config"]["frames_total"] == 8 << 20

@@ -160,8 +160,15 @@ def host_fuzz_case(torch_cuda, engine, seed):
                              f"(zerocopy {zerocopy}, flags {flags:#x}): " + "; ".join(where))
 
 
+@pytest.fixture
+def fpt_reset(engine):
+    """the header kernel's frames per thread back to the default after a test"""
+    yield
+    engine.set_tuning(X.TUNE_IPHDR_FPT, 4)
+
+
 @pytest.mark.parametrize("seed", range(48))
-def test_fuzz_iphdr_only(torch_cuda, engine, monkeypatch, seed):
+def test_fuzz_iphdr_only(torch_cuda, engine, fpt_reset, seed):
     """XCSUM_F_IPHDR_ONLY (libxudp's IPv4 call) on random batches -- IPv6
     and malformed frames mixed in, random phases, layouts and frames per
     thread -- on the device against the oracle (orc_iphdr_only), and through
@@ -172,7 +179,7 @@ def test_fuzz_iphdr_only(torch_cuda, engine, monkeypatch, seed):
     umem, desc = random_batch(rng)
     mode = int(rng.choice([X.MODE_V4_LEGACY, X.MODE_V4_RFC, X.MODE_AUTO]))
     flags = X.F_IPHDR_ONLY | int(rng.choice([0, X.F_INPLACE, X.F_VERIFY, X.F_VERIFY | X.F_INPLACE]))
-    monkeypatch.setenv("XCSUM_IPHDR_FPT", str(rng.choice(["1", "2", "4", "8"])))
+    engine.set_tuning(X.TUNE_IPHDR_FPT, int(rng.choice([1, 2, 4, 8])))
     exp = oracle.batch(umem, desc, mode, flags & ~X.F_INPLACE)
     got, after = run_device(torch_cuda, engine, umem, desc, mode, flags)
     bad = np.nonzero(got != exp)[0]

@@ -139,20 +139,20 @@ def test_host_batch_mtu_frames_in_slots_gathered(engine, monkeypatch, fam):
     the range: gathered frame by frame since round 5 (gather_pays), the
     copies and the in-place stores split over threads (>= 16384 frames),
     several chunks.  The same results with the range copy
-    (XCSUM_GATHER_RATIO=8, the rule before) and through the receive path."""
+    (XCSUM_TUNE_GATHER_RATIO 8, the rule before) and through the receive path."""
     n = 40000
     umem, desc = X.gen_frames_host(n, fam, 1000, 1472 if fam == 4 else 1452, seed=77 + fam,
                                    stride=4096, offset=322 if fam == 6 else 342)
     mode = X.MODE_V6 if fam == 6 else X.MODE_V4_RFC
     exp = oracle.batch(umem, desc, mode)
     before = umem.copy()
-    for ratio in ("8", None):
-        if ratio:
-            monkeypatch.setenv("XCSUM_GATHER_RATIO", ratio)
-        else:
-            monkeypatch.delenv("XCSUM_GATHER_RATIO", raising=False)
-        assert np.array_equal(host_batch(engine, umem, desc, mode), exp), ratio
-        assert np.array_equal(umem, before)
+    try:
+        for ratio in (8, 0):
+            engine.set_tuning(X.TUNE_GATHER_RATIO, ratio)     # 0: the default, 2
+            assert np.array_equal(host_batch(engine, umem, desc, mode), exp), ratio
+            assert np.array_equal(umem, before)
+    finally:
+        engine.set_tuning(X.TUNE_GATHER_RATIO, 0)
     flags = X.F_INPLACE | (X.F_IPHDR if fam == 4 else 0)
     assert np.array_equal(host_batch(engine, umem, desc, mode, flags), exp)
     a = desc["addr"].astype(np.int64)

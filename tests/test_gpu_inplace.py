@@ -76,14 +76,13 @@ def test_golden_schedules(torch_cuda, engine, golden, sched, geom, flags, out):
 @pytest.mark.parametrize("block", [0, 32, 64])
 @pytest.mark.parametrize("layout", ["packed1", "packed8", "slots"])
 def test_two_pass_store_widths(torch_cuda, monkeypatch, block, layout):
-    """The second pass's store widths (XCSUM_INPLACE_BLOCK): 2-byte stores,
+    """The second pass's store widths (XCSUM_TUNE_INPLACE_BLOCK): 2-byte stores,
     or the whole 32-B sector / 64-B line holding a field, read and patched
     when it lies inside the frame.  Frames at every byte phase, packed (the
     blocks of neighbouring frames' fields meet) and in xudp's slots: the
     reference's fields in place and not one other byte changed."""
-    monkeypatch.setenv("XCSUM_INPLACE_BLOCK", str(block))
     e = X.Engine(0)
-    monkeypatch.delenv("XCSUM_INPLACE_BLOCK")
+    e.set_tuning(X.TUNE_INPLACE_BLOCK, block)
     try:
         e.set_inplace(X.INPLACE_TWO_PASS)
         for fam, mode in ((4, X.MODE_V4_RFC), (6, X.MODE_V6), (4, X.MODE_AUTO)):

@@ -56,18 +56,21 @@ def test_receive_across_2g_and_4g(torch_cuda, engine, big, geometry, monkeypatch
     umem, desc = X.gen_frames_host(700, 6, 0, 3000, seed=3)
     exp = oracle.rx_batch(umem, desc, X.F_VERIFY)
     if geometry:
-        monkeypatch.setenv("XCSUM_RX_GEOMETRY", geometry)
-    for off in OFFSETS:
-        d_desc = place(torch_cuda, big, umem, desc, off)
-        msgs = torch_cuda.zeros(len(desc) * 64, dtype=torch_cuda.uint8, device="cuda:0")
-        engine.rx_device(big, d_desc, len(desc), msgs, None, X.F_VERIFY, 1500)
-        torch_cuda.cuda.synchronize()
-        got = d2h(msgs).view(X.RX_MSG_DTYPE)
-        # records hold UMEM offsets: compare with the expected ones moved by off
-        e = exp.copy()
-        e["frame"] += off
-        e["body"][e["body"] != 0] += off
-        assert np.array_equal(got.view(np.uint8), e.view(np.uint8)), (geometry, off)
+        engine.set_tuning(X.TUNE_RX_GEOMETRY, *[int(v) for v in geometry.split(",")])
+    try:
+        for off in OFFSETS:
+            d_desc = place(torch_cuda, big, umem, desc, off)
+            msgs = torch_cuda.zeros(len(desc) * 64, dtype=torch_cuda.uint8, device="cuda:0")
+            engine.rx_device(big, d_desc, len(desc), msgs, None, X.F_VERIFY, 1500)
+            torch_cuda.cuda.synchronize()
+            got = d2h(msgs).view(X.RX_MSG_DTYPE)
+            # records hold UMEM offsets: compare with the expected ones moved by off
+            e = exp.copy()
+            e["frame"] += off
+            e["body"][e["body"] != 0] += off
+            assert np.array_equal(got.view(np.uint8), e.view(np.uint8)), (geometry, off)
+    finally:
+        engine.set_tuning(X.TUNE_RX_GEOMETRY, 0)
 
 
 @pytest.mark.parametrize("inplace", [False, True])

@@ -37,18 +37,15 @@ def run_rx(torch, eng, umem, desc, flags, len_hint=0, geometry=None):
     d_desc = h2d(torch, desc.view(np.uint8), dev)
     d_msgs = torch.full((max(len(desc), 1) * 64,), 0xA5, dtype=torch.uint8, device=dev)
     d_count = torch.full((1,), 77, dtype=torch.int32, device=dev)
-    old = os.environ.get("XCSUM_RX_GEOMETRY")
     if geometry:
-        os.environ["XCSUM_RX_GEOMETRY"] = str(geometry)
+        # the context's forced receive geometry (XCSUM_TUNE_RX_GEOMETRY: G, K, U)
+        eng.set_tuning(X.TUNE_RX_GEOMETRY, *[int(v) for v in str(geometry).split(",")])
     try:
         eng.rx_device(d_umem, d_desc, len(desc), d_msgs, d_count, flags, len_hint)
         torch.cuda.synchronize()
     finally:
         if geometry:
-            if old is None:
-                del os.environ["XCSUM_RX_GEOMETRY"]
-            else:
-                os.environ["XCSUM_RX_GEOMETRY"] = old
+            eng.set_tuning(X.TUNE_RX_GEOMETRY, 0)
     recs = d2h(d_msgs)[:len(desc) * 64].view(X.RX_MSG_DTYPE)
     return recs, int(d_count.cpu().item())
 
@@ -144,13 +141,11 @@ def test_rx_sparse_umem_vs_oracle(torch_cuda, engine, geometry, order):
     """Frames one per UMEM chunk (sparse: the kernels visit them in region
     order, launch_rx) and a batch size that leaves the last tiles partly or
     wholly past the end: the same records and count as the oracle, with the
-    order on and off (XCSUM_RX_ORDER=0)."""
+    order on and off (XCSUM_TUNE_RX_ORDER 0)."""
     frames = [f for f, _ in rx_frames.corpus(seed=11)]
     rng = np.random.default_rng(12)
     umem, desc = umem_chunks(frames, rng, 4099)
-    old = os.environ.pop("XCSUM_RX_ORDER", None)
-    if order != "auto":
-        os.environ["XCSUM_RX_ORDER"] = order
+    engine.set_tuning(X.TUNE_RX_ORDER, -1 if order == "auto" else int(order))
     try:
         for flags in FLAGS.values():
             exp = oracle.rx_batch(umem, desc, flags)
@@ -159,9 +154,7 @@ def test_rx_sparse_umem_vs_oracle(torch_cuda, engine, geometry, order):
             assert len(bad[0]) == 0, (flags, sorted(set(bad[0].tolist()))[:10])
             assert count == int((exp["status"] == X.RX_OK).sum())
     finally:
-        os.environ.pop("XCSUM_RX_ORDER", None)
-        if old is not None:
-            os.environ["XCSUM_RX_ORDER"] = old
+        engine.set_tuning(X.TUNE_RX_ORDER, -1)
 
 
 def test_rx_empty_batch(torch_cuda, engine):

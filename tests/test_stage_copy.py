@@ -16,6 +16,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 DRIVER = r'''
 #include "xcsum_stage.h"
+#include <algorithm>
 #include <stdio.h>
 #include <stdlib.h>
 #include <vector>
@@ -29,6 +30,13 @@ static uint64_t rnd() {                      /* SplitMix64 */
 }
 
 int main(int argc, char **argv) {
+  if (argc == 2 && !strcmp(argv[1], "budget")) {
+    /* threads a large copy takes under this process's CPU budget */
+    printf("usable=%d threads=%d\n", xcsum::usable_cpus(),
+           xcsum::stage_threads(64u << 20, 1));
+    return 0;
+  }
+  xcsum::StagePool pool;
   const uint32_t n = (uint32_t)atoi(argv[1]);
   const uint32_t cap = (uint32_t)strtoul(argv[2], 0, 10);
   const uint32_t maxlen = (uint32_t)atoi(argv[3]);
@@ -56,7 +64,12 @@ int main(int argc, char **argv) {
   for (uint32_t k = 0; k < n; k++)
     memcpy(ref.data() + ref_ds[k].addr, umem.data() + d[k].addr,
            d[k].len < cap ? d[k].len : cap);
-  const uint64_t r = xcsum::gather_frames(got.data(), umem.data(), d.data(), ds.data(), n, cap);
+  uint64_t r = 0;
+  for (int rep = 0; rep < 3; rep++) {   /* the pool's threads serve every call */
+    std::fill(got.begin(), got.end(), 0xa5);
+    r = xcsum::gather_frames(&pool, got.data(), umem.data(), d.data(), ds.data(), n, cap);
+    if (memcmp(ref.data(), got.data(), ref.size())) { printf("gathered bytes differ\n"); return 1; }
+  }
   if (r != total) { printf("pos %llu != %llu\n", (unsigned long long)r, (unsigned long long)total); return 1; }
   for (uint32_t k = 0; k < n; k++)
     if (ds[k].addr != ref_ds[k].addr || ds[k].len != d[k].len || ds[k].options) {
@@ -66,9 +79,11 @@ int main(int argc, char **argv) {
   /* the range copy, at a size that splits (>= 4 MiB, not a page multiple) */
   const uint64_t m = umem_bytes - 4093 < (9u << 20) ? umem_bytes - 4093 : (9u << 20) + 77;
   std::vector<uint8_t> dst(m + 16, 0x3c);
-  xcsum::stage_copy(dst.data(), umem.data() + 3, m);
+  xcsum::stage_copy(&pool, dst.data(), umem.data() + 3, m);
   if (memcmp(dst.data(), umem.data() + 3, m) || dst[m] != 0x3c) { printf("range copy\n"); return 1; }
-  printf("ok threads=%d\n", xcsum::stage_threads(total, n));
+  xcsum::stage_copy(nullptr, dst.data(), umem.data() + 5, m);   /* no pool: serial */
+  if (memcmp(dst.data(), umem.data() + 5, m)) { printf("serial range copy\n"); return 1; }
+  printf("ok threads=%d pool=%d\n", xcsum::stage_threads(total, n), pool.threads());
   return 0;
 }
 '''
@@ -105,8 +120,41 @@ def test_gather_and_range_copy(driver, n, cap, maxlen, seed):
     r = subprocess.run([driver, str(n), str(cap), str(maxlen), str(seed)], capture_output=True,
                        text=True, timeout=120)
     assert r.returncode == 0 and r.stdout.startswith("ok"), r.stdout + r.stderr
-    if n >= 16384:
-        assert "threads=1" not in r.stdout       # the split path ran
+    if n >= 16384 and _usable() >= 4:
+        assert "threads=1 " not in r.stdout      # the split path ran
+        assert "pool=0" not in r.stdout          # on the pool's threads
+
+
+def _usable():
+    n = len(os.sched_getaffinity(0))
+    try:
+        q, p = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            n = min(n, -(-int(q) // int(p)))
+    except (OSError, ValueError):
+        pass
+    return n
+
+
+def test_budget_follows_affinity(driver):
+    """the copy threads follow the caller's CPU budget, not the
+    machine's CPU count: one CPU in the affinity mask (a libxudp TX worker
+    pinned to a core) -> 1 thread; a wide mask -> STAGE_THREADS (4)."""
+    import shutil
+    if not shutil.which("taskset"):
+        pytest.skip("no taskset")
+    cpu = sorted(os.sched_getaffinity(0))[0]
+    r = subprocess.run(["taskset", "-c", str(cpu), driver, "budget"], capture_output=True,
+                       text=True, timeout=60)
+    assert r.returncode == 0 and r.stdout.split() == ["usable=1", "threads=1"], r.stdout
+    cpus = sorted(os.sched_getaffinity(0))
+    if len(cpus) >= 3:
+        r = subprocess.run(["taskset", "-c", ",".join(map(str, cpus[:3])), driver, "budget"],
+                           capture_output=True, text=True, timeout=60)
+        assert r.stdout.split() == ["usable=3", "threads=1"], r.stdout
+    r = subprocess.run([driver, "budget"], capture_output=True, text=True, timeout=60)
+    want = 4 if _usable() >= 8 else (_usable() // 2 if _usable() >= 4 else 1)
+    assert r.stdout.split() == [f"usable={_usable()}", f"threads={want}"], r.stdout
 
 
 def test_gather_threads_tsan_clean():

@@ -1,4 +1,8 @@
 #!/bin/bash
+# The XCSUM_* tuning variables are read only by the A/B build (`make -C
+# libxudp_amd variant NAME=ab`, -DXCSUM_ENV_TUNING): run with
+# XCSUM_LIB=libxudp_amd/variants/ab/libxcsum.so; libxcsum.so takes them
+# through xcsum_ctx_set_tuning only.
 # same-box A/B of the resident inline descriptors: ring bench, 1/2/4 frames
 set -u
 for r in 1 2; do

@@ -85,11 +85,8 @@ def main():
         flags = {"inplace": X.F_BUILD_INPLACE, "inplace_sum": X.F_BUILD_INPLACE,
                  "copy_aligned": X.F_SRC_ALIGNED}.get(mode, 0)
         # inplace_sum (A/B): IPv4 in place through the payload-summing build
-        # kernel (XCSUM_BUILD_HDR=0, read per launch), as before round 5
-        if mode == "inplace_sum":
-            os.environ["XCSUM_BUILD_HDR"] = "0"
-        else:
-            os.environ.pop("XCSUM_BUILD_HDR", None)
+        # kernel (xcsum_ctx_set_tuning XCSUM_TUNE_BUILD_HDR 0), as before round 5
+        eng.set_tuning(X.TUNE_BUILD_HDR, 0 if mode == "inplace_sum" else 1)
         for order in args.orders.split(","):
             if order == "auto":
                 eng.set_order(-1, 0)
@@ -122,7 +119,7 @@ def main():
             else:
                 moved = n * (L + hdr + L + 32)
             rec = {"mode": mode, "order": order, "rotating_umems": args.rot,
-                   "geometry": os.environ.get("XCSUM_BUILD_GEOMETRY", "auto"),
+                   "geometry": "auto",
                    "payload": L, "family": fam, "frames": n, "ms": round(t * 1e3, 4),
                    "mpps": round(n / t / 1e6, 1), "GBps_moved": round(moved / t / 1e9, 1),
                    "pct_hbm_peak": round(100 * moved / t / 8e12, 1)}

@@ -83,9 +83,9 @@ def main():
         def rx_fn(flags, gname):
             def rx(k):
                 if gname == "auto":
-                    os.environ.pop("XCSUM_RX_GEOMETRY", None)
+                    eng.set_tuning(X.TUNE_RX_GEOMETRY, 0)
                 else:
-                    os.environ["XCSUM_RX_GEOMETRY"] = gname
+                    eng.set_tuning(X.TUNE_RX_GEOMETRY, *[int(v) for v in gname.split(",")])
                 eng.rx_device(bufs[k % nrot], d_desc, n, d_msgs,
                               None if args.no_count else d_count, flags, hint,
                               stream=s.cuda_stream)
@@ -128,7 +128,7 @@ def main():
                 e1.record(s)
                 torch.cuda.synchronize()
                 times[i].append(e0.elapsed_time(e1) / K * 1e-3)
-        os.environ.pop("XCSUM_RX_GEOMETRY", None)
+        eng.set_tuning(X.TUNE_RX_GEOMETRY, 0)
         # clocks while kernels run: the boxes differ on this kernel far more
         # than on the checksum kernel, and SCLK is the first suspect
         for k in range(3 * K):

@@ -20,12 +20,12 @@ frames, packed (1520-B stride) or in xudp's 4096-B slots, 1M frames in a
   lib_plain+X     the library's plain pass, then second pass X (copy64,
                   blind64, w2)
   lib_two_pass_wW[_out]  the library's TWO_PASS schedule with second-pass
-                  store width W (XCSUM_INPLACE_BLOCK; 0: 2-byte stores);
+                  store width W (XCSUM_TUNE_INPLACE_BLOCK; 0: 2-byte stores);
                   _out: with a result array (no scratch)
   fused_blkW      the read, each W-byte block holding a field stored back
                   whole by the wave that read it (W = 16/32/64/128)
   lib_fused_tl2/4 the library's fused pass with each frame's first 2 / 4
-                  chunks loaded temporally (XCSUM_INPLACE_TL)
+                  chunks loaded temporally (XCSUM_TUNE_INPLACE_TL)
 Prints one JSON line per layout and family."""
 import argparse
 import ctypes
@@ -134,9 +134,8 @@ def main():
         return f
     engs_tl = {}
     for tl in (2, 4):
-        os.environ["XCSUM_INPLACE_TL"] = str(tl)
         engs_tl[tl] = X.Engine(0)
-    del os.environ["XCSUM_INPLACE_TL"]
+        engs_tl[tl].set_tuning(X.TUNE_INPLACE_TL, tl)
 
     def lib_tl(tl):
         def f(b):
@@ -146,10 +145,9 @@ def main():
         return f
     engs_blk = {}
     for w in (0, 32, 64):
-        os.environ["XCSUM_INPLACE_BLOCK"] = str(w)
         engs_blk[w] = X.Engine(0)
+        engs_blk[w].set_tuning(X.TUNE_INPLACE_BLOCK, w)
         engs_blk[w].set_inplace(X.INPLACE_TWO_PASS)
-    del os.environ["XCSUM_INPLACE_BLOCK"]
 
     def lib_blk(w, o):
         def f(b):

@@ -2,7 +2,7 @@
 """Same-run legs of libxudp's IPv4 TX call on the device (xcsum_batch_device
 with XCSUM_F_IPHDR_ONLY, csrc/xcsum_iphdr.hip) on BASELINE config 2's frames,
 packed (1520-byte stride) and in xudp's 4096-byte slots: in place and/or
-into a result array, frames per thread (XCSUM_IPHDR_FPT), visiting orders.
+into a result array, frames per thread (XCSUM_TUNE_IPHDR_FPT), visiting orders.
 Each leg: `per` back-to-back launches between two events, median of `reps`,
 legs interleaved over `rounds` rounds, the lowest median kept.
 One JSON line per layout.
@@ -88,7 +88,7 @@ def main():
         for rnd in range(args.rounds):
             for leg in legs:
                 flags, with_out, fpt, order = LEGS[leg]
-                os.environ["XCSUM_IPHDR_FPT"] = fpt
+                eng.set_tuning(X.TUNE_IPHDR_FPT, int(fpt))
                 eng.set_order(*(order or (-1, 0)))
                 o = out if with_out else None
                 ts = []
@@ -106,7 +106,7 @@ def main():
                 if with_out and args.ref:
                     assert torch.equal(out, ref), leg
         eng.set_order(-1, 0)
-        os.environ.pop("XCSUM_IPHDR_FPT", None)
+        eng.set_tuning(X.TUNE_IPHDR_FPT, 4)
         real = bench.real_bytes(desc, X.F_IPHDR_ONLY)
         print(json.dumps({"layout": layout, "frames": cfg["n"], "real_bytes": real,
                           "rotating_buffers": args.rot,

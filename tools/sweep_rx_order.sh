@@ -1,4 +1,8 @@
 #!/bin/bash
+# The XCSUM_* tuning variables are read only by the A/B build (`make -C
+# libxudp_amd variant NAME=ab`, -DXCSUM_ENV_TUNING): run with
+# XCSUM_LIB=libxudp_amd/variants/ab/libxcsum.so; libxcsum.so takes them
+# through xcsum_ctx_set_tuning only.
 # RX visiting-order sweep on xudp's UMEM layout: tools/bench_rx.py under each
 # XCSUM_RX_ORDER value ("0" off, "R,T" 2^R regions of 2^T-frame tiles).
 #   tools/sweep_rx_order.sh <outdir under gpurun_out> "0;5,6;3,6" [configs]
