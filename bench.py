@@ -583,6 +583,60 @@ def stream_ceiling(torch, dev, bufs, sptr):
                     f"two events, median of 5"}
 
 
+def span_ceiling(torch, dev, bufs, d_desc, desc, sptr, real):
+    """Like-for-like ceiling of a sparse layout (xudp's 4096-byte slots,
+    --layout umem): tools/libhbmprobe.so's probe_frame_spans
+    makes exactly the loads the checksum kernel must make -- per frame its
+    descriptor and every 16-byte chunk of [addr & ~15, addr + len) -- with no
+    arithmetic, the frames visited in the kernel's sparse order (32 regions
+    of 16-frame tiles) and, as a second leg, in descriptor order; plain and
+    nontemporal loads; the fastest leg counts.  Rates over the same real
+    bytes as roofline.real_achieved.  None where the probe is missing."""
+    path = os.path.join(ROOT, "tools", "libhbmprobe.so")
+    if not os.path.exists(path) or not len(desc):
+        return None
+    L = ctypes.CDLL(path)
+    fn = getattr(L, "probe_frame_spans", None)
+    if fn is None:
+        return None
+    fn.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_int, ctypes.c_int,
+                   ctypes.c_uint32, ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]
+    a = desc["addr"].astype(np.int64)
+    span16 = int((((a + desc["len"].astype(np.int64) + 15) >> 4) - (a >> 4)).max())
+    # host-side bounds: every chunk the probe may load lies inside the buffer
+    assert int(((a + desc["len"].astype(np.int64) + 15) & ~15).max()) <= bufs[0].numel()
+    cus = torch.cuda.get_device_properties(dev).multi_processor_count
+    blocks = cus * 8
+    scratch = torch.empty(blocks, dtype=torch.int32, device=dev)
+    per = max(10, len(bufs))
+    s = torch.cuda.current_stream(dev)
+    legs = {}
+    for name, (rlog, tlog) in (("regions_5_4", (5, 4)), ("descriptor_order", (0, 0))):
+        for nt in (0, 1):
+            ts = []
+            for r in range(6):
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(s)
+                for k in range(per):
+                    if fn(bufs[k % len(bufs)].data_ptr(), d_desc.data_ptr(), len(desc), rlog, tlog,
+                          span16, nt, scratch.data_ptr(), blocks, sptr) != 0:
+                        return None
+                e1.record(s)
+                torch.cuda.synchronize(dev)
+                ts.append(e0.elapsed_time(e1) / per)
+            legs[f"{name}{'_nt' if nt else ''}"] = float(np.median(ts[1:]))
+    best = min(legs, key=legs.get)
+    t = legs[best]
+    return {"ms": round(t, 4), "ms_by_leg": {k: round(v, 4) for k, v in legs.items()},
+            "fastest": best, "GBps": round(real / (t * 1e-3) / 1e9, 1),
+            "what": f"tools/hbm_probe.hip probe_frame_spans: per frame the 16-byte descriptor and "
+                    f"the {span16} 16-byte chunks of its span, no arithmetic, in the kernel's "
+                    f"sparse order (32 regions of 16-frame tiles) or descriptor order, plain or "
+                    f"nontemporal loads; the fastest leg; rate over the same real bytes as "
+                    f"real_achieved; {per} back-to-back launches between two events, median "
+                    f"of 5"}
+
+
 def inplace_ceiling(torch, dev, bufs, desc, flags, family, sptr):
     """Same-run ceiling of the in-place pass: tools/libhbmprobe.so's stream
     read of the same buffers plus one 2-byte store per frame into its
@@ -1044,9 +1098,12 @@ def main():
     elapsed_max = float(np.median(walls_max))
     alg_all, frames_all = float(tot[0]), float(tot[1])
 
-    ceiling = inplace = orders = hdr_probe = None
+    ceiling = inplace = orders = hdr_probe = spans = None
     if rank == 0 and not args.no_ceiling:
         ceiling = stream_ceiling(torch, dev, bufs, sptr)
+        if args.layout == "umem" and not flags & (X.F_INPLACE | X.F_IPHDR_ONLY):
+            # xudp's slots: the loads the kernel must make, in its order
+            spans = span_ceiling(torch, dev, bufs, d_desc, desc, sptr, real_bytes(desc, flags))
         if flags & X.F_IPHDR_ONLY:
             hdr_probe = header_ceiling(torch, dev, bufs, d_desc, count,
                                        bool(flags & X.F_INPLACE) and not flags & X.F_VERIFY,
@@ -1153,6 +1210,13 @@ def main():
             roof["layout_bound_GBps"] = round(bound, 1)
             roof["layout_bound_frac"] = round(bound / HBM_PEAK_GBS, 4)
             roof["frac_of_layout_bound"] = round(achieved / bound, 4)
+        if spans:
+            # the layout's like-for-like bound: the same loads, no arithmetic
+            roof["span_probe_ms"] = spans["ms"]
+            roof["span_probe_GBps"] = spans["GBps"]
+            roof["span_probe_ms_by_leg"] = spans["ms_by_leg"]
+            roof["frac_vs_span_probe"] = round(spans["ms"] / kern_ms, 4)
+            roof["span_probe"] = spans["what"]
         if orders:
             roof["order_ab"] = orders
         if hdr_probe:

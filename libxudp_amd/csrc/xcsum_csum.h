@@ -386,6 +386,14 @@ static __device__ __forceinline__ void consume_any(const A &a, const Frame (&fc)
 		consume<G, U, K, false, ORD, FEAT, A>(a, fc, vc, lane, p0, nseg);
 }
 
+#ifdef XCSUM_WAVE_STAMPS
+/* `make variant NAME=stamps DEFS=-DXCSUM_WAVE_STAMPS` only (tools/wave_tail.py,
+ * DESIGN.md 9.4): every wave's start and end on the 100 MHz constant clock,
+ * to see the persistent grid's tail.  Not in libxcsum.so. */
+constexpr uint32_t WAVE_STAMPS_MAX = 65536;
+static __device__ uint64_t g_wave_stamps[2 * WAVE_STAMPS_MAX];
+#endif
+
 /*
  * Persistent grid; segment s (G lanes) owns frames s, s + nseg, ... and
  * handles U of them per step.  Two-stage software pipeline written as a
@@ -400,6 +408,10 @@ static __device__ __forceinline__ void consume_any(const A &a, const Frame (&fc)
 template <int G, int U, int K, bool ORD, int FEAT, class A, int TL = 0>
 static __device__ __forceinline__ void csum_loop(const A &a)
 {
+#ifdef XCSUM_WAVE_STAMPS
+	const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
+	__builtin_amdgcn_s_waitcnt(0xC07F);
+#endif
 	const uint32_t lane = threadIdx.x & (G - 1);
 	uint32_t seg = (blockIdx.x * 256u + threadIdx.x) / G;
 	const uint32_t nseg = gridDim.x * (256u / G);
@@ -453,6 +465,15 @@ static __device__ __forceinline__ void csum_loop(const A &a)
 		issue<G, U, K, TL>(fa, lane, va);
 		consume_any<G, U, K, ORD, FEAT, A>(a, fb, vb, lane, p0 + step, nseg);
 	}
+#ifdef XCSUM_WAVE_STAMPS
+	const uint64_t t_end = __builtin_amdgcn_s_memrealtime();
+	__builtin_amdgcn_s_waitcnt(0xC07F);
+	const uint32_t wv = (blockIdx.x * 256u + threadIdx.x) >> 6;
+	if ((threadIdx.x & 63u) == 0u && wv < WAVE_STAMPS_MAX) {
+		g_wave_stamps[2 * wv] = t_start;
+		g_wave_stamps[2 * wv + 1] = t_end;
+	}
+#endif
 }
 
 /* The identity order gets its own copy of the loop, so descriptor-order

@@ -717,3 +717,94 @@ extern "C" int probe_slot_write(void *umem, uint32_t n, int desc, int msgs, cons
 			   (uint8_t *)umem, n, desc, msgs, (const u32x4 *)m, (u32x4 *)d);
 	return hipGetLastError() == hipSuccess ? 0 : -1;
 }
+
+/* Frame-span probe (round 6): the loads the checksum kernel
+ * must make on a sparse batch -- per frame its 16-byte descriptor and every
+ * 16-byte chunk of [addr & ~15, addr + len) -- and nothing else, the frames
+ * taken in the kernel's visiting order for sparse batches (2^rlog regions of
+ * 2^tlog-frame tiles, csrc/xcsum_internal.h order_regions / frame_of).  One
+ * flat grid-stride stream over (logical frame, chunk) pairs, `span16` =
+ * the widest frame's chunks; shorter frames mask their tail.  The same-run
+ * ceiling of xudp's slot layout (one ~1.5 KB frame per 4096-byte chunk): the
+ * contiguous stream read of the whole buffer moves the gaps too, and a read
+ * of the lines alone in address order is not the kernel's order. */
+struct probe_order {
+	uint32_t nlog, rshift, tshift, q;
+};
+
+static __device__ __forceinline__ uint32_t probe_frame_of(const probe_order &o, uint32_t p)
+{
+	if (o.rshift == 0)
+		return p;
+	const uint32_t t = p >> o.tshift;
+	const uint32_t r = t & ((1u << o.rshift) - 1u);
+	return ((r * o.q + (t >> o.rshift)) << o.tshift) | (p & ((1u << o.tshift) - 1u));
+}
+
+/* UNROLL (logical frame, chunk) pairs per thread per pass: their
+ * descriptor loads first, then their chunk loads, so a thread keeps UNROLL
+ * independent chunk loads in flight (the checksum kernel keeps two steps of
+ * its frames in flight the same way); 32-bit indices */
+template <bool NT, int UNROLL>
+__global__ void __launch_bounds__(256) frame_spans(const uint8_t *umem, const probe_desc *desc,
+						   uint32_t n, probe_order o, uint32_t span16,
+						   uint32_t *out)
+{
+	const uint32_t total = o.nlog * span16;
+	const uint32_t stride = gridDim.x * 256u;
+	uint32_t acc = 0;
+	for (uint32_t i0 = blockIdx.x * 256u + threadIdx.x; i0 < total; i0 += UNROLL * stride) {
+		u32x4 d[UNROLL];
+		uint32_t w[UNROLL];
+		bool ok[UNROLL];
+#pragma unroll
+		for (int u = 0; u < UNROLL; u++) {
+			const uint32_t i = i0 + u * stride;
+			const uint32_t k = i / span16;
+			w[u] = i - k * span16;
+			const uint32_t f = probe_frame_of(o, k);
+			ok[u] = i < total && f < n;
+			d[u] = *((gu32x4 *)(desc + (ok[u] ? f : 0u)));   /* the kernel reads it per frame */
+		}
+		u32x4 v[UNROLL];
+#pragma unroll
+		for (int u = 0; u < UNROLL; u++) {
+			const uint64_t addr = ((uint64_t)d[u].y << 32) | d[u].x;
+			const uint64_t lo = addr & ~(uint64_t)15;
+			const bool in = ok[u] && lo + 16ull * w[u] < addr + d[u].z;
+			const gu32x4 *c = (gu32x4 *)(umem + (in ? lo + 16ull * w[u] : lo));
+			v[u] = NT ? __builtin_nontemporal_load(c) : *c;
+			if (!in)
+				v[u] = u32x4{0u, 0u, 0u, 0u};
+		}
+#pragma unroll
+		for (int u = 0; u < UNROLL; u++)
+			acc += v[u].x ^ v[u].y ^ v[u].z ^ v[u].w;
+	}
+	if (acc == 0x9e3779b9u)
+		out[blockIdx.x] = acc;
+}
+
+extern "C" int probe_frame_spans(const void *umem, const void *desc, uint32_t n, int rlog,
+				 int tlog, uint32_t span16, int nt, uint32_t *out, int blocks,
+				 void *stream)
+{
+	if (!n || !span16 || blocks <= 0 || rlog < 0 || tlog < 0 || rlog + tlog > 30 ||
+	    (uint64_t)n * span16 * 2 >= (1ull << 32))
+		return -1;
+	probe_order o{n, 0u, 0u, 0u};
+	if (rlog > 0 && n >= (1u << (rlog + tlog))) {   /* order_regions */
+		const uint32_t ntiles = (n + (1u << tlog) - 1) >> tlog;
+		const uint32_t q = (ntiles + (1u << rlog) - 1) >> rlog;
+		o = probe_order{(q << rlog) << tlog, (uint32_t)rlog, (uint32_t)tlog, q};
+	}
+	auto *u = (const uint8_t *)umem;
+	auto *d = (const probe_desc *)desc;
+	if (nt)
+		hipLaunchKernelGGL((frame_spans<true, 8>), dim3(blocks), dim3(256), 0,
+				   (hipStream_t)stream, u, d, n, o, span16, out);
+	else
+		hipLaunchKernelGGL((frame_spans<false, 8>), dim3(blocks), dim3(256), 0,
+				   (hipStream_t)stream, u, d, n, o, span16, out);
+	return hipGetLastError() == hipSuccess ? 0 : -1;
+}

@@ -187,6 +187,44 @@ PY
     done ;;
   profile)
     bash tools/profile_round.sh $t/profile || exit $? ;;
+  tail)
+    # the persistent grid's tail: per-wave start/end stamps (the stamps
+    # variant, tools/wave_tail.py) on config 2, config 5 and two of its shards
+    XCSUM_LIB=$PWD/libxudp_amd/variants/stamps/libxcsum.so tools/gpu_run.sh $t/wave_tail 500 \
+      python -u tools/wave_tail.py --work c2 c5 c5s0/8 c5s7/8 || exit $? ;;
+  shards)
+    # config 5 whole, and shards 0 and 7 of 8 timed alone (bench.py --shard)
+    for a in "--config 5" "--config 5 --shard 0/8" "--config 5 --shard 7/8"; do
+      n=$(echo "$a" | sed 's/--config 5//; s/ --shard /_shard/; s/\//of/')
+      tools/gpu_run.sh "$t/bench_c5$n" 400 \
+        python -u bench.py --steps 50 --warmup 5 --no-cpu-baseline $a || exit $?
+    done ;;
+  sweep5)
+    # config 5 geometry x blocks-per-CU sweep on the current kernels (the
+    # sweep variant carries the extra geometries, -DXCSUM_SWEEP_GEOMS)
+    XCSUM_LIB=$PWD/libxudp_amd/variants/sweep/libxcsum.so tools/gpu_run.sh $t/sweep5 600 \
+      python -u tools/sweep.py --config 5 --rounds 3 --launches 10 \
+      --geoms "${SWEEP_GEOMS:-64,1,9;64,2,9;64,1,12;64,2,6;32,2,9;64,3,6;32,1,6;16,1,12}" \
+      --bpc "${SWEEP_BPC:-1,2,3,4}" --orders "-1,0;4,2;0,0" || exit $? ;;
+  slots)
+    # xudp's 4096-byte slots with the like-for-like span probe
+    tools/gpu_run.sh $t/bench_c2u 300 python -u bench.py --steps 100 --warmup 5 \
+      --no-cpu-baseline --layout umem || exit $? ;;
+  host_ab)
+    # host batches: this library against round 5's (libxudp_amd/variants/r05,
+    # built from git), wide and one-CPU affinity (the staging budget)
+    cpu0=$(python3 -c "import os; print(min(os.sched_getaffinity(0)))")
+    for lib in new r05; do
+      L=$PWD/libxudp_amd/libxcsum.so
+      [ $lib = r05 ] && L=$PWD/libxudp_amd/variants/r05/libxcsum.so
+      for a in "--config 2 --layout umem" "--config 3 --layout umem" "--config 2 --iphdr-only"; do
+        n=$(echo $a | sed 's/--config /c/; s/ --layout umem/u/; s/ --iphdr-only/_iphdr/')
+        XCSUM_LIB=$L tools/gpu_run.sh $t/host_${lib}_$n 300 python -u tools/bench_e2e.py $a \
+          --reps 5 || exit $?
+        XCSUM_LIB=$L tools/gpu_run.sh $t/host_${lib}_${n}_cpu1 300 taskset -c $cpu0 \
+          python -u tools/bench_e2e.py $a --reps 5 || exit $?
+      done
+    done ;;
   *)
     echo "unknown recipe $r"; exit 2 ;;
   esac
