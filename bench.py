@@ -584,57 +584,69 @@ def stream_ceiling(torch, dev, bufs, sptr):
 
 
 def span_ceiling(torch, dev, bufs, d_desc, desc, sptr, real):
-    """Like-for-like ceiling of a sparse layout (xudp's 4096-byte slots,
-    --layout umem): tools/libhbmprobe.so's probe_frame_spans
-    makes exactly the loads the checksum kernel must make -- per frame its
-    descriptor and every 16-byte chunk of [addr & ~15, addr + len) -- with no
-    arithmetic, the frames visited in the kernel's sparse order (32 regions
-    of 16-frame tiles) and, as a second leg, in descriptor order; plain and
-    nontemporal loads; the fastest leg counts.  Rates over the same real
-    bytes as roofline.real_achieved.  None where the probe is missing."""
+    """Like-for-like ceiling of the frame-per-wave access pattern (VERDICT r5
+    #3, #6): tools/libhbmprobe.so's probe_frame_spans2 reads what the
+    checksum kernel must fetch -- per frame its descriptor and the 128-byte
+    lines (or the 16-byte chunks) around its span -- with no arithmetic, one
+    wave per frame (64 x 16 B per load instruction), 4 MTU or 2 jumbo frames
+    per wave in flight, the frames in one of the kernel's visiting orders (32
+    regions of 16-frame tiles: sparse; 8 of 16: MTU; 16 of 4: mixed sizes;
+    descriptor order), plain or nontemporal loads; the fastest leg counts.
+    For xudp's slots (--layout umem) and for mixed sizes (config 5) the
+    contiguous stream read of the whole buffer is not that pattern.  Rates
+    over the same real bytes as roofline.real_achieved.  None where the probe
+    is missing or a frame's span exceeds 10 KiB."""
     path = os.path.join(ROOT, "tools", "libhbmprobe.so")
     if not os.path.exists(path) or not len(desc):
         return None
     L = ctypes.CDLL(path)
-    fn = getattr(L, "probe_frame_spans", None)
+    fn = getattr(L, "probe_frame_spans2", None)
     if fn is None:
         return None
     fn.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_int, ctypes.c_int,
-                   ctypes.c_uint32, ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]
+                   ctypes.c_uint32, ctypes.c_int, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_int,
+                   ctypes.c_void_p]
     a = desc["addr"].astype(np.int64)
-    span16 = int((((a + desc["len"].astype(np.int64) + 15) >> 4) - (a >> 4)).max())
-    # host-side bounds: every chunk the probe may load lies inside the buffer
-    assert int(((a + desc["len"].astype(np.int64) + 15) & ~15).max()) <= bufs[0].numel()
+    end = a + desc["len"].astype(np.int64)
+    max_span = int((((end + 127) & ~127) - (a & ~127)).max())
+    if max_span > 10240:
+        return None
+    # host-side bounds: every line the probe may load lies inside the buffer
+    assert int(((end + 127) & ~127).max()) <= bufs[0].numel()
     cus = torch.cuda.get_device_properties(dev).multi_processor_count
-    blocks = cus * 8
+    blocks = cus * (8 if max_span <= 2048 else 4)
     scratch = torch.empty(blocks, dtype=torch.int32, device=dev)
-    per = max(10, len(bufs))
+    per = max(10, len(bufs)) if max_span <= 2048 else 4
     s = torch.cuda.current_stream(dev)
     legs = {}
-    for name, (rlog, tlog) in (("regions_5_4", (5, 4)), ("descriptor_order", (0, 0))):
-        for nt in (0, 1):
-            ts = []
-            for r in range(6):
-                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                e0.record(s)
-                for k in range(per):
-                    if fn(bufs[k % len(bufs)].data_ptr(), d_desc.data_ptr(), len(desc), rlog, tlog,
-                          span16, nt, scratch.data_ptr(), blocks, sptr) != 0:
-                        return None
-                e1.record(s)
-                torch.cuda.synchronize(dev)
-                ts.append(e0.elapsed_time(e1) / per)
-            legs[f"{name}{'_nt' if nt else ''}"] = float(np.median(ts[1:]))
+    for rlog, tlog in ((5, 4), (3, 4), (4, 2), (0, 0)):
+        for line in (128, 16):
+            for nt in (0, 1):
+                ts = []
+                for r in range(6):
+                    e0 = torch.cuda.Event(enable_timing=True)
+                    e1 = torch.cuda.Event(enable_timing=True)
+                    e0.record(s)
+                    for k in range(per):
+                        if fn(bufs[k % len(bufs)].data_ptr(), d_desc.data_ptr(), len(desc), rlog,
+                              tlog, line, nt, max_span, scratch.data_ptr(), blocks, sptr) != 0:
+                            return None
+                    e1.record(s)
+                    torch.cuda.synchronize(dev)
+                    ts.append(e0.elapsed_time(e1) / per)
+                legs[f"order_{rlog}_{tlog}_line{line}{'_nt' if nt else ''}"] = \
+                    float(np.median(ts[1:]))
     best = min(legs, key=legs.get)
     t = legs[best]
     return {"ms": round(t, 4), "ms_by_leg": {k: round(v, 4) for k, v in legs.items()},
             "fastest": best, "GBps": round(real / (t * 1e-3) / 1e9, 1),
-            "what": f"tools/hbm_probe.hip probe_frame_spans: per frame the 16-byte descriptor and "
-                    f"the {span16} 16-byte chunks of its span, no arithmetic, in the kernel's "
-                    f"sparse order (32 regions of 16-frame tiles) or descriptor order, plain or "
-                    f"nontemporal loads; the fastest leg; rate over the same real bytes as "
+            "what": "tools/hbm_probe.hip probe_frame_spans2: per frame the 16-byte descriptor "
+                    "and the 128-byte lines (or 16-byte chunks) around its span, no arithmetic, "
+                    "one wave per frame, 4 MTU / 2 jumbo frames per wave in flight, in one of "
+                    "the kernel's visiting orders (regions R,T) or descriptor order, plain or "
+                    "nontemporal loads; the fastest leg; rate over the same real bytes as "
                     f"real_achieved; {per} back-to-back launches between two events, median "
-                    f"of 5"}
+                    "of 5"}
 
 
 def inplace_ceiling(torch, dev, bufs, desc, flags, family, sptr):
@@ -1101,8 +1113,10 @@ def main():
     ceiling = inplace = orders = hdr_probe = spans = None
     if rank == 0 and not args.no_ceiling:
         ceiling = stream_ceiling(torch, dev, bufs, sptr)
-        if args.layout == "umem" and not flags & (X.F_INPLACE | X.F_IPHDR_ONLY):
-            # xudp's slots: the loads the kernel must make, in its order
+        if (args.layout == "umem" or cfg["id"] == 5) and \
+                not flags & (X.F_INPLACE | X.F_IPHDR_ONLY):
+            # xudp's slots, mixed sizes: the loads the kernel must make, in
+            # its orders, one wave per frame
             spans = span_ceiling(torch, dev, bufs, d_desc, desc, sptr, real_bytes(desc, flags))
         if flags & X.F_IPHDR_ONLY:
             hdr_probe = header_ceiling(torch, dev, bufs, d_desc, count,

@@ -242,7 +242,14 @@ int xcsum_ctx_set_inplace(xcsum_ctx *ctx, int schedule);
  *   RESIDENT_INLINE  a = 0: resident requests carry their descriptors only
  *                    in the array (A/B of the inline lines);
  *   RESIDENT_LIMIT_CUT a = bytes: resident requests carry a limit this much
- *                    short (test hook for the workgroups' descriptor check).
+ *                    short (test hook for the workgroups' descriptor check);
+ *   CLAIM            a = the share of a batch's frames the checksum kernel
+ *                    schedules statically, in 64ths (64: all, the default),
+ *                    b = frames per claim in steps of a wave (0: 16): the
+ *                    rest is claimed from a device counter by the waves that
+ *                    are ahead (the claimed tail, geometries (64,1,9),
+ *                    (64,1,2), (16,2,6); A/B build only -- -XCSUM_ERR_INVAL
+ *                    from libxcsum.so for a < 64).
  * -XCSUM_ERR_INVAL for an unknown knob or a value not compiled in. */
 enum xcsum_tuning {
 	XCSUM_TUNE_IPHDR_FPT = 1,
@@ -255,6 +262,7 @@ enum xcsum_tuning {
 	XCSUM_TUNE_INPLACE_TL = 8,
 	XCSUM_TUNE_RESIDENT_INLINE = 9,
 	XCSUM_TUNE_RESIDENT_LIMIT_CUT = 10,
+	XCSUM_TUNE_CLAIM = 11,
 };
 int xcsum_ctx_set_tuning(xcsum_ctx *ctx, int knob, int a, int b, int c, int d);
 

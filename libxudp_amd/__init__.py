@@ -114,7 +114,7 @@ INPLACE_AUTO, INPLACE_FUSED, INPLACE_TWO_PASS = 0, 1, 2
 # xcsum_ctx_set_tuning knobs (enum xcsum_tuning)
 TUNE_IPHDR_FPT, TUNE_BUILD_HDR, TUNE_BUILD_GEOMETRY, TUNE_RX_GEOMETRY, TUNE_RX_ORDER = 1, 2, 3, 4, 5
 TUNE_GATHER_RATIO, TUNE_INPLACE_BLOCK, TUNE_INPLACE_TL = 6, 7, 8
-TUNE_RESIDENT_INLINE, TUNE_RESIDENT_LIMIT_CUT = 9, 10
+TUNE_RESIDENT_INLINE, TUNE_RESIDENT_LIMIT_CUT, TUNE_CLAIM = 9, 10, 11
 
 # device placement (include/xcsum.h)
 DEVICE_ENV, DEVICE_AUTO = -1, -2

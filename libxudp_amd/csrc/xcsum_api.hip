@@ -162,6 +162,8 @@ static void tuning_defaults(xcsum_ctx *c)
 	t.rx_rlog = -1;
 	t.rx_tlog = 0;
 	t.gather_ratio = 2;
+	t.claim_static_64 = 64;
+	t.claim_steps = 16;
 	c->inplace_block = 0;
 	c->inplace_tl = 1;
 }
@@ -221,6 +223,13 @@ extern "C" int xcsum_ctx_set_tuning(xcsum_ctx *c, int knob, int a, int b, int cc
 			return -XCSUM_ERR_INVAL;
 		c->res_limit_cut = (uint64_t)a;
 		return 0;
+	case XCSUM_TUNE_CLAIM:
+		/* the claimed-tail kernels are in the A/B build only */
+		if (a < 0 || a > 64 || b < 0 || b > 4096 || (a < 64 && !launch_csum_claim_f0))
+			return -XCSUM_ERR_INVAL;
+		t.claim_static_64 = (uint32_t)a;
+		t.claim_steps = b ? (uint32_t)b : 16u;
+		return 0;
 	default:
 		return -XCSUM_ERR_INVAL;
 	}
@@ -263,6 +272,10 @@ static void read_env_tuning(xcsum_ctx *c)
 		(void)xcsum_ctx_set_tuning(c, XCSUM_TUNE_RESIDENT_INLINE, atoi(e), 0, 0, 0);
 	if ((e = getenv("XCSUM_RESIDENT_LIFE_US")) && atoi(e) > 0)
 		c->res_life_us = (uint32_t)atoi(e);
+	a = 64;
+	b = 0;
+	if ((e = getenv("XCSUM_CLAIM")) && sscanf(e, "%d,%d", &a, &b) >= 1)
+		(void)xcsum_ctx_set_tuning(c, XCSUM_TUNE_CLAIM, a, b, 0, 0);
 }
 #endif
 
@@ -841,6 +854,8 @@ extern "C" void xcsum_ctx_destroy(xcsum_ctx *c)
 		(void)hipFree(c->d_rx_part);
 	if (c->d_inplace)
 		(void)hipFree(c->d_inplace);
+	if (c->d_claim)
+		(void)hipFree(c->d_claim);
 	if (c->inplace_done)
 		(void)hipEventDestroy(c->inplace_done);
 	delete c;
@@ -1093,7 +1108,17 @@ extern "C" int xcsum_batch_device(xcsum_ctx *c, uint8_t *d_umem, const struct xc
 		HIPCHK(launch_csum_inplace_tl(a, g, c->cus, (hipStream_t)stream));
 		return 0;
 	}
-	HIPCHK(launch_csum(a, g, c->cus, (hipStream_t)stream));
+	ClaimParams cp{nullptr, c->tune.claim_static_64, c->tune.claim_steps};
+	if (cp.static_64 < 64) {
+		/* the claimed tail: a counter pair of the context's ring, zero on
+		 * allocation and reset by the last wave of each launch */
+		if (!c->d_claim) {
+			HIPCHK(hipMalloc((void **)&c->d_claim, 2 * CLAIM_SLOTS * sizeof(uint32_t)));
+			HIPCHK(hipMemset(c->d_claim, 0, 2 * CLAIM_SLOTS * sizeof(uint32_t)));
+		}
+		cp.claim = c->d_claim + 2 * (c->claim_seq++ % CLAIM_SLOTS);
+	}
+	HIPCHK(launch_csum(a, g, c->cus, (hipStream_t)stream, &cp));
 	return 0;
 }
 

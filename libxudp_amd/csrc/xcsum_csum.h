@@ -522,6 +522,167 @@ static hipError_t launch_t(const CsumArgs &a, int cus, int bpc, hipStream_t s)
 	return hipGetLastError();
 }
 
+/* ---- claimed tail (xcsum_ctx_set_tuning XCSUM_TUNE_CLAIM, A/B) -----------
+ * csum_kernel's static schedule gives every segment the same number of
+ * frames; with mixed frame sizes (config 5) and unequal bandwidth between
+ * CUs the waves end at different times, and the last ones run alone
+ * (tools/wave_tail.py).  csum_kernel_claim runs the same pipeline over the
+ * first `from` logical frames statically, then every wave claims chunks of
+ * `chunk` logical frames from a device counter (one returning atomic per
+ * chunk, wave-uniform), so the waves that are ahead take the tail.  The
+ * counter pair lives in a ring of the context (claim[0] next offset,
+ * claim[1] waves done); the last wave to finish resets both, so the next
+ * launch that gets this slot finds them zero. */
+struct ClaimArgs {
+	CsumArgs a;
+	uint32_t *claim;
+	uint32_t from;                 /* multiple of the static step */
+	uint32_t chunk;                /* multiple of (64 / G) * U */
+};
+
+/* csum_loop's pipeline over the logical range of one segment: frames seg,
+ * seg + nseg, ... below limit (nseg = spacing of the U slots of a step) */
+template <int G, int U, int K, bool ORD, int FEAT>
+static __device__ __forceinline__ void csum_range(const CsumArgs &a, uint32_t seg, uint32_t nseg,
+						  uint32_t limit)
+{
+	const uint32_t lane = threadIdx.x & (G - 1);
+	const uint32_t step = nseg * U;
+	if (G == 64)
+		seg = __builtin_amdgcn_readfirstlane(seg);
+	auto has = [&](uint32_t q) { return q < limit && fidx<ORD>(a, q) < a.n; };
+	u32x4 d[U];
+	Frame fa[U];
+	u32x4 va[U][K];
+#pragma unroll
+	for (int u = 0; u < U; u++)
+		d[u] = load_desc<G == 64>(a, fidx<ORD>(a, seg + u * nseg));
+#pragma unroll
+	for (int u = 0; u < U; u++)
+		fa[u] = resolve<Grid<G, K>::DW, FEAT, CsumArgs>(a, d[u], has(seg + u * nseg));
+#pragma unroll
+	for (int u = 0; u < U; u++)
+		d[u] = load_desc<G == 64>(a, fidx<ORD>(a, seg + step + u * nseg));
+	__builtin_amdgcn_sched_barrier(0);
+	issue<G, U, K, 0>(fa, lane, va);
+	Frame fb[U];
+	u32x4 vb[U][K];
+	for (uint32_t p0 = seg; p0 < limit; p0 += 2 * step) {
+#pragma unroll
+		for (int u = 0; u < U; u++)
+			fb[u] = resolve<Grid<G, K>::DW, FEAT, CsumArgs>(a, d[u], has(p0 + step + u * nseg));
+#pragma unroll
+		for (int u = 0; u < U; u++)
+			d[u] = load_desc<G == 64>(a, fidx<ORD>(a, p0 + 2 * step + u * nseg));
+		__builtin_amdgcn_sched_barrier(0);
+		issue<G, U, K, 0>(fb, lane, vb);
+		consume_any<G, U, K, ORD, FEAT, CsumArgs>(a, fa, va, lane, p0, nseg);
+#pragma unroll
+		for (int u = 0; u < U; u++)
+			fa[u] = resolve<Grid<G, K>::DW, FEAT, CsumArgs>(a, d[u],
+								has(p0 + 2 * step + u * nseg));
+#pragma unroll
+		for (int u = 0; u < U; u++)
+			d[u] = load_desc<G == 64>(a, fidx<ORD>(a, p0 + 3 * step + u * nseg));
+		__builtin_amdgcn_sched_barrier(0);
+		issue<G, U, K, 0>(fa, lane, va);
+		consume_any<G, U, K, ORD, FEAT, CsumArgs>(a, fb, vb, lane, p0 + step, nseg);
+	}
+}
+
+template <int G, int U, int K, bool ORD, int FEAT>
+static __device__ __forceinline__ void claim_loop(const ClaimArgs &c, const CsumArgs &a)
+{
+#ifdef XCSUM_WAVE_STAMPS
+	const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
+	__builtin_amdgcn_s_waitcnt(0xC07F);
+#endif
+	constexpr uint32_t W = 64u / G;      /* segments per wave */
+	const uint32_t wave = __builtin_amdgcn_readfirstlane((blockIdx.x * 256u + threadIdx.x) >> 6);
+	const uint32_t j = (threadIdx.x & 63u) / G;
+	const uint32_t nwaves = gridDim.x * 4u;
+	const uint32_t limit = ORD ? a.ord.nlog : a.n;
+	/* the static part: csum_kernel's schedule below `from` */
+	csum_range<G, U, K, ORD, FEAT>(a, wave * W + j, nwaves * W, c.from < limit ? c.from : limit);
+	/* the claimed part: chunks of consecutive logical frames, the wave's
+	 * segment j taking frames base + j + u * W + i * W * U */
+	for (;;) {
+		uint32_t got = 0;
+		if ((threadIdx.x & 63u) == 0u)
+			got = atomicAdd(&c.claim[0], c.chunk);
+		const uint32_t base = __builtin_amdgcn_readfirstlane(got) + c.from;
+		if (base >= limit || base < c.from)
+			break;
+		const uint32_t end = limit - base > c.chunk ? base + c.chunk : limit;
+		csum_range<G, U, K, ORD, FEAT>(a, base + j, W, end);
+	}
+	/* the last wave out resets the slot for the launch that reuses it */
+	if ((threadIdx.x & 63u) == 0u && atomicAdd(&c.claim[1], 1u) == nwaves - 1u) {
+		atomicExch(&c.claim[0], 0u);
+		atomicExch(&c.claim[1], 0u);
+	}
+#ifdef XCSUM_WAVE_STAMPS
+	const uint64_t t_end = __builtin_amdgcn_s_memrealtime();
+	__builtin_amdgcn_s_waitcnt(0xC07F);
+	const uint32_t wv = (blockIdx.x * 256u + threadIdx.x) >> 6;
+	if ((threadIdx.x & 63u) == 0u && wv < WAVE_STAMPS_MAX) {
+		g_wave_stamps[2 * wv] = t_start;
+		g_wave_stamps[2 * wv + 1] = t_end;
+	}
+#endif
+}
+
+template <int G, int U, int K, int FEAT>
+__global__ void __launch_bounds__(256) csum_kernel_claim(ClaimArgs c)
+{
+	CsumArgs a = c.a;
+	resolve_order(a);
+	if (a.ord.rshift == 0)
+		claim_loop<G, U, K, false, FEAT>(c, a);
+	else
+		claim_loop<G, U, K, true, FEAT>(c, a);
+}
+
+/* static_64: the static share in 64ths of the logical range; chunk_steps:
+ * wave steps per claim */
+template <int G, int U, int K, int FEAT>
+static hipError_t launch_claim_t(const CsumArgs &a, int cus, int bpc, uint32_t *claim,
+				 uint32_t static_64, uint32_t chunk_steps, hipStream_t s)
+{
+	static std::atomic<int> occ_cache[OCC_MAX_DEVICES];
+	const int occ = occupancy_cached(occ_cache, [] {
+		int nb = 0;
+		if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, csum_kernel_claim<G, U, K, FEAT>,
+								 256, 0) != hipSuccess || nb <= 0)
+			nb = 4;
+		return nb;
+	});
+	int per_cu = (bpc > 0 && bpc < occ) ? bpc : occ;
+	uint64_t segs = ((uint64_t)a.ord.nlog + U - 1) / U;
+	uint64_t blocks = (segs * G + 255) / 256;
+	uint64_t cap = (uint64_t)cus * per_cu;
+	if (blocks > cap)
+		blocks = cap;
+	if (blocks == 0)
+		blocks = 1;
+	ClaimArgs c;
+	c.a = a;
+	c.claim = claim;
+	/* the static step of the grid: every segment's U frames */
+	const uint64_t step = blocks * (256u / G) * U;
+	const uint64_t nlog = a.ord.nlog;   /* >= n; the dense order may differ, which
+					       only moves the split point */
+	c.from = (uint32_t)((nlog * static_64 / 64u) / step * step);
+	c.chunk = (uint32_t)(chunk_steps * (64u / G) * U);
+	(void)hipGetLastError();
+	hipLaunchKernelGGL((csum_kernel_claim<G, U, K, FEAT>), dim3((unsigned)blocks), dim3(256), 0,
+			   s, c);
+	return hipGetLastError();
+}
+
+/* the geometries with a claimed-tail kernel */
+#define XCSUM_CLAIM_GEOMETRIES(X) X(64, 1, 9) X(64, 1, 2) X(16, 2, 6)
+
 #define XCSUM_GEOMETRIES(X) \
 	X(64, 1, 2) X(64, 1, 9) X(32, 1, 3) X(32, 1, 6) \
 	X(16, 1, 2) X(16, 1, 3) X(16, 1, 6) X(16, 2, 6) X(16, 1, 12) \

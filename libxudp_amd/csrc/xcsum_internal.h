@@ -168,6 +168,8 @@ struct Tuning {
 	int rx_rlog, rx_tlog;          /* receive visiting order: rlog -1 automatic,
 					  0 descriptor order, else 2^R regions of 2^T tiles */
 	uint32_t gather_ratio;         /* host path: gather when the span > ratio x bytes */
+	uint32_t claim_static_64;      /* claimed tail: static share in 64ths (0: off) */
+	uint32_t claim_steps;          /* claimed tail: wave steps per claim */
 };
 
 hipError_t launch_build(const BuildArgs &a, uint32_t len_hint, int cus, const Tuning &t,
@@ -184,6 +186,8 @@ struct RxArgs {
 	Order ord;                     /* visiting order (set by launch_rx) */
 	Order dense;                   /* ord.sparse_only: a dense batch's order */
 };
+
+constexpr uint32_t CLAIM_SLOTS = 256;
 
 /* per-block delivered counts of one receive launch: >= CUs x blocks per CU */
 constexpr uint32_t RX_PART_MAX = 4096;
@@ -216,7 +220,24 @@ int batch_host_impl(struct xcsum_ctx *c, uint8_t *h_umem, const struct xcsum_des
 		    uint32_t n, uint16_t *h_out, uint16_t *h_out_ip, uint32_t mode, uint32_t flags,
 		    bool gather = false);
 bool geometry_supported(Geometry g);
-hipError_t launch_csum(const CsumArgs &a, Geometry g, int cus, hipStream_t s);
+/* the claimed-tail schedule of csum_kernel (XCSUM_TUNE_CLAIM, xcsum_csum.h):
+ * a counter pair of the context's ring, the static share in 64ths, wave
+ * steps per claim */
+struct ClaimParams {
+	uint32_t *claim;
+	uint32_t static_64, chunk_steps;
+};
+hipError_t launch_csum(const CsumArgs &a, Geometry g, int cus, hipStream_t s,
+		       const ClaimParams *cp = nullptr);
+/* A/B only (csrc/variants/xcsum_claim.hip, `make variant`; null in
+ * libxcsum.so): -> hipErrorNotSupported for a geometry without a
+ * claimed-tail kernel */
+XCSUM_VARIANT_HOOK hipError_t launch_csum_claim_f0(const CsumArgs &a, Geometry g, int cus,
+						   const ClaimParams &cp, hipStream_t s);
+XCSUM_VARIANT_HOOK hipError_t launch_csum_claim_f1(const CsumArgs &a, Geometry g, int cus,
+						   const ClaimParams &cp, hipStream_t s);
+XCSUM_VARIANT_HOOK hipError_t launch_csum_claim_f2(const CsumArgs &a, Geometry g, int cus,
+						   const ClaimParams &cp, hipStream_t s);
 /* csum_kernel per feature set (xcsum_csum_f{0,1,2}.hip): plain, + VERIFY, + IPHDR */
 hipError_t launch_csum_f0(const CsumArgs &a, Geometry g, int cus, hipStream_t s);
 hipError_t launch_csum_f1(const CsumArgs &a, Geometry g, int cus, hipStream_t s);
@@ -247,6 +268,8 @@ struct StagePool;   /* xcsum_stage.h: the context's host copy threads */
 struct Ctx {
 	int device;
 	Tuning tune;                   /* xcsum_ctx_set_tuning */
+	uint32_t *d_claim;             /* claimed tail: CLAIM_SLOTS counter pairs (lazy) */
+	uint32_t claim_seq;            /* next slot */
 	StagePool *stage_pool;         /* host copies split over threads (lazy threads) */
 	int cus;
 	int max_blocks;

@@ -331,10 +331,19 @@ bool geometry_supported(Geometry g)
 	return false;
 }
 
-hipError_t launch_csum(const CsumArgs &a, Geometry g, int cus, hipStream_t s)
+hipError_t launch_csum(const CsumArgs &a, Geometry g, int cus, hipStream_t s, const ClaimParams *cp)
 {
 	if (a.n == 0)
 		return hipSuccess;
+	/* the claimed-tail schedule, where the geometry has it (A/B builds
+	 * only: csrc/variants/xcsum_claim.hip) */
+	if (cp && cp->claim && cp->static_64 < 64 && g.U > 0 && launch_csum_claim_f0) {
+		const hipError_t e = (a.flags & XCSUM_F_IPHDR)    ? launch_csum_claim_f2(a, g, cus, *cp, s)
+				     : (a.flags & XCSUM_F_VERIFY) ? launch_csum_claim_f1(a, g, cus, *cp, s)
+								  : launch_csum_claim_f0(a, g, cus, *cp, s);
+		if (e != hipErrorNotSupported)
+			return e;
+	}
 	/* stream kernel: G = 64 lanes per 64 frames, U = 0, K = KiB of stage */
 	if (g.G == 64 && g.U == 0) {
 		if (g.K == 4) return launch_stream_t<4>(a, cus, g.B, s);

@@ -240,6 +240,7 @@ def test_constants_match_header():
         "XCSUM_TUNE_INPLACE_TL": X.TUNE_INPLACE_TL,
         "XCSUM_TUNE_RESIDENT_INLINE": X.TUNE_RESIDENT_INLINE,
         "XCSUM_TUNE_RESIDENT_LIMIT_CUT": X.TUNE_RESIDENT_LIMIT_CUT,
+        "XCSUM_TUNE_CLAIM": X.TUNE_CLAIM,
         "XCSUM_DEVICE_ENV": X.DEVICE_ENV, "XCSUM_DEVICE_AUTO": X.DEVICE_AUTO,
         "XCSUM_DEVICE_GROUP(7)": X.DEVICE_GROUP(7),
     }

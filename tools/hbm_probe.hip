@@ -718,16 +718,17 @@ extern "C" int probe_slot_write(void *umem, uint32_t n, int desc, int msgs, cons
 	return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
-/* Frame-span probe (round 6): the loads the checksum kernel
- * must make on a sparse batch -- per frame its 16-byte descriptor and every
- * 16-byte chunk of [addr & ~15, addr + len) -- and nothing else, the frames
- * taken in the kernel's visiting order for sparse batches (2^rlog regions of
- * 2^tlog-frame tiles, csrc/xcsum_internal.h order_regions / frame_of).  One
- * flat grid-stride stream over (logical frame, chunk) pairs, `span16` =
- * the widest frame's chunks; shorter frames mask their tail.  The same-run
- * ceiling of xudp's slot layout (one ~1.5 KB frame per 4096-byte chunk): the
- * contiguous stream read of the whole buffer moves the gaps too, and a read
- * of the lines alone in address order is not the kernel's order. */
+/* Frame-line probe (round 6): the bytes the checksum kernel
+ * must fetch on a sparse batch -- per frame its 16-byte descriptor and the
+ * `line`-aligned span around [addr, addr + len) (line = 128: the request
+ * size of a scattered read, profiles/r05/iphdr/r05j_line_probe.txt; 16: the
+ * kernel's own chunks) -- read as a stream, with no arithmetic: one wave per
+ * frame at a time (64 x 16 B = 1 KiB per load instruction, coalesced), F
+ * frames per wave in flight, the frames taken in the kernel's visiting order
+ * for sparse batches (2^rlog regions of 2^tlog-frame tiles,
+ * csrc/xcsum_internal.h order_regions / frame_of).  The same-run ceiling of
+ * xudp's slot layout (one ~1.5 KB frame per 4096-byte chunk): the contiguous
+ * stream read of the whole buffer moves the gaps too. */
 struct probe_order {
 	uint32_t nlog, rshift, tshift, q;
 };
@@ -741,56 +742,57 @@ static __device__ __forceinline__ uint32_t probe_frame_of(const probe_order &o, 
 	return ((r * o.q + (t >> o.rshift)) << o.tshift) | (p & ((1u << o.tshift) - 1u));
 }
 
-/* UNROLL (logical frame, chunk) pairs per thread per pass: their
- * descriptor loads first, then their chunk loads, so a thread keeps UNROLL
- * independent chunk loads in flight (the checksum kernel keeps two steps of
- * its frames in flight the same way); 32-bit indices */
-template <bool NT, int UNROLL>
-__global__ void __launch_bounds__(256) frame_spans(const uint8_t *umem, const probe_desc *desc,
-						   uint32_t n, probe_order o, uint32_t span16,
+/* MAXI: load instructions per frame (64 lanes x 16 B each) */
+template <bool NT, int F, int MAXI>
+__global__ void __launch_bounds__(256) frame_lines(const uint8_t *umem, const probe_desc *desc,
+						   uint32_t n, probe_order o, uint32_t line,
 						   uint32_t *out)
 {
-	const uint32_t total = o.nlog * span16;
-	const uint32_t stride = gridDim.x * 256u;
+	const uint32_t lane = threadIdx.x & 63u;
+	const uint32_t wave = __builtin_amdgcn_readfirstlane((blockIdx.x * 256u + threadIdx.x) >> 6);
+	const uint32_t nwaves = gridDim.x * 4u;
 	uint32_t acc = 0;
-	for (uint32_t i0 = blockIdx.x * 256u + threadIdx.x; i0 < total; i0 += UNROLL * stride) {
-		u32x4 d[UNROLL];
-		uint32_t w[UNROLL];
-		bool ok[UNROLL];
+	for (uint32_t k0 = wave * F; k0 < o.nlog; k0 += nwaves * F) {
+		u32x4 d[F];
 #pragma unroll
-		for (int u = 0; u < UNROLL; u++) {
-			const uint32_t i = i0 + u * stride;
-			const uint32_t k = i / span16;
-			w[u] = i - k * span16;
-			const uint32_t f = probe_frame_of(o, k);
-			ok[u] = i < total && f < n;
-			d[u] = *((gu32x4 *)(desc + (ok[u] ? f : 0u)));   /* the kernel reads it per frame */
+		for (int f = 0; f < F; f++) {
+			const uint32_t fr = probe_frame_of(o, k0 + f);
+			d[f] = *((gu32x4 *)(desc + (k0 + f < o.nlog && fr < n ? fr : 0u)));
 		}
-		u32x4 v[UNROLL];
+		u32x4 v[F][MAXI];
 #pragma unroll
-		for (int u = 0; u < UNROLL; u++) {
-			const uint64_t addr = ((uint64_t)d[u].y << 32) | d[u].x;
-			const uint64_t lo = addr & ~(uint64_t)15;
-			const bool in = ok[u] && lo + 16ull * w[u] < addr + d[u].z;
-			const gu32x4 *c = (gu32x4 *)(umem + (in ? lo + 16ull * w[u] : lo));
-			v[u] = NT ? __builtin_nontemporal_load(c) : *c;
-			if (!in)
-				v[u] = u32x4{0u, 0u, 0u, 0u};
+		for (int f = 0; f < F; f++) {
+			const uint32_t fr = probe_frame_of(o, k0 + f);
+			const bool ok = k0 + f < o.nlog && fr < n;
+			const uint64_t addr = ((uint64_t)d[f].y << 32) | d[f].x;
+			const uint64_t lo = addr & ~(uint64_t)(line - 1);
+			const uint64_t hi = (addr + d[f].z + line - 1) & ~(uint64_t)(line - 1);
+#pragma unroll
+			for (int j = 0; j < MAXI; j++) {
+				const uint64_t at = lo + 16ull * (lane + 64u * j);
+				const bool in = ok && at < hi;
+				const gu32x4 *c = (gu32x4 *)(umem + (in ? at : lo));
+				v[f][j] = in ? (NT ? __builtin_nontemporal_load(c) : *c) : u32x4{0u, 0u, 0u, 0u};
+			}
 		}
 #pragma unroll
-		for (int u = 0; u < UNROLL; u++)
-			acc += v[u].x ^ v[u].y ^ v[u].z ^ v[u].w;
+		for (int f = 0; f < F; f++)
+#pragma unroll
+			for (int j = 0; j < MAXI; j++)
+				acc += v[f][j].x ^ v[f][j].y ^ v[f][j].z ^ v[f][j].w;
 	}
 	if (acc == 0x9e3779b9u)
 		out[blockIdx.x] = acc;
 }
 
-extern "C" int probe_frame_spans(const void *umem, const void *desc, uint32_t n, int rlog,
-				 int tlog, uint32_t span16, int nt, uint32_t *out, int blocks,
-				 void *stream)
+/* line 16 or 128; every frame's span must fit 2 KiB (MTU frames, 4 frames
+ * per wave in flight) or 10 KiB (jumbo frames, 2 in flight) */
+extern "C" int probe_frame_spans2(const void *umem, const void *desc, uint32_t n, int rlog,
+				  int tlog, uint32_t line, int nt, uint32_t max_span,
+				  uint32_t *out, int blocks, void *stream)
 {
-	if (!n || !span16 || blocks <= 0 || rlog < 0 || tlog < 0 || rlog + tlog > 30 ||
-	    (uint64_t)n * span16 * 2 >= (1ull << 32))
+	if (!n || (line != 16 && line != 128) || blocks <= 0 || rlog < 0 || tlog < 0 ||
+	    rlog + tlog > 30 || max_span > 10240)
 		return -1;
 	probe_order o{n, 0u, 0u, 0u};
 	if (rlog > 0 && n >= (1u << (rlog + tlog))) {   /* order_regions */
@@ -800,11 +802,14 @@ extern "C" int probe_frame_spans(const void *umem, const void *desc, uint32_t n,
 	}
 	auto *u = (const uint8_t *)umem;
 	auto *d = (const probe_desc *)desc;
-	if (nt)
-		hipLaunchKernelGGL((frame_spans<true, 8>), dim3(blocks), dim3(256), 0,
-				   (hipStream_t)stream, u, d, n, o, span16, out);
-	else
-		hipLaunchKernelGGL((frame_spans<false, 8>), dim3(blocks), dim3(256), 0,
-				   (hipStream_t)stream, u, d, n, o, span16, out);
+	hipStream_t st = (hipStream_t)stream;
+#define L(NT_, F_, M_) hipLaunchKernelGGL((frame_lines<NT_, F_, M_>), dim3(blocks), dim3(256), 0, \
+					   st, u, d, n, o, line, out)
+	if (max_span <= 2048) {
+		if (nt) L(true, 4, 2); else L(false, 4, 2);
+	} else {
+		if (nt) L(true, 2, 10); else L(false, 2, 10);
+	}
+#undef L
 	return hipGetLastError() == hipSuccess ? 0 : -1;
 }

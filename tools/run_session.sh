@@ -205,7 +205,24 @@ PY
     XCSUM_LIB=$PWD/libxudp_amd/variants/sweep/libxcsum.so tools/gpu_run.sh $t/sweep5 600 \
       python -u tools/sweep.py --config 5 --rounds 3 --launches 10 \
       --geoms "${SWEEP_GEOMS:-64,1,9;64,2,9;64,1,12;64,2,6;32,2,9;64,3,6;32,1,6;16,1,12}" \
-      --bpc "${SWEEP_BPC:-1,2,3,4}" --orders "-1,0;4,2;0,0" || exit $? ;;
+      --bpc "${SWEEP_BPC:-1,2,3,4}" --orders="-1,0;4,2;0,0" || exit $? ;;
+  claim)
+    # the claimed tail (XCSUM_TUNE_CLAIM) against the static schedule: config
+    # 5 whole and one shard, config 2; then the wave stamps with a claim setting
+    C="${CLAIMS:-64,0;60,16;56,16;56,4;48,16;48,64;32,16}"
+    tools/gpu_run.sh $t/claim_c5 600 python -u tools/sweep.py --config 5 --rounds 3 \
+      --launches 10 --geoms auto --claims "$C" || exit $?
+    tools/gpu_run.sh $t/claim_c5s7 400 python -u tools/sweep.py --config 5 --shard 7/8 \
+      --rounds 3 --launches 20 --geoms auto --claims "$C" || exit $?
+    tools/gpu_run.sh $t/claim_c2 400 python -u tools/sweep.py --config 2 --rounds 3 \
+      --launches 50 --geoms auto --claims "$C" || exit $?
+    XCSUM_LIB=$PWD/libxudp_amd/variants/stamps/libxcsum.so tools/gpu_run.sh $t/wave_tail_claim \
+      500 python -u tools/wave_tail.py --work c2 c5 c5s7/8 --claim "${TAIL_CLAIM:-56,16}" \
+      || exit $? ;;
+  claimtest)
+    # the claimed-tail A/B kernels live in the variant builds only
+    XCSUM_LIB=$PWD/libxudp_amd/variants/sweep/libxcsum.so tools/gpu_run.sh $t/pytest_claim 600 \
+      $P tests/test_gpu_claim.py || exit $? ;;
   slots)
     # xudp's 4096-byte slots with the like-for-like span probe
     tools/gpu_run.sh $t/bench_c2u 300 python -u bench.py --steps 100 --warmup 5 \

@@ -31,6 +31,10 @@ def main():
     ap.add_argument("--orders", default="-1,0",
                     help="visiting orders to try, 'R,T;R,T' (log2 regions, log2 tile frames; "
                          "-1,0 = automatic)")
+    ap.add_argument("--claims", default="64,0",
+                    help="claimed-tail settings to try, 'S,C;S,C' (XCSUM_TUNE_CLAIM: static "
+                         "share in 64ths, wave steps per claim; 64 = static only)")
+    ap.add_argument("--shard", default="", help="r/N: time shard r of N of a sharded config")
     ap.add_argument("--layout", default="packed", choices=["packed", "umem"])
     ap.add_argument("--flags", default="", help="comma list of inplace,iphdr,verify,rfc")
     ap.add_argument("--payload", default="", help="MIN,MAX payload bytes instead of the config's")
@@ -44,7 +48,8 @@ def main():
         cfg["pmin"], cfg["pmax"] = (int(v) for v in args.payload.split(","))
     eng = X.Engine(0)
     s = torch.cuda.current_stream(dev)
-    desc, d_desc, bufs, out, first, count = bench.build_batch(cfg, 0, 1, torch, dev, eng,
+    sr, sn = bench.parse_shard(args.shard) or (0, 1)
+    desc, d_desc, bufs, out, first, count = bench.build_batch(cfg, sr, sn, torch, dev, eng,
                                                               s.cuda_stream)
     alg = X.alg_bytes(desc, cfg["family"])
     mode = cfg["mode"]
@@ -57,13 +62,15 @@ def main():
     len_hint = int(desc["len"].mean()) if len(desc) else 0
     bpcs = [int(b) for b in args.bpc.split(",")]
     orders = [tuple(int(v) for v in o.split(",")) for o in args.orders.split(";")]
-    geoms = [(g, b, o) for g in geoms for b in bpcs for o in orders]
+    claims = [tuple(int(v) for v in c.split(",")) for c in args.claims.split(";")]
+    geoms = [(g, b, o, c) for g in geoms for b in bpcs for o in orders for c in claims]
     times = {g: [] for g in geoms}
     for r in range(args.rounds):
-        for g, b, o in geoms:
+        for g, b, o, c in geoms:
             eng.set_geometry(*g) if g[0] else eng.set_geometry(0)
             eng.set_launch(b)
             eng.set_order(*o)
+            eng.set_tuning(X.TUNE_CLAIM, *c)
             for k in range(3):
                 eng.batch_device(bufs[k % len(bufs)], d_desc, count, out, mode, flags,
                                  len_hint, stream=s.cuda_stream)
@@ -75,12 +82,12 @@ def main():
                                  len_hint, stream=s.cuda_stream)
                 evs[k][1].record(s)
             torch.cuda.synchronize()
-            times[(g, b, o)] += [e0.elapsed_time(e1) for e0, e1 in evs]
-    for g, b, o in geoms:
-        t = np.array(times[(g, b, o)])
+            times[(g, b, o, c)] += [e0.elapsed_time(e1) for e0, e1 in evs]
+    for g, b, o, c in geoms:
+        t = np.array(times[(g, b, o, c)])
         print(json.dumps({"config": args.config, "payload": [cfg["pmin"], cfg["pmax"]],
                           "layout": args.layout, "flags": args.flags,
-                          "geometry": g, "bpc": b,
+                          "geometry": g, "bpc": b, "claim": c,
                           "order": o, "median_ms": round(float(
             np.median(t)), 4), "min_ms": round(float(t.min()), 4), "GBps_median": round(
             alg / (np.median(t) * 1e-3) / 1e9, 1), "GBps_best": round(alg / (t.min() * 1e-3) / 1e9,

@@ -63,6 +63,8 @@ def main():
     ap.add_argument("--work", nargs="+", default=["c2", "c5", "c5s0/8", "c5s7/8"])
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--warm", type=int, default=40)
+    ap.add_argument("--claim", default="64,0",
+                    help="XCSUM_TUNE_CLAIM static share in 64ths, wave steps per claim")
     args = ap.parse_args()
     import torch
     L = X.lib()
@@ -74,6 +76,7 @@ def main():
     dev = torch.device("cuda:0")
     torch.cuda.set_device(dev)
     eng = X.Engine(0)
+    eng.set_tuning(X.TUNE_CLAIM, *[int(v) for v in args.claim.split(",")])
     s = torch.cuda.current_stream(dev)
     for w in args.work:
         cid, shard = parse_work(w)
@@ -103,7 +106,7 @@ def main():
             rows.append(st)
         med = {k: float(np.median([r_[k] for r_ in rows])) for k in rows[0]}
         frames_per_wave = count / med["waves"]
-        print(json.dumps({"work": w, "frames": count, "frames_per_wave": round(frames_per_wave, 1),
+        print(json.dumps({"work": w, "claim": args.claim, "frames": count, "frames_per_wave": round(frames_per_wave, 1),
                           "median": med, "reps": rows}), flush=True)
         del bufs, d_desc, out
         torch.cuda.empty_cache()
