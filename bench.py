@@ -478,7 +478,7 @@ def pmc_traffic(cid, layout, flags, sha):
     traffic is null and the reason says which code the counters came from.
     Returns (bytes, source, reason, kernel hash)."""
     tag = f"{'_umem' if layout == 'umem' else ''}{'_f%x' % flags if flags else ''}"
-    for rnd in ("r05", "r04", "r03", "r02", "r01", ""):
+    for rnd in ("r06", "r05", "r04", "r03", "r02", "r01", ""):
         path = os.path.join(ROOT, "profiles", rnd, f"pmc_config{cid}{tag}.json")
         if not os.path.exists(path):
             continue
