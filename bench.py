@@ -281,10 +281,19 @@ def launch_ranks(world, argv, grace_s=30.0, script=None):
     port = free_port()
     script = script or os.path.abspath(__file__)
     procs = []
-    for r in range(world):
-        procs.append(subprocess.Popen([sys.executable, "-u", script, *argv],
-                                      env=rank_env(os.environ, r, world, port),
-                                      stdout=None if r == 0 else sys.stderr.fileno()))
+    try:
+        for r in range(world):
+            procs.append(subprocess.Popen([sys.executable, "-u", script, *argv],
+                                          env=rank_env(os.environ, r, world, port),
+                                          stdout=None if r == 0 else sys.stderr.fileno()))
+    except OSError as e:
+        # the ranks already started would wait for the missing one at the
+        # rendezvous: end them
+        print(f"bench: could not start rank {len(procs)}: {e}", file=sys.stderr)
+        for p in procs:
+            p.kill()
+            p.wait()
+        return 1
 
     def forward(sig, _frame):
         for p in procs:

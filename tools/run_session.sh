@@ -223,6 +223,10 @@ PY
     # the claimed-tail A/B kernels live in the variant builds only
     XCSUM_LIB=$PWD/libxudp_amd/variants/sweep/libxcsum.so tools/gpu_run.sh $t/pytest_claim 600 \
       $P tests/test_gpu_claim.py || exit $? ;;
+  scan)
+    # config 5 strong scaling projected from every shard of N = 1, 2, 4, 8
+    # timed alone on this GPU (tools/shard_scan.py)
+    tools/gpu_run.sh $t/shard_scan 600 python -u tools/shard_scan.py || exit $? ;;
   slots)
     # xudp's 4096-byte slots with the like-for-like span probe
     tools/gpu_run.sh $t/bench_c2u 300 python -u bench.py --steps 100 --warmup 5 \
