@@ -1211,6 +1211,18 @@ def main():
             roof["traffic_kernel_sha16"] = ksha   # the counted kernel's code, this build
         if why:
             roof["traffic_note"] = why
+        if traffic is not None and cfg["shard"] and (world > 1 or shard is not None):
+            # the counters were taken on the whole 8M-frame job; this line's
+            # launches are shards of it: no per-launch bytes to report, only
+            # the whole job's ratio to its algorithmic bytes
+            try:
+                j = json.load(open(os.path.join(ROOT, traffic_src)))
+                roof["traffic_over_alg_whole_job"] = j.get("traffic_over_alg")
+            except (OSError, ValueError):
+                pass
+            roof["traffic"] = None
+            roof["traffic_note"] = (f"counters in {traffic_src} were taken on the whole "
+                                    f"{cfg['n']}-frame job, this line's launches are shards")
         # bytes the kernel must move per launch (every 64-byte line holding a
         # frame byte, once, + 16-byte descriptors + 2-byte results): the
         # apples-to-apples numerator for the stream-read ceiling
