@@ -813,3 +813,57 @@ extern "C" int probe_frame_spans2(const void *umem, const void *desc, uint32_t n
 #undef L
 	return hipGetLastError() == hipSuccess ? 0 : -1;
 }
+
+/* Wave-contiguous read (round 6): each wave streams its own contiguous
+ * region of `region` bytes, 1 KiB per load instruction (64 lanes x 16 B),
+ * UNROLL instructions in flight -- the other way to cut a stream read than
+ * stream_read's grid stride, to see whether the same-run ceiling is the
+ * read rate of the chip or of that one pattern. */
+template <bool NT, int UNROLL>
+__global__ void __launch_bounds__(256) wave_region_read(const u32x4 *p, uint64_t n16,
+							uint64_t region16, uint32_t *out)
+{
+	const uint64_t lane = threadIdx.x & 63u;
+	const uint64_t wave = ((uint64_t)blockIdx.x * 256u + threadIdx.x) >> 6;
+	const uint64_t nwaves = (uint64_t)gridDim.x * 4u;
+	uint32_t acc = 0;
+	for (uint64_t r0 = wave * region16; r0 < n16; r0 += nwaves * region16) {
+		const uint64_t r1 = r0 + region16 < n16 ? r0 + region16 : n16;
+		uint64_t i = r0 + lane;
+		for (; i + 64u * (UNROLL - 1) < r1; i += 64u * UNROLL) {
+			u32x4 v[UNROLL];
+#pragma unroll
+			for (int u = 0; u < UNROLL; u++)
+				v[u] = NT ? __builtin_nontemporal_load((gu32x4 *)(p + i + 64u * u))
+					  : *((gu32x4 *)(p + i + 64u * u));
+#pragma unroll
+			for (int u = 0; u < UNROLL; u++)
+				acc += v[u].x ^ v[u].y ^ v[u].z ^ v[u].w;
+		}
+		for (; i < r1; i += 64u) {
+			const u32x4 v = *((gu32x4 *)(p + i));
+			acc += v.x ^ v.y ^ v.z ^ v.w;
+		}
+	}
+	if (acc == 0x9e3779b9u)
+		out[blockIdx.x] = acc;
+}
+
+extern "C" int probe_wave_region_read(const void *p, uint64_t nbytes, uint64_t region,
+				      int blocks, int nt, int unroll, uint32_t *out, void *stream)
+{
+	if (blocks <= 0 || region < 1024 || (region & 1023))
+		return -1;
+	const uint64_t n16 = nbytes / 16, r16 = region / 16;
+	hipStream_t s = (hipStream_t)stream;
+	const u32x4 *q = (const u32x4 *)p;
+#define L(NT_, U_) hipLaunchKernelGGL((wave_region_read<NT_, U_>), dim3(blocks), dim3(256), 0, s, \
+				      q, n16, r16, out)
+	if (nt) {
+		if (unroll == 2) L(true, 2); else if (unroll == 4) L(true, 4); else if (unroll == 8) L(true, 8); else L(true, 16);
+	} else {
+		if (unroll == 2) L(false, 2); else if (unroll == 4) L(false, 4); else if (unroll == 8) L(false, 8); else L(false, 16);
+	}
+#undef L
+	return hipGetLastError() == hipSuccess ? 0 : -1;
+}
