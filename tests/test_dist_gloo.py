@@ -96,7 +96,8 @@ def test_bench_helpers_present_and_real_bytes():
     import bench
     for name in ("digest_check", "stream_ceiling", "gpu_clocks", "cpu_baseline", "pmc_traffic",
                  "host_cpu_facts", "real_bytes", "rank_slice", "build_batch", "inplace_ceiling",
-                 "lib_sha16", "parse_flags", "alg_bytes_flags", "order_ab"):
+                 "lib_sha16", "parse_flags", "alg_bytes_flags", "order_ab", "span_ceiling",
+                 "launch_plan", "launch_ranks", "parse_shard"):
         assert callable(getattr(bench, name)), name
     d = np.zeros(3, dtype=X.DESC_DTYPE)
     d["addr"] = [0, 100, 4096]
