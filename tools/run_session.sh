@@ -227,6 +227,23 @@ PY
     # config 5 strong scaling projected from every shard of N = 1, 2, 4, 8
     # timed alone on this GPU (tools/shard_scan.py)
     tools/gpu_run.sh $t/shard_scan 600 python -u tools/shard_scan.py || exit $? ;;
+  sqtail)
+    # the tail in counters: waves, their summed lifetimes
+    # (SQ_WAVE_CYCLES, quad-cycles) and the GPU's busy cycles, one pass per
+    # workload; tools/sq_summary.py summarises
+    mkdir -p gpurun_out/$t/sq
+    for w in "c2:--config 2" "c5:--config 5" "c5s7:--config 5 --shard 7/8"; do
+      n=${w%%:*}; a=${w#*:}
+      d=gpurun_out/$t/sq/$n
+      timeout -s KILL 180 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE \
+        --output-format csv -d $d -o run -- python3 bench.py $a --steps 3 --warmup 1 --no-graph \
+        --ramp-ms 0 --reps 1 --no-ceiling --no-calibrate --no-cpu-baseline --no-order-ab \
+        > $d.log 2>&1
+      rc=$?
+      echo "sq $n rc=$rc"
+      [ $rc -eq 0 ] || exit $rc
+      python3 tools/sq_summary.py $d > $d.json
+    done ;;
   slots)
     # xudp's 4096-byte slots with the like-for-like span probe
     tools/gpu_run.sh $t/bench_c2u 300 python -u bench.py --steps 100 --warmup 5 \
