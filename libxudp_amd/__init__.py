@@ -65,6 +65,8 @@ GEOMETRIES = REG_GEOMETRIES + STREAM_GEOMETRIES
 # unit, rows in flight)
 LDS_GEOMETRIES = [(16, 12, 6), (16, 13, 6), (16, 12, 3), (16, 14, 3)]
 SEG_GEOMETRIES = [(64, 64, 4), (64, 64, 8), (64, 16, 4)]
+# round 6: the same with the finished spans added into LDS words (K = 100 + D)
+SEG_ATOM_GEOMETRIES = [(g, f, 100 + d) for g, f, d in SEG_GEOMETRIES]
 
 
 # bounds-checked debug build (make -C libxudp_amd debug; BoundsSite in
@@ -105,7 +107,7 @@ def variants_built():
 
 def variant_geometries():
     """The A/B geometries the loaded library runs ([] for libxcsum.so)."""
-    return LDS_GEOMETRIES + SEG_GEOMETRIES if variants_built() else []
+    return LDS_GEOMETRIES + SEG_GEOMETRIES + SEG_ATOM_GEOMETRIES if variants_built() else []
 
 
 # xcsum_ctx_set_inplace schedules

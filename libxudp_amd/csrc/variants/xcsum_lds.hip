@@ -149,7 +149,7 @@ bool variant_supported(Geometry g)
 		return true;
 	if (g.G == 16 && ((g.U == 12 || g.U == 14) && g.K == 3))
 		return true;
-#define X(f_, d_) if (g.G == 64 && g.U == f_ && g.K == d_) return true;
+#define X(f_, d_) if (g.G == 64 && g.U == f_ && (g.K == d_ || g.K == 100 + d_)) return true;
 	XCSUM_SEG_GEOMETRIES(X)
 #undef X
 	return false;

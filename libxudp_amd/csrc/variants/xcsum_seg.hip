@@ -89,9 +89,14 @@ static __device__ __forceinline__ u32x4 keep_bytes(u32x4 v, int lo, int hi)
 
 } /* namespace */
 
-template <int D, int F>
+/* ATOM (round 6): a finished span's per-lane sums go to the frame's word in
+ * LDS by one ds_add per lane instead of a wave reduction (DPP + permlane
+ * swaps) -- no dependency chain per frame; the unit's words are read back
+ * once by their lanes */
+template <int D, int F, bool ATOM>
 __global__ void __launch_bounds__(256) csum_seg_kernel(CsumArgs a)
 {
+	__shared__ uint32_t lds_acc[ATOM ? 4 : 1][ATOM ? F : 1];
 	if (!dense_batch(a)) {
 		/* sparse batch: the frame-group kernel, region order as usual
 		 * (K = 2: its registers set this kernel's occupancy; frames over
@@ -104,6 +109,7 @@ __global__ void __launch_bounds__(256) csum_seg_kernel(CsumArgs a)
 	const uint32_t nunits = (uint32_t)(((uint64_t)a.n + F - 1) / F);
 	const uint8_t *zero = (const uint8_t *)g_zero_chunk;
 	const uint32_t w0 = __builtin_amdgcn_readfirstlane(blockIdx.x * 4u + (threadIdx.x >> 6));
+	const uint32_t wv = ATOM ? threadIdx.x >> 6 : 0u;
 
 	/* scalar (wave-uniform) bounds of unit u from two descriptors */
 	auto bounds_of = [&](uint32_t u) __attribute__((always_inline)) {
@@ -156,6 +162,8 @@ __global__ void __launch_bounds__(256) csum_seg_kernel(CsumArgs a)
 			return;
 		/* frames never reached by a row (no span in the region) flush 0 */
 		const uint32_t p = F * cu + lane;
+		if (ATOM && lane < (uint32_t)F)
+			acc = lds_acc[wv][lane];
 		if (f.mode != -2)
 			finalize<2>(a, f, p, acc);
 	};
@@ -199,6 +207,8 @@ __global__ void __launch_bounds__(256) csum_seg_kernel(CsumArgs a)
 		s_rel = (uint32_t)(s64 < 0 ? 0 : s64);
 		h_rel = (uint32_t)(h64 < 0 ? 0 : h64);
 		acc = 0;
+		if (ATOM && lane < (uint32_t)F)
+			lds_acc[wv][lane] = 0u;
 		E = 0;
 		O = 0;
 		cf = 0;
@@ -235,8 +245,13 @@ __global__ void __launch_bounds__(256) csum_seg_kernel(CsumArgs a)
 	/* frame cf's span is complete: its lane takes the wave's total */
 	auto flush = [&]() __attribute__((always_inline)) {
 		uint32_t s = oddc ? (O << 8) + E : (E << 8) + O;
-		s = seg_sum<64>(s);
-		acc = lane == cf ? s : acc;
+		if (ATOM) {
+			if (s)
+				atomicAdd(&lds_acc[wv][cf], s);
+		} else {
+			s = seg_sum<64>(s);
+			acc = lane == cf ? s : acc;
+		}
 		E = 0;
 		O = 0;
 		cf++;
@@ -295,13 +310,13 @@ __global__ void __launch_bounds__(256) csum_seg_kernel(CsumArgs a)
 	}
 }
 
-template <int D, int F>
+template <int D, int F, bool ATOM>
 static hipError_t launch_seg_t(const CsumArgs &a, int cus, int bpc, hipStream_t s)
 {
 	static std::atomic<int> occ_cache[OCC_MAX_DEVICES];
 	const int occ = occupancy_cached(occ_cache, [] {
 		int nb = 0;
-		if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, csum_seg_kernel<D, F>, 256, 0) !=
+		if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, csum_seg_kernel<D, F, ATOM>, 256, 0) !=
 			    hipSuccess || nb <= 0)
 			nb = 1;
 		return nb;
@@ -316,7 +331,7 @@ static hipError_t launch_seg_t(const CsumArgs &a, int cus, int bpc, hipStream_t 
 	if (blocks == 0)
 		blocks = 1;
 	(void)hipGetLastError();
-	hipLaunchKernelGGL((csum_seg_kernel<D, F>), dim3((unsigned)blocks), dim3(256), 0, s, a);
+	hipLaunchKernelGGL((csum_seg_kernel<D, F, ATOM>), dim3((unsigned)blocks), dim3(256), 0, s, a);
 	return hipGetLastError();
 }
 
@@ -325,7 +340,8 @@ static hipError_t launch_seg_t(const CsumArgs &a, int cus, int bpc, hipStream_t 
 hipError_t launch_seg(const CsumArgs &a, int F, int D, int cus, int bpc, hipStream_t s)
 {
 #define XCSUM_SEG(f_, d_) \
-	if (F == f_ && D == d_) return launch_seg_t<d_, f_>(a, cus, bpc, s);
+	if (F == f_ && D == d_) return launch_seg_t<d_, f_, false>(a, cus, bpc, s); \
+	if (F == f_ && D == 100 + d_) return launch_seg_t<d_, f_, true>(a, cus, bpc, s);
 	XCSUM_SEG_GEOMETRIES(XCSUM_SEG)
 #undef XCSUM_SEG
 	return hipErrorInvalidValue;

@@ -7,8 +7,9 @@
  * (variant_supported / launch_variant), which are null there.
  *   - csum_lds_kernel<K, D>: chunks moved by LDS-DMA into a D-deep ring,
  *     Geometry{16, 10 + D, K};
- *   - csum_seg_kernel<D, F>: segmented stream for packed mixed sizes,
- *     Geometry{64, F, D}. */
+ *   - csum_seg_kernel<D, F, ATOM>: segmented stream for packed mixed sizes,
+ *     Geometry{64, F, D}; Geometry{64, F, 100 + D}: the round-6 form whose
+ *     finished spans go to LDS words by ds_add instead of a wave reduction. */
 #ifndef XCSUM_VARIANTS_H
 #define XCSUM_VARIANTS_H
 

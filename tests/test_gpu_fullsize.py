@@ -183,7 +183,7 @@ def test_config5_every_jumbo_geometry_same_digest(torch_cuda, engine, digests):
     the segmented stream at every D): the reference's digest each time;
     then INPLACE and a VERIFY pass over the written frames."""
     cfg, desc, d_desc, d_umem = device_batch(torch_cuda, engine, 5)
-    for g in (X.SEG_GEOMETRIES if X.variants_built() else []) + [(64, 1, 9)]:
+    for g in (X.SEG_GEOMETRIES + X.SEG_ATOM_GEOMETRIES if X.variants_built() else []) + [(64, 1, 9)]:
         engine.set_geometry(*g)
         try:
             got = run(torch_cuda, engine, d_umem, d_desc, len(desc), cfg["mode"])

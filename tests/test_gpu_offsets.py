@@ -14,7 +14,7 @@ import oracle
 pytestmark = pytest.mark.gpu
 
 OFFSETS = [(1 << 31) - 5000, (1 << 32) - 3000]
-GEOMS = [None, (16, 2, 6), (64, 1, 9), (4, 1, 2)] + X.STREAM_GEOMETRIES[1:2] + (X.SEG_GEOMETRIES if X.variants_built() else [])
+GEOMS = [None, (16, 2, 6), (64, 1, 9), (4, 1, 2)] + X.STREAM_GEOMETRIES[1:2] + (X.SEG_GEOMETRIES + X.SEG_ATOM_GEOMETRIES if X.variants_built() else [])
 
 
 @pytest.fixture(scope="module")

@@ -25,7 +25,7 @@ def mixed(n, family, seed, align=8):
     return X.gen_frames_host(n, family, 0, 9000, seed=seed, align=align)
 
 
-@pytest.mark.parametrize("geom", X.SEG_GEOMETRIES)
+@pytest.mark.parametrize("geom", X.SEG_GEOMETRIES + X.SEG_ATOM_GEOMETRIES)
 @pytest.mark.parametrize("family", [4, 6])
 @pytest.mark.parametrize("align", [1, 8])
 def test_seg_mixed_vs_oracle(torch_cuda, engine, geom, family, align):
@@ -37,7 +37,7 @@ def test_seg_mixed_vs_oracle(torch_cuda, engine, geom, family, align):
             assert np.array_equal(got, oracle.batch(umem, desc, m)), m
 
 
-@pytest.mark.parametrize("geom", X.SEG_GEOMETRIES)
+@pytest.mark.parametrize("geom", X.SEG_GEOMETRIES + X.SEG_ATOM_GEOMETRIES)
 def test_seg_flags_vs_oracle(torch_cuda, engine, geom):
     """INPLACE | IPHDR writes the same bytes as the default kernel; VERIFY
     after it passes; one flipped byte per frame fails."""
@@ -63,7 +63,7 @@ def test_seg_flags_vs_oracle(torch_cuda, engine, geom):
         assert (got != 0).all()
 
 
-@pytest.mark.parametrize("geom", X.SEG_GEOMETRIES)
+@pytest.mark.parametrize("geom", X.SEG_GEOMETRIES + X.SEG_ATOM_GEOMETRIES)
 def test_seg_unsorted_and_overlapping_units(torch_cuda, engine, geom):
     """Units whose spans are out of order or overlap are walked: same output."""
     umem, desc = mixed(64 * 6 + 5, 4, seed=9)
@@ -81,7 +81,7 @@ def test_seg_unsorted_and_overlapping_units(torch_cuda, engine, geom):
         assert np.array_equal(got, oracle.batch(umem, desc, X.MODE_V4_RFC, X.F_VERIFY))
 
 
-@pytest.mark.parametrize("geom", X.SEG_GEOMETRIES)
+@pytest.mark.parametrize("geom", X.SEG_GEOMETRIES + X.SEG_ATOM_GEOMETRIES)
 def test_seg_region_over_cap_and_malformed(torch_cuda, engine, geom):
     """A 9 MiB hole inside one unit (its region is over the cap: walked), and
     malformed frames (too short, UDP length over 65535) in streamed units."""
@@ -102,7 +102,7 @@ def test_seg_region_over_cap_and_malformed(torch_cuda, engine, geom):
         assert engine.take_errors() == 2
 
 
-@pytest.mark.parametrize("geom", X.SEG_GEOMETRIES)
+@pytest.mark.parametrize("geom", X.SEG_GEOMETRIES + X.SEG_ATOM_GEOMETRIES)
 def test_seg_sparse_batch_fallback(torch_cuda, engine, geom):
     """xudp's 4096-byte chunks (sparse): the frame-group fallback, frames up
     to 3 KB (over its 2 KiB preload: its walk)."""
@@ -112,7 +112,7 @@ def test_seg_sparse_batch_fallback(torch_cuda, engine, geom):
     assert np.array_equal(got, oracle.batch(umem, desc, X.MODE_V4_LEGACY))
 
 
-@pytest.mark.parametrize("geom", X.SEG_GEOMETRIES)
+@pytest.mark.parametrize("geom", X.SEG_GEOMETRIES + X.SEG_ATOM_GEOMETRIES)
 @pytest.mark.parametrize("n", [1, 2, 63, 64, 65, 130])
 def test_seg_small_batches(torch_cuda, engine, geom, n):
     umem, desc = mixed(n, 6, seed=n)
