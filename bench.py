@@ -280,12 +280,22 @@ def launch_ranks(world, argv, grace_s=30.0, script=None):
     import subprocess
     port = free_port()
     script = script or os.path.abspath(__file__)
+
+    def die_with_parent():
+        # in the child, before it runs anything: a parent killed outright
+        # (SIGKILL from a time limit) takes its ranks with it
+        try:
+            import ctypes
+            ctypes.CDLL(None).prctl(1, signal.SIGKILL)   # PR_SET_PDEATHSIG
+        except (OSError, AttributeError):
+            pass
     procs = []
     try:
         for r in range(world):
             procs.append(subprocess.Popen([sys.executable, "-u", script, *argv],
                                           env=rank_env(os.environ, r, world, port),
-                                          stdout=None if r == 0 else sys.stderr.fileno()))
+                                          stdout=None if r == 0 else sys.stderr.fileno(),
+                                          preexec_fn=die_with_parent))
     except OSError as e:
         # the ranks already started would wait for the missing one at the
         # rendezvous: end them

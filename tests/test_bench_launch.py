@@ -126,3 +126,29 @@ def test_shard_digests_tile_the_job():
     for w in (2, 4, 8):
         hs = d[f"sha256_out_shards{w}"]
         assert len(hs) == w and len(set(hs)) == w and all(len(h) == 64 for h in hs)
+
+
+def test_ranks_die_with_a_killed_launcher(tmp_path):
+    """A launcher killed outright (SIGKILL, as a time limit does) takes its
+    rank processes with it (PR_SET_PDEATHSIG): none is left holding a GPU."""
+    import signal
+    import time
+    script = tmp_path / "rank.py"
+    script.write_text("import os, time\nprint(os.getpid(), flush=True)\ntime.sleep(120)\n")
+    code = (f"import sys; sys.path.insert(0, {ROOT!r}); import bench; "
+            f"sys.exit(bench.launch_ranks(2, [], script={str(script)!r}))")
+    p = subprocess.Popen([sys.executable, "-c", code], stdout=subprocess.PIPE,
+                         stderr=subprocess.PIPE, text=True)
+    pid0 = int(p.stdout.readline())           # rank 0 is up
+    time.sleep(0.5)
+    p.send_signal(signal.SIGKILL)
+    p.wait(timeout=30)
+    for _ in range(100):
+        try:
+            os.kill(pid0, 0)
+        except ProcessLookupError:
+            break
+        time.sleep(0.1)
+    else:
+        os.kill(pid0, signal.SIGKILL)
+        pytest.fail("rank 0 outlived its killed launcher")
