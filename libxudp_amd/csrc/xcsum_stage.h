@@ -158,8 +158,11 @@ private:
 	{
 		while (nth_ < want && nth_ < STAGE_THREADS - 1) {
 			const int id = nth_;
+			/* the generation before the job this call posts: only run(),
+			 * on the calling thread, moves gen_ */
+			const uint64_t g0 = gen_;
 			try {
-				th_[id] = std::thread([this, id] { worker(id); });
+				th_[id] = std::thread([this, id, g0] { worker(id, g0); });
 			} catch (...) {
 				return;
 			}
@@ -167,9 +170,8 @@ private:
 		}
 	}
 
-	void worker(int id)
+	void worker(int id, uint64_t seen)
 	{
-		uint64_t seen = 0;
 		std::unique_lock<std::mutex> l(mu_);
 		for (;;) {
 			cv_work_.wait(l, [&] { return quit_ || gen_ != seen; });

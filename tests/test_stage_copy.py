@@ -36,6 +36,22 @@ int main(int argc, char **argv) {
            xcsum::stage_threads(64u << 20, 1));
     return 0;
   }
+  if (argc == 2 && !strcmp(argv[1], "grow")) {
+    /* the pool grows between calls (2 parts, then 4, then 3 ...): every part
+     * of every call runs exactly once, on a worker or the caller */
+    xcsum::StagePool pool;
+    const int ks[] = {2, 4, 3, 1, 4, 2};
+    for (int rep = 0; rep < 2000; rep++) {
+      const int k = ks[rep % 6];
+      int hits[xcsum::STAGE_THREADS] = {0};
+      pool.run(k, [&](int t) { hits[t]++; });
+      for (int t = 0; t < xcsum::STAGE_THREADS; t++)
+        if (hits[t] != (t < k)) { printf("rep %d k %d part %d ran %d times\n", rep, k, t, hits[t]); return 1; }
+      if (rep == 0 && pool.threads() != 1) { printf("threads %d after k=2\n", pool.threads()); return 1; }
+    }
+    printf("ok pool=%d\n", pool.threads());
+    return 0;
+  }
   xcsum::StagePool pool;
   const uint32_t n = (uint32_t)atoi(argv[1]);
   const uint32_t cap = (uint32_t)strtoul(argv[2], 0, 10);
@@ -163,4 +179,20 @@ def test_gather_threads_tsan_clean():
         pytest.skip("no ThreadSanitizer runtime for g++ here")
     r = subprocess.run([exe, "70000", "42", "1514", "11"], capture_output=True, text=True,
                        timeout=300, env=dict(os.environ, TSAN_OPTIONS="halt_on_error=1"))
+    assert r.returncode == 0 and "ThreadSanitizer" not in r.stderr, r.stderr[-3000:]
+
+
+def test_pool_grows_between_calls(driver):
+    """A pool started by a 2-part call grows on a 4-part one; the new workers
+    take only the job posted after they start, every part runs once."""
+    r = subprocess.run([driver, "grow"], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0 and r.stdout.split() == ["ok", "pool=3"], r.stdout + r.stderr
+
+
+def test_pool_growth_tsan_clean():
+    exe = build(tsan=True)
+    if exe is None:
+        pytest.skip("no ThreadSanitizer runtime for g++ here")
+    r = subprocess.run([exe, "grow"], capture_output=True, text=True, timeout=300,
+                       env=dict(os.environ, TSAN_OPTIONS="halt_on_error=1"))
     assert r.returncode == 0 and "ThreadSanitizer" not in r.stderr, r.stderr[-3000:]
